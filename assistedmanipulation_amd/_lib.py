@@ -1,0 +1,78 @@
+"""Loader for the in-tree engine library (assistedmanipulation_amd/lib/libmppi_amd.so).
+
+There is no fallback: if the library is missing the import fails with the build command.
+The library is loaded before anything imports torch so that its ROCm runtime (/opt/rocm,
+RUNPATH) is the one both share (same sonames, first loaded wins).
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmppi_amd.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "mppi_amd.h")
+
+_dp = C.POINTER(C.c_double)
+_h = C.c_void_p
+_i64p = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); every function include/mppi_amd.h declares
+PROTOTYPES = {
+    "mppi_abi_version": (C.c_int, []),
+    "mppi_build_info": (C.c_char_p, []),
+    "mppi_default_frankaridgeback": (None, [C.POINTER(abi.mppi_frankaridgeback_desc)]),
+    "mppi_default_assisted_manipulation": (None, [C.POINTER(abi.mppi_assisted_manipulation_desc)]),
+    "mppi_create": (C.c_int, [C.POINTER(abi.mppi_config), C.POINTER(abi.mppi_dynamics_desc),
+                              C.POINTER(abi.mppi_cost_desc), C.c_int, C.POINTER(_h)]),
+    "mppi_destroy": (None, [_h]),
+    "mppi_last_error": (C.c_char_p, [_h]),
+    "mppi_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, _i64p, _i64p]),
+    "mppi_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "mppi_comm_init": (C.c_int, [_h, C.c_int, C.c_int, C.c_char_p]),
+    "mppi_set_shard": (C.c_int, [_h, C.c_int, C.c_int]),
+    "mppi_set_noise_source": (C.c_int, [_h, C.c_int, C.c_uint64]),
+    "mppi_inject_noise": (C.c_int, [_h, _dp, C.c_int64]),
+    "mppi_noise_draws": (C.c_int, [_h, C.c_double, _i64p]),
+    "mppi_set_index_semantics": (C.c_int, [_h, C.c_int]),
+    "mppi_set_forecast": (C.c_int, [_h, _dp]),
+    "mppi_update": (C.c_int, [_h, _dp, C.c_double]),
+    "mppi_update_phase1": (C.c_int, [_h, _dp, C.c_double]),
+    "mppi_update_phase2": (C.c_int, [_h]),
+    "mppi_update_phase3": (C.c_int, [_h]),
+    "mppi_device_costs": (C.c_void_p, [_h]),
+    "mppi_device_gradient": (C.c_void_p, [_h]),
+    "mppi_stream": (C.c_void_p, [_h]),
+    "mppi_get": (C.c_int, [_h, C.c_double, _dp]),
+    "mppi_costs": (C.c_int, [_h, _dp]),
+    "mppi_weights": (C.c_int, [_h, _dp]),
+    "mppi_gradient": (C.c_int, [_h, _dp]),
+    "mppi_optimal_control": (C.c_int, [_h, _dp]),
+    "mppi_optimal_cost": (C.c_int, [_h, _dp]),
+    "mppi_argmin": (C.c_int, [_h, _i64p]),
+    "mppi_update_duration": (C.c_int, [_h, _dp]),
+    "mppi_noise": (C.c_int, [_h, _dp]),
+    "mppi_dims": (C.c_int, [_h, _i64p, _i64p, _i64p, _i64p]),
+    "mppi_smoothing_windows": (C.c_int, [_h, _dp, _dp, _i64p]),
+    "mppi_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float)]),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "assistedmanipulation_amd: engine library %s is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+            "assistedmanipulation_amd/csrc`" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in PROTOTYPES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L

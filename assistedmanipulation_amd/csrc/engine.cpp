@@ -1,0 +1,960 @@
+// engine.cpp — host runtime of the MI355X MPPI engine: the C-ABI of include/mppi_amd.h.
+//
+// Replaces mppi::Trajectory (reference src/controller/mppi.{hpp,cpp}).  The host keeps the
+// reference's scalar bookkeeping (shift count, times, counters, the published U* for get());
+// every per-rollout array lives in HBM and is produced by the kernels of kernels.hip.
+// One handle = one HIP device + one stream (+ one RCCL communicator when sharded).
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+// Host arithmetic mirrors the reference's double expressions exactly (shift counts, step
+// constants): no FMA contraction.
+#pragma clang fp contract(off)
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mppi_amd.h"
+#include "../../include/mppi_amd_frankaridgeback.h"
+#include "engine_types.hpp"
+#include "kernels.hpp"
+
+using namespace mppi_eng;
+
+namespace {
+
+std::string g_last_error;
+
+struct DeviceBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct mppi_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    float kernel_ms[5] = {0, 0, 0, 0, 0};
+    int dyn_kind = 0, cost_kind = 0;
+    int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
+    double dt = 0, gradient_step = 0, cost_scale = 0, gamma = 1;
+    int control_bound = 0;
+    std::vector<double> cmin, cmax, cdefault, init_state, T;
+    bool has_default = false, tdiag = false;
+    int sg_window = 0, sg_order = 0;
+    // sharding
+    int world = 1, rank = 0;
+    int64_t begin = 0, count = 0, Rpad = 0;
+    ncclComm_t comm = nullptr;
+    bool updated_once = false;
+    // reference scalar state (mppi.hpp:545-657)
+    double last_shift_time = 0, rollout_time = 0, last_rollout_time = 0, update_last = 0, update_duration = 0;
+    uint64_t update_count = 0;
+    int64_t shift_by = 0, shifted = 0;
+    int compat_uint8 = 0;
+    int noise_source = MPPI_NOISE_DEVICE_PHILOX;
+    uint64_t seed = 0x5EEDull;
+    std::vector<double> inj_pending;
+    // published (host) — guarded by mtx for get() concurrent with update()
+    std::mutex mtx;
+    std::vector<double> U_host;
+    double opt_cost = 0;
+    // forecast / per-step constants
+    std::vector<double> forecast;   // H x 6
+    mppi_assisted_manipulation_desc am{};
+    mppi_quadratic_cost_desc quad{};
+    double pm_mass = 1.0;
+    // device buffers
+    DevModel *d_model = nullptr;
+    DevCost *d_cost = nullptr;
+    DevPointMass *d_pm = nullptr;
+    StepConst *d_steps = nullptr;
+    double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_weights = nullptr;
+    double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
+    double *d_cmin = nullptr, *d_cmax = nullptr;
+    size_t inj_capacity = 0;   // doubles
+    int *d_rank = nullptr;
+    Status *d_status = nullptr;
+    double *d_sg_w = nullptr, *d_sg_uu = nullptr, *d_sg_tt = nullptr, *d_sg_last = nullptr;
+    int64_t *d_sg_start = nullptr;
+    double *h_out = nullptr;     // pinned [HC + 8]
+    double *h_stage = nullptr;   // pinned staging for the state
+    std::vector<void *> allocations;
+    std::string err;
+    // per-update phase state
+    bool phase_open = false;
+    std::chrono::steady_clock::time_point t_start;
+    double phase_time = 0;
+};
+
+namespace {
+
+mppi_status fail(mppi_handle *h, mppi_status st, const std::string &msg)
+{
+    if (h) h->err = msg;
+    else g_last_error = msg;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                                          \
+    do {                                                                                                       \
+        hipError_t e_ = (expr);                                                                                \
+        if (e_ != hipSuccess) return fail(h, MPPI_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                                              \
+    do {                                                                                                            \
+        ncclResult_t r_ = (expr);                                                                                   \
+        if (r_ != ncclSuccess) return fail(h, MPPI_ERR_COMM, std::string(#expr ": ") + ncclGetErrorString(r_));    \
+    } while (0)
+
+template <class T>
+hipError_t dalloc(mppi_handle *h, T **p, size_t n)
+{
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) return e;
+    h->allocations.push_back(q);
+    *p = (T *)q;
+    return hipMemset(q, 0, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+// Gaussian::set_covariance (gaussian.hpp:48-55): T = V sqrt(L); any T with T T^T = Sigma gives
+// the same distribution (parity runs inject eps).  Diagonal Sigma -> T = diag(sqrt).
+void noise_transform(int n, const double *cov_colmajor, std::vector<double> &T, bool &diag)
+{
+    diag = true;
+    for (int c = 0; c < n; c++)
+        for (int r = 0; r < n; r++)
+            if (r != c && cov_colmajor[(size_t)c * n + r] != 0.0) diag = false;
+    T.assign((size_t)n * n, 0.0);
+    if (diag) {
+        for (int i = 0; i < n; i++) T[(size_t)i * n + i] = std::sqrt(std::max(0.0, cov_colmajor[(size_t)i * n + i]));
+        return;
+    }
+    std::vector<double> A((size_t)n * n), V((size_t)n * n, 0.0);
+    for (int c = 0; c < n; c++)
+        for (int r = 0; r < n; r++) A[(size_t)r * n + c] = 0.5 * (cov_colmajor[(size_t)c * n + r] + cov_colmajor[(size_t)r * n + c]);
+    for (int i = 0; i < n; i++) V[(size_t)i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; sweep++) {   // cyclic Jacobi
+        double off = 0;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) off += A[(size_t)p * n + q] * A[(size_t)p * n + q];
+        if (off < 1e-30) break;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = A[(size_t)p * n + q];
+                if (std::fabs(apq) < 1e-300) continue;
+                const double theta = (A[(size_t)q * n + q] - A[(size_t)p * n + p]) / (2 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
+                const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; k++) {
+                    const double akp = A[(size_t)k * n + p], akq = A[(size_t)k * n + q];
+                    A[(size_t)k * n + p] = c * akp - s * akq;
+                    A[(size_t)k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double apk = A[(size_t)p * n + k], aqk = A[(size_t)q * n + k];
+                    A[(size_t)p * n + k] = c * apk - s * aqk;
+                    A[(size_t)q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double vkp = V[(size_t)k * n + p], vkq = V[(size_t)k * n + q];
+                    V[(size_t)k * n + p] = c * vkp - s * vkq;
+                    V[(size_t)k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int j = 0; j < n; j++) {
+        const double l = std::sqrt(std::max(0.0, A[(size_t)j * n + j]));
+        for (int i = 0; i < n; i++) T[(size_t)i * n + j] = V[(size_t)i * n + j] * l;
+    }
+}
+
+// --- Savitzky-Golay weights (gram_savitzky_golay.cpp: GramPoly / GenFact / Weight) ----------
+double gram_poly(int i, int m, int k, int s)
+{
+    if (k > 0)
+        return (4. * k - 2.) / (k * (2. * m - k + 1.)) * (i * gram_poly(i, m, k - 1, s) + s * gram_poly(i, m, k - 1, s - 1)) -
+               ((k - 1.) * (2. * m + k)) / (k * (2. * m - k + 1.)) * gram_poly(i, m, k - 2, s);
+    return (k == 0 && s == 0) ? 1. : 0.;
+}
+double gen_fact(int a, int b)
+{
+    double gf = 1.;
+    for (int j = (a - b) + 1; j <= a; j++) gf *= j;
+    return gf;
+}
+std::vector<double> sg_weights(int m, int n)
+{
+    std::vector<double> w(2 * (size_t)m + 1);
+    for (int i = 0; i < 2 * m + 1; ++i) {
+        double v = 0;
+        for (int k = 0; k <= n; ++k)
+            v = v + (2 * k + 1) * (gen_fact(2 * m, k) / gen_fact(2 * m + k + 1, k + 1)) * gram_poly(i - m, m, k, 0) * gram_poly(0, m, k, 0);
+        w[(size_t)i] = v;
+    }
+    return w;
+}
+
+double left_barrier_h(const mppi_barrier &b, double v)
+{
+    if (v <= b.bound) {
+        const double d = b.bound - v;
+        return b.maximum_cost + b.scale * (d * d);
+    }
+    const double x = b.scale / (v - b.bound);
+    return (b.maximum_cost < x) ? b.maximum_cost : x;
+}
+
+DevBarrier devb(const mppi_barrier &b) { return DevBarrier{b.bound, b.scale, b.maximum_cost}; }
+
+// trajectory_cost() per-step constants and pow(gamma, k) (mppi.cpp:326).
+void build_steps(const mppi_handle *h, std::vector<StepConst> &steps)
+{
+    steps.assign((size_t)h->H, StepConst{});
+    const mppi_assisted_manipulation_desc &a = h->am;
+    for (int64_t k = 0; k < h->H; k++) {
+        StepConst &s = steps[(size_t)k];
+        s.gamma_k = std::pow(h->gamma, (double)k);
+        if (h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION) continue;
+        double F[3] = {0, 0, 0};
+        if (!h->forecast.empty())
+            for (int i = 0; i < 3; i++) F[i] = h->forecast[(size_t)(6 * k + i)];
+        const double mx = a.trajectory_target_maximum;
+        for (int i = 0; i < 3; i++) {
+            double t = a.trajectory_target_scale * F[i];
+            t = (mx < t) ? mx : t;           // cwiseMin(max)
+            t = (t < -mx) ? -mx : t;         // cwiseMax(-max)
+            s.target[i] = t;
+        }
+        s.tt = (s.target[0] * s.target[0] + s.target[1] * s.target[1]) + s.target[2] * s.target[2];
+        const double distance = std::sqrt(s.tt);
+        s.active = (a.has_forecast && distance > a.trajectory_position_threshold) ? 1 : 0;
+        const mppi_quadratic &pc = a.trajectory_position_cost;
+        s.pos_cost = (pc.constant_cost + pc.linear_cost * std::fabs(distance)) + pc.quadratic_cost * distance * distance;
+        double vt = std::exp(a.trajectory_velocity_dropoff * distance) - 1;
+        vt = (vt < a.trajectory_velocity_minimum) ? a.trajectory_velocity_minimum : ((a.trajectory_velocity_maximum < vt) ? a.trajectory_velocity_maximum : vt);
+        s.vtarget = vt;
+    }
+}
+
+mppi_status upload_steps(mppi_handle *h)
+{
+    std::vector<StepConst> steps;
+    build_steps(h, steps);
+    HIP_TRY(hipMemcpyAsync(h->d_steps, steps.data(), steps.size() * sizeof(StepConst), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MPPI_OK;
+}
+
+mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
+{
+    if (d.nbodies != FR_NB) { why = "frankaridgeback model must have 12 bodies"; return MPPI_ERR_UNSUPPORTED; }
+    for (int i = 0; i < FR_NB; i++) {
+        const mppi_body &b = d.bodies[i];
+        if (b.parent != FR_PARENT[i]) { why = "body " + std::to_string(i) + " parent does not match the FrankaRidgeback topology"; return MPPI_ERR_UNSUPPORTED; }
+        const double *a = b.axis;
+        bool ok = false;
+        switch (FR_KIND[i]) {
+        case KIND_PX: ok = b.type == MPPI_JOINT_PRISMATIC && a[0] == 1 && a[1] == 0 && a[2] == 0; break;
+        case KIND_PY: ok = b.type == MPPI_JOINT_PRISMATIC && a[0] == 0 && a[1] == 1 && a[2] == 0; break;
+        case KIND_PNY: ok = b.type == MPPI_JOINT_PRISMATIC && a[0] == 0 && a[1] == -1 && a[2] == 0; break;
+        case KIND_RZ: ok = b.type == MPPI_JOINT_REVOLUTE && a[0] == 0 && a[1] == 0 && a[2] == 1; break;
+        }
+        if (!ok) { why = "body " + std::to_string(i) + " joint type/axis does not match the FrankaRidgeback topology"; return MPPI_ERR_UNSUPPORTED; }
+    }
+    if (d.end_effector.parent != FR_EE_PARENT || d.arm_mount.parent != FR_AM_PARENT) {
+        why = "end-effector / arm-mount frame parents do not match the FrankaRidgeback topology";
+        return MPPI_ERR_UNSUPPORTED;
+    }
+    return MPPI_OK;
+}
+
+mppi_status alloc_shard_buffers(mppi_handle *h)
+{
+    h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
+    HIP_TRY(dalloc(h, &h->d_noise, (size_t)(h->H * h->C * h->Rpad)));
+    return MPPI_OK;
+}
+
+int64_t keep_count(const mppi_handle *h)
+{
+    int64_t k = h->compat_uint8 ? (int64_t)(uint8_t)h->K : h->K;
+    return std::min(k, h->S);
+}
+
+int64_t draws_for(const mppi_handle *h, int64_t shift_by)
+{
+    const int64_t keep = keep_count(h);
+    int64_t d = (h->S - keep) * h->H;
+    if (shift_by > 0) d += keep * std::min<int64_t>(shift_by, h->H);
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mppi_abi_version(void) { return MPPI_AMD_ABI_VERSION; }
+
+const char *mppi_build_info(void)
+{
+    return "mppi_amd: gfx950 HIP kernels (fp64 rollout, one lane per rollout, LDS ABA stack), RCCL sharding";
+}
+
+void mppi_default_frankaridgeback(mppi_frankaridgeback_desc *out) { mppi_frankaridgeback_model(out); }
+void mppi_default_assisted_manipulation(mppi_assisted_manipulation_desc *out) { mppi_assisted_manipulation_default(out); }
+
+const char *mppi_last_error(const mppi_handle *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+
+mppi_status mppi_shard_range(int64_t rollout_count, int world, int rank, int64_t *begin, int64_t *end)
+{
+    if (world < 1 || rank < 0 || rank >= world || rollout_count < 2 * (int64_t)world || !begin || !end)
+        return MPPI_ERR_INVALID;
+    // contiguous blocks, the first (R mod world) ranks one larger (the reference's ThreadPool
+    // partition, mppi.cpp:277-302); rollouts 0 and 1 always land on rank 0.
+    const int64_t each = rollout_count / world, extra = rollout_count % world;
+    const int64_t b = (int64_t)rank * each + std::min<int64_t>(rank, extra);
+    *begin = b;
+    *end = b + each + (rank < extra ? 1 : 0);
+    return MPPI_OK;
+}
+
+mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, const mppi_cost_desc *cost, int device,
+                        mppi_handle **out)
+{
+    mppi_handle *h = nullptr;
+    if (!cfg || !dyn || !cost || !out) return fail(nullptr, MPPI_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const int64_t Cd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 3 : (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK ? FR_C : -1);
+    const int64_t Xd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 6 : FR_X;
+    const int64_t Cc = cost->kind == MPPI_COST_QUADRATIC ? 3 : (cost->kind == MPPI_COST_ASSISTED_MANIPULATION ? FR_C : -2);
+    const int64_t Xc = cost->kind == MPPI_COST_QUADRATIC ? 6 : FR_X;
+    // Trajectory::create validation, in the reference's order (mppi.cpp:17-69)
+    if (Cd < 0) return fail(nullptr, MPPI_ERR_INVALID, "unknown dynamics kind");
+    if (Cc < 0) return fail(nullptr, MPPI_ERR_INVALID, "unknown cost kind");
+    if (Cd != Cc) return fail(nullptr, MPPI_ERR_INVALID, "controller dynamics control dof " + std::to_string(Cd) + " != cost control dof " + std::to_string(Cc));
+    if (Xd != Xc) return fail(nullptr, MPPI_ERR_INVALID, "controller dynamics state dof " + std::to_string(Xd) + " != cost state dof " + std::to_string(Xc));
+    if (cfg->control_dof != Cd || !cfg->control_min || !cfg->control_max)
+        return fail(nullptr, MPPI_ERR_INVALID, "controller maximum and minimum must have length " + std::to_string(Cd));
+    if (!cfg->covariance) return fail(nullptr, MPPI_ERR_INVALID, "controller covariance matrix not square");
+    if (cfg->state_dof != Xd || !cfg->initial_state) return fail(nullptr, MPPI_ERR_INVALID, "initial state must have length " + std::to_string(Xd));
+    if (cfg->rollouts < 1) return fail(nullptr, MPPI_ERR_INVALID, "trajectory rollouts must be greater than zero");
+    if (cfg->keep_best_rollouts < 0) return fail(nullptr, MPPI_ERR_INVALID, "trajectory cached rollouts cannot be less than zero");
+    if (cfg->threads <= 0) return fail(nullptr, MPPI_ERR_INVALID, "trajectory threads must be positive nonzero");
+    if (cfg->keep_best_rollouts > cfg->rollouts)
+        return fail(nullptr, MPPI_ERR_INVALID, "keep_best_rollouts > rollouts (std::span::first out of range in the reference)");
+    if (!(cfg->time_step > 0) || !(cfg->horison > 0)) return fail(nullptr, MPPI_ERR_INVALID, "time_step and horison must be positive");
+    if (cfg->has_smoothing && (cfg->smoothing_window < 1)) return fail(nullptr, MPPI_ERR_INVALID, "smoothing window must be >= 1");
+    std::string why;
+    if (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        mppi_status st = check_topology(dyn->frankaridgeback, why);
+        if (st != MPPI_OK) return fail(nullptr, st, why);
+        if (cost->assisted_manipulation.enable_energy_limit)
+            return fail(nullptr, MPPI_ERR_UNSUPPORTED, "enable_energy_limit needs the NLE power term (SURVEY §8f item 3, not built yet)");
+    }
+
+    h = new mppi_handle();
+    h->device = device;
+    h->dyn_kind = dyn->kind;
+    h->cost_kind = cost->kind;
+    h->S = cfg->rollouts;
+    h->K = cfg->keep_best_rollouts;
+    h->R = h->S + 2;
+    h->dt = cfg->time_step;
+    h->H = (int64_t)std::ceil(cfg->horison / cfg->time_step);
+    h->C = Cd;
+    h->X = Xd;
+    h->gradient_step = cfg->gradient_step;
+    h->cost_scale = cfg->cost_scale;
+    h->gamma = cfg->cost_discount_factor;
+    h->control_bound = cfg->control_bound;
+    h->cmin.assign(cfg->control_min, cfg->control_min + Cd);
+    h->cmax.assign(cfg->control_max, cfg->control_max + Cd);
+    h->has_default = cfg->has_control_default != 0 && cfg->control_default;
+    if (h->has_default) h->cdefault.assign(cfg->control_default, cfg->control_default + Cd);
+    h->init_state.assign(cfg->initial_state, cfg->initial_state + Xd);
+    h->sg_window = cfg->has_smoothing ? (int)cfg->smoothing_window : 0;
+    h->sg_order = cfg->has_smoothing ? (int)cfg->smoothing_order : 0;
+    h->am = cost->assisted_manipulation;
+    h->quad = cost->quadratic;
+    h->pm_mass = dyn->point_mass.mass;
+    h->begin = 0;
+    h->count = h->R;
+    h->U_host.assign((size_t)(h->H * h->C), 0.0);
+    noise_transform((int)Cd, cfg->covariance, h->T, h->tdiag);
+    if (h->H < 1 || h->H > (1 << 20)) { delete h; return fail(nullptr, MPPI_ERR_INVALID, "horizon steps out of range"); }
+
+    auto cleanup_fail = [&](mppi_status st) {
+        std::string m = h->err;
+        mppi_destroy(h);
+        return fail(nullptr, st, m);
+    };
+#define CREATE_TRY(expr)                                                                                     \
+    do {                                                                                                     \
+        hipError_t e_ = (expr);                                                                              \
+        if (e_ != hipSuccess) { h->err = std::string(#expr ": ") + hipGetErrorString(e_); return cleanup_fail(MPPI_ERR_DEVICE); } \
+    } while (0)
+
+    CREATE_TRY(hipSetDevice(device));
+    CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    for (auto &e : h->ev) CREATE_TRY(hipEventCreate(&e));
+    const size_t HC = (size_t)(h->H * h->C);
+    CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
+    CREATE_TRY(dalloc(h, &h->d_U, HC));
+    CREATE_TRY(dalloc(h, &h->d_Us, HC));
+    CREATE_TRY(dalloc(h, &h->d_costs, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_weights, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_gpart, HC));
+    CREATE_TRY(dalloc(h, &h->d_grad, HC));
+    CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
+    CREATE_TRY(dalloc(h, &h->d_opt, 1));
+    CREATE_TRY(dalloc(h, &h->d_out, HC + 8));
+    CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
+    CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
+    CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_status, 1));
+    CREATE_TRY(dalloc(h, &h->d_steps, (size_t)h->H));
+    CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc((void **)&h->h_stage, 64 * sizeof(double), hipHostMallocDefault));
+    CREATE_TRY(hipMemcpy(h->d_T, h->T.data(), h->T.size() * sizeof(double), hipMemcpyHostToDevice));
+    CREATE_TRY(hipMemcpy(h->d_cmin, h->cmin.data(), (size_t)Cd * sizeof(double), hipMemcpyHostToDevice));
+    CREATE_TRY(hipMemcpy(h->d_cmax, h->cmax.data(), (size_t)Cd * sizeof(double), hipMemcpyHostToDevice));
+    CREATE_TRY(hipMemcpy(h->d_x0, h->init_state.data(), (size_t)Xd * sizeof(double), hipMemcpyHostToDevice));
+
+    if (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        DevModel m{};
+        const mppi_frankaridgeback_desc &d = dyn->frankaridgeback;
+        for (int i = 0; i < FR_NB; i++) {
+            const mppi_body &b = d.bodies[i];
+            std::memcpy(m.b[i].R, b.rotation, sizeof(m.b[i].R));
+            std::memcpy(m.b[i].p, b.translation, sizeof(m.b[i].p));
+            m.b[i].mass = b.mass;
+            std::memcpy(m.b[i].c, b.lever, sizeof(m.b[i].c));
+            std::memcpy(m.b[i].Ic, b.inertia, sizeof(m.b[i].Ic));
+        }
+        std::memcpy(m.ee_R, d.end_effector.rotation, sizeof(m.ee_R));
+        std::memcpy(m.ee_p, d.end_effector.translation, sizeof(m.ee_p));
+        std::memcpy(m.am_R, d.arm_mount.rotation, sizeof(m.am_R));
+        std::memcpy(m.am_p, d.arm_mount.translation, sizeof(m.am_p));
+        CREATE_TRY(dalloc(h, &h->d_model, 1));
+        CREATE_TRY(hipMemcpy(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
+        const mppi_assisted_manipulation_desc &a = cost->assisted_manipulation;
+        DevCost c{};
+        c.en_joint = a.enable_joint_limit;
+        c.en_self = a.enable_self_collision_limit;
+        c.en_work = a.enable_workspace_limit;
+        c.en_energy = a.enable_energy_limit;
+        c.en_vel = a.enable_velocity_cost;
+        c.en_traj = a.enable_trajectory_cost;
+        c.en_manip = a.enable_manipulability_cost;
+        for (int i = 0; i < FR_NB; i++) {
+            c.lower[i] = devb(a.lower_joint_limit[i]);
+            c.upper[i] = devb(a.upper_joint_limit[i]);
+            c.vel_q[i] = a.velocity_cost[i].quadratic_cost;
+        }
+        // self_collision_cost with get_link_position == 0 (assisted_manipulation.cpp:90-158)
+        static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8}, {4, 9}, {4, 10},
+                                         {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
+        double sc = 0.0;
+        for (auto &p : pairs) {
+            const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
+            const double radii = a.self_collision_radii[p[0] - 3] + a.self_collision_radii[p[1] - 3];
+            sc += left_barrier_h(a.self_collision_limit, distance - radii);
+        }
+        c.self_collision = sc;
+        c.ws_above = devb(a.workspace_limit_above);
+        c.ws_infront = devb(a.workspace_limit_infront);
+        c.ws_reach = devb(a.workspace_limit_reach);
+        c.yaw_c = a.workspace_cost_yaw.constant_cost;
+        c.yaw_l = a.workspace_cost_yaw.linear_cost;
+        c.yaw_q = a.workspace_cost_yaw.quadratic_cost;
+        c.manip_c = a.manipulability_cost.constant_cost;
+        c.manip_l = a.manipulability_cost.linear_cost;
+        c.manip_q = a.manipulability_cost.quadratic_cost;
+        c.traj_vel_c = a.trajectory_velocity_cost.constant_cost;
+        c.traj_vel_l = a.trajectory_velocity_cost.linear_cost;
+        c.traj_vel_q = a.trajectory_velocity_cost.quadratic_cost;
+        CREATE_TRY(dalloc(h, &h->d_cost, 1));
+        CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
+    } else {
+        DevPointMass p{};
+        p.inv_mass = 1.0 / dyn->point_mass.mass;
+        for (int i = 0; i < 3; i++) {
+            p.target[i] = cost->quadratic.target[i];
+            p.q[i] = cost->quadratic.q[i];
+            p.r[i] = cost->quadratic.r[i];
+        }
+        CREATE_TRY(dalloc(h, &h->d_pm, 1));
+        CREATE_TRY(hipMemcpy(h->d_pm, &p, sizeof(p), hipMemcpyHostToDevice));
+    }
+    if (h->sg_window > 0) {
+        const int w = h->sg_window;
+        const int64_t W = h->H + 2 * w + 1;
+        std::vector<double> sw = sg_weights(w, h->sg_order);
+        CREATE_TRY(dalloc(h, &h->d_sg_w, sw.size()));
+        CREATE_TRY(hipMemcpy(h->d_sg_w, sw.data(), sw.size() * sizeof(double), hipMemcpyHostToDevice));
+        CREATE_TRY(dalloc(h, &h->d_sg_uu, (size_t)(h->C * W)));
+        CREATE_TRY(dalloc(h, &h->d_sg_tt, (size_t)(h->C * W)));
+        std::vector<double> tt((size_t)(h->C * W), -1.0);   // MovingExtendedWindow: tt = -1, uu = 0
+        CREATE_TRY(hipMemcpy(h->d_sg_tt, tt.data(), tt.size() * sizeof(double), hipMemcpyHostToDevice));
+        CREATE_TRY(dalloc(h, &h->d_sg_start, (size_t)h->C));
+        std::vector<int64_t> st((size_t)h->C, (int64_t)w);
+        CREATE_TRY(hipMemcpy(h->d_sg_start, st.data(), st.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+        CREATE_TRY(dalloc(h, &h->d_sg_last, (size_t)h->C));
+        std::vector<double> lt((size_t)h->C, -1.0);
+        CREATE_TRY(hipMemcpy(h->d_sg_last, lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    {
+        mppi_status st = alloc_shard_buffers(h);
+        if (st != MPPI_OK) return cleanup_fail(st);
+        st = upload_steps(h);
+        if (st != MPPI_OK) return cleanup_fail(st);
+    }
+#undef CREATE_TRY
+    *out = h;
+    return MPPI_OK;
+}
+
+void mppi_destroy(mppi_handle *h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->comm) ncclCommDestroy(h->comm);
+    for (void *p : h->allocations) (void)hipFree(p);
+    if (h->h_out) (void)hipHostFree(h->h_out);
+    if (h->h_stage) (void)hipHostFree(h->h_stage);
+    for (auto &e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+mppi_status mppi_set_shard(mppi_handle *h, int world, int rank)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    if (h->updated_once) return fail(h, MPPI_ERR_INVALID, "shard must be set before the first update");
+    int64_t b, e;
+    if (mppi_shard_range(h->R, world, rank, &b, &e) != MPPI_OK) return fail(h, MPPI_ERR_INVALID, "invalid shard");
+    HIP_TRY(hipSetDevice(h->device));
+    h->world = world;
+    h->rank = rank;
+    h->begin = b;
+    h->count = e - b;
+    return alloc_shard_buffers(h);
+}
+
+mppi_status mppi_comm_unique_id(char out[128])
+{
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MPPI_ERR_COMM;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(out, &id, 128);
+    return MPPI_OK;
+}
+
+mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char unique_id[128])
+{
+    if (!h) return MPPI_ERR_INVALID;
+    mppi_status st = mppi_set_shard(h, world, rank);
+    if (st != MPPI_OK) return st;
+    if (world == 1) return MPPI_OK;
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, 128);
+    HIP_TRY(hipSetDevice(h->device));
+    NCCL_TRY(ncclCommInitRank(&h->comm, world, id, rank));
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_noise_source(mppi_handle *h, int source, uint64_t seed)
+{
+    if (!h || (source != MPPI_NOISE_DEVICE_PHILOX && source != MPPI_NOISE_HOST_INJECTED)) return MPPI_ERR_INVALID;
+    h->noise_source = source;
+    h->seed = seed;
+    return MPPI_OK;
+}
+
+mppi_status mppi_inject_noise(mppi_handle *h, const double *eps, int64_t columns)
+{
+    if (!h || (!eps && columns) || columns < 0) return MPPI_ERR_INVALID;
+    h->inj_pending.insert(h->inj_pending.end(), eps, eps + columns * h->C);
+    return MPPI_OK;
+}
+
+mppi_status mppi_noise_draws(mppi_handle *h, double time, int64_t *columns)
+{
+    if (!h || !columns) return MPPI_ERR_INVALID;
+    *columns = draws_for(h, (int64_t)((time - h->last_shift_time) / h->dt));
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_index_semantics(mppi_handle *h, int semantics)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    if (semantics == MPPI_INDEX_COMPAT_UINT8) {
+        if (h->R > 255) return fail(h, MPPI_ERR_UNSUPPORTED, "compat uint8 index semantics require rollouts + 2 <= 255 (the reference hangs beyond)");
+        h->compat_uint8 = 1;
+    } else if (semantics == MPPI_INDEX_WIDE) {
+        h->compat_uint8 = 0;
+    } else {
+        return MPPI_ERR_INVALID;
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    if (wrench_Hx6) h->forecast.assign(wrench_Hx6, wrench_Hx6 + 6 * h->H);
+    else h->forecast.clear();
+    HIP_TRY(hipSetDevice(h->device));
+    return upload_steps(h);
+}
+
+void *mppi_device_costs(mppi_handle *h) { return h ? (void *)h->d_costs : nullptr; }
+void *mppi_device_gradient(mppi_handle *h) { return h ? (void *)h->d_gpart : nullptr; }
+void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
+
+// ---- update ---------------------------------------------------------------------------------
+
+mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
+{
+    if (!h || !state) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    h->t_start = std::chrono::steady_clock::now();
+    h->rollout_time = time;
+    std::memcpy(h->h_stage, state, (size_t)h->X * sizeof(double));
+    HIP_TRY(hipEventRecord(h->ev[0], h->stream));
+    HIP_TRY(hipMemcpyAsync(h->d_x0, h->h_stage, (size_t)h->X * sizeof(double), hipMemcpyHostToDevice, h->stream));
+
+    // sample(): shift count by truncation (mppi.cpp:194-201)
+    h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);
+    if (h->shift_by > 0) {
+        h->last_shift_time = time;
+        h->shifted = std::max<int64_t>(0, h->H - h->shift_by);
+    }
+    SampleParams sp{};
+    sp.shift_by = h->shift_by;
+    sp.shifted = h->shift_by > 0 ? h->shifted : h->H;
+    sp.keep = keep_count(h);
+    sp.keep_draws = h->shift_by > 0 ? sp.keep * (h->H - h->shifted) : 0;
+    sp.update_index = h->update_count;
+    sp.seed = h->seed;
+    sp.injected = h->noise_source == MPPI_NOISE_HOST_INJECTED;
+    sp.tdiag = h->tdiag ? 1 : 0;
+    if (sp.injected) {
+        const int64_t draws = draws_for(h, h->shift_by);
+        const size_t need = (size_t)(draws * h->C);
+        if (h->inj_pending.size() < need) return fail(h, MPPI_ERR_NOISE, "injected noise stream too short: need " + std::to_string(draws) + " columns");
+        if (need > h->inj_capacity) {
+            if (h->d_inj) {
+                (void)hipFree(h->d_inj);
+                h->allocations.erase(std::find(h->allocations.begin(), h->allocations.end(), (void *)h->d_inj));
+                h->d_inj = nullptr;
+            }
+            HIP_TRY(dalloc(h, &h->d_inj, need));
+            h->inj_capacity = need;
+        }
+        if (need) HIP_TRY(hipMemcpy(h->d_inj, h->inj_pending.data(), need * sizeof(double), hipMemcpyHostToDevice));
+        h->inj_pending.erase(h->inj_pending.begin(), h->inj_pending.begin() + (long)need);
+    }
+    HIP_TRY(hipMemsetAsync(h->d_rank, 0, (size_t)h->R * sizeof(int), h->stream));
+    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->stream));
+    HIP_TRY(launch_shift(h->d_U, h->d_Us, (int)h->H, (int)h->C, h->shift_by, h->stream));
+    if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
+    HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        FrRolloutArgs a{};
+        a.model = h->d_model;
+        a.cost = h->d_cost;
+        a.steps = h->d_steps;
+        a.x0 = h->d_x0;
+        a.Ushift = h->d_Us;
+        a.Uprev = h->d_U;
+        a.noise = h->d_noise;
+        a.rank = h->d_rank;
+        a.inj = h->d_inj;
+        a.T = h->d_T;
+        a.cost_out = h->d_costs;
+        a.sp = sp;
+        a.begin = h->begin;
+        a.count = h->count;
+        a.Rpad = h->Rpad;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 0;
+        HIP_TRY(launch_fr_rollout(a, h->stream));
+    } else {
+        PmRolloutArgs a{};
+        a.pm = h->d_pm;
+        a.steps = h->d_steps;
+        a.x0 = h->d_x0;
+        a.Ushift = h->d_Us;
+        a.Uprev = h->d_U;
+        a.noise = h->d_noise;
+        a.rank = h->d_rank;
+        a.inj = h->d_inj;
+        a.T = h->d_T;
+        a.cost_out = h->d_costs;
+        a.sp = sp;
+        a.begin = h->begin;
+        a.count = h->count;
+        a.Rpad = h->Rpad;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 0;
+        HIP_TRY(launch_pm_rollout(a, h->stream));
+    }
+    HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    h->updated_once = true;
+    h->phase_open = true;
+    return MPPI_OK;
+}
+
+mppi_status mppi_update_phase2(mppi_handle *h)
+{
+    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
+    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)(h->H * h->C), h->d_status, h->d_gpart,
+                            h->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_update_phase3(mppi_handle *h)
+{
+    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemsetAsync(&h->d_status->sg_error, 0, sizeof(int), h->stream));
+    FinishArgs f{};
+    f.status = h->d_status;
+    f.status_w = h->d_status;
+    f.gpart = h->d_gpart;
+    f.gradient = h->d_grad;
+    f.Ushift = h->d_Us;
+    f.cmin = h->d_cmin;
+    f.cmax = h->d_cmax;
+    f.gradient_step = h->gradient_step;
+    f.control_bound = h->control_bound;
+    f.H = (int)h->H;
+    f.C = (int)h->C;
+    f.t0 = h->rollout_time;
+    f.dt = h->dt;
+    f.sg_window = h->sg_window;
+    f.sg_weights = h->d_sg_w;
+    f.sg_uu = h->d_sg_uu;
+    f.sg_tt = h->d_sg_tt;
+    f.sg_start = h->d_sg_start;
+    f.sg_last_trim = h->d_sg_last;
+    HIP_TRY(launch_finish(f, h->stream));
+    HIP_TRY(hipEventRecord(h->ev[3], h->stream));
+    // filter(): cost of the optimal control (mppi.cpp:450-479)
+    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        FrRolloutArgs a{};
+        a.model = h->d_model;
+        a.cost = h->d_cost;
+        a.steps = h->d_steps;
+        a.x0 = h->d_x0;
+        a.Ushift = h->d_Us;
+        a.Uprev = h->d_U;
+        a.cost_out = h->d_opt;
+        a.count = 1;
+        a.Rpad = 64;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 1;
+        HIP_TRY(launch_fr_rollout(a, h->stream));
+    } else {
+        PmRolloutArgs a{};
+        a.pm = h->d_pm;
+        a.steps = h->d_steps;
+        a.x0 = h->d_x0;
+        a.Ushift = h->d_Us;
+        a.Uprev = h->d_U;
+        a.cost_out = h->d_opt;
+        a.count = 1;
+        a.Rpad = 64;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 1;
+        HIP_TRY(launch_pm_rollout(a, h->stream));
+    }
+    HIP_TRY(hipEventRecord(h->ev[4], h->stream));
+    const int HC = (int)(h->H * h->C);
+    HIP_TRY(launch_publish(h->d_Us, h->d_U, HC, h->d_opt, h->d_status, h->d_out, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipEventRecord(h->ev[5], h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->phase_open = false;
+    for (int i = 0; i < 4; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
+    (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
+    const bool all_nan = h->h_out[HC + 1] != 0.0;
+    const bool sg_error = h->h_out[HC + 3] != 0.0;
+    if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
+    if (sg_error) return fail(h, MPPI_ERR_SMOOTHING, "Savitzky-Golay window: time went backwards");
+    {
+        std::lock_guard<std::mutex> lock(h->mtx);   // publish under lock (mppi.cpp:178-182)
+        h->last_rollout_time = h->rollout_time;
+        std::memcpy(h->U_host.data(), h->h_out, (size_t)HC * sizeof(double));
+        h->opt_cost = h->h_out[HC];
+    }
+    h->update_duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - h->t_start).count();
+    h->update_last = h->rollout_time;
+    ++h->update_count;
+    return MPPI_OK;
+}
+
+mppi_status mppi_update(mppi_handle *h, const double *state, double time)
+{
+    mppi_status st = mppi_update_phase1(h, state, time);
+    if (st != MPPI_OK) return st;
+    if (h->world > 1) {
+        if (!h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
+        NCCL_TRY(ncclAllReduce(h->d_costs, h->d_costs, (size_t)h->R, ncclDouble, ncclSum, h->comm, h->stream));
+    }
+    st = mppi_update_phase2(h);
+    if (st != MPPI_OK) return st;
+    if (h->world > 1)
+        NCCL_TRY(ncclAllReduce(h->d_gpart, h->d_gpart, (size_t)(h->H * h->C), ncclDouble, ncclSum, h->comm, h->stream));
+    return mppi_update_phase3(h);
+}
+
+// ---- queries --------------------------------------------------------------------------------
+
+mppi_status mppi_get(mppi_handle *h, double time, double *control)
+{
+    if (!h || !control) return MPPI_ERR_INVALID;
+    std::lock_guard<std::mutex> lock(h->mtx);
+    if (time < h->last_rollout_time) return fail(h, MPPI_ERR_TIME, "get() time precedes the last update");
+    double t = (time - h->last_rollout_time) / h->dt;
+    const int lower = (int)t, upper = lower + 1;
+    const int64_t C = h->C;
+    if (upper >= h->H) {
+        for (int64_t c = 0; c < C; c++)
+            control[c] = h->has_default ? h->cdefault[(size_t)c] : h->U_host[(size_t)((h->H - 1) * C + c)];
+        return MPPI_OK;
+    }
+    t -= lower;
+    for (int64_t c = 0; c < C; c++)
+        control[c] = (1.0 - t) * h->U_host[(size_t)(lower * C + c)] + t * h->U_host[(size_t)(upper * C + c)];
+    return MPPI_OK;
+}
+
+mppi_status mppi_costs(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpy(out, h->d_costs, (size_t)h->R * sizeof(double), hipMemcpyDeviceToHost));
+    return MPPI_OK;
+}
+
+mppi_status mppi_weights(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpy(out, h->d_weights, (size_t)h->R * sizeof(double), hipMemcpyDeviceToHost));
+    return MPPI_OK;
+}
+
+mppi_status mppi_gradient(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpy(out, h->d_grad, (size_t)(h->H * h->C) * sizeof(double), hipMemcpyDeviceToHost));
+    return MPPI_OK;
+}
+
+mppi_status mppi_optimal_control(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    std::lock_guard<std::mutex> lock(h->mtx);
+    std::memcpy(out, h->U_host.data(), h->U_host.size() * sizeof(double));
+    return MPPI_OK;
+}
+
+mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
+{
+    if (!h || !cost) return MPPI_ERR_INVALID;
+    std::lock_guard<std::mutex> lock(h->mtx);
+    *cost = h->opt_cost;
+    return MPPI_OK;
+}
+
+mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout)
+{
+    if (!h || !rollout) return MPPI_ERR_INVALID;
+    std::vector<double> c((size_t)h->R);
+    mppi_status st = mppi_costs(h, c.data());
+    if (st != MPPI_OK) return st;
+    int64_t best = -1;
+    for (int64_t i = 0; i < h->R; i++) {
+        if (std::isnan(c[(size_t)i])) continue;
+        if (best < 0 || c[(size_t)i] < c[(size_t)best]) best = i;   // first minimum
+    }
+    *rollout = best;
+    return MPPI_OK;
+}
+
+mppi_status mppi_update_duration(mppi_handle *h, double *seconds)
+{
+    if (!h || !seconds) return MPPI_ERR_INVALID;
+    *seconds = h->update_duration;
+    return MPPI_OK;
+}
+
+mppi_status mppi_noise(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    const int64_t HC = h->H * h->C;
+    std::vector<double> dev((size_t)(HC * h->Rpad));
+    HIP_TRY(hipMemcpy(dev.data(), h->d_noise, dev.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::memset(out, 0, (size_t)(h->R * HC) * sizeof(double));
+    for (int64_t lr = 0; lr < h->count; lr++) {
+        double *o = out + (h->begin + lr) * HC;
+        for (int64_t j = 0; j < HC; j++) o[j] = dev[(size_t)(j * h->Rpad + lr)];
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_dims(mppi_handle *h, int64_t *R, int64_t *H, int64_t *C, int64_t *X)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    if (R) *R = h->R;
+    if (H) *H = h->H;
+    if (C) *C = h->C;
+    if (X) *X = h->X;
+    return MPPI_OK;
+}
+
+mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64_t *start_idx)
+{
+    if (!h || !uu || !tt || !start_idx) return MPPI_ERR_INVALID;
+    if (h->sg_window <= 0) return fail(h, MPPI_ERR_INVALID, "smoothing disabled");
+    HIP_TRY(hipSetDevice(h->device));
+    const size_t n = (size_t)(h->C * (h->H + 2 * h->sg_window + 1));
+    HIP_TRY(hipMemcpy(uu, h->d_sg_uu, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(tt, h->d_sg_tt, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(start_idx, h->d_sg_start, (size_t)h->C * sizeof(int64_t), hipMemcpyDeviceToHost));
+    return MPPI_OK;
+}
+
+mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
+{
+    if (!h || !ms5) return MPPI_ERR_INVALID;
+    std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
+    return MPPI_OK;
+}
+
+}  // extern "C"

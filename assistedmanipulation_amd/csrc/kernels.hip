@@ -1,0 +1,902 @@
+// kernels.hip — MPPI device kernels for gfx950 (CDNA4, wave64).
+//
+// One update of mppi::Trajectory (reference src/controller/mppi.cpp:154-187) is the launch
+// sequence issued by engine.cpp:
+//
+//   rank_kernel      stable order of the previous costs            (sample(), mppi.cpp:222-231)
+//   shift_kernel     U*_shifted <- shift(U*)                        (sample(), mppi.cpp:194-217)
+//   fr_rollout_kernel / pm_rollout_kernel
+//                    per rollout: eps columns (kept-shift / fresh draw / -U*), fp64 horizon
+//                    rollout of the dynamics with the per-step cost fused, cost[r]
+//                                                                  (mppi.cpp:242-342)
+//   [RCCL all-reduce of cost[R] when sharded]
+//   weights_kernel   min/max over non-NaN, softmin weights          (optimise(), mppi.cpp:344-408)
+//   gradient_kernel  partial gradient sum_r w_r eps_r over the local shard (mppi.cpp:415-418)
+//   [RCCL all-reduce of the partial gradient when sharded]
+//   finish_kernel    U* += step * g, Savitzky-Golay, clamp          (mppi.cpp:421-447)
+//   fr_rollout_kernel(optimal) / pm_rollout_kernel(optimal)
+//                    cost of the new U* (filter(), mppi.cpp:450-479)
+//   publish_kernel   U* <- U*_shifted, pack the host-visible block   (mppi.cpp:178-182)
+//
+// Precision: the rollout runs in fp64.  The reference's cost is dominated by 1e10-scale
+// barrier terms (controller/cost.hpp:57-62, 88-93) and a 2e11 self-collision constant, so its
+// softmin weights are decided by how many horizon steps breach a barrier; fp32 dynamics flip
+// those counts within one or two updates (tools/precision_probe.py).
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+#include "engine_types.hpp"
+#include "kernels.hpp"
+
+using namespace mppi_eng;
+using mppi_dev::smax;
+using mppi_dev::smin;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Cost primitives (controller/cost.hpp).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v)
+{
+    if (v >= b.bound) {
+        double d = v - b.bound;
+        return b.max + b.scale * (d * d);
+    }
+    return smin(b.scale / (b.bound - v), b.max);
+}
+__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v)
+{
+    if (v <= b.bound) {
+        double d = b.bound - v;
+        return b.max + b.scale * (d * d);
+    }
+    return smin(b.scale / (v - b.bound), b.max);
+}
+
+// ---------------------------------------------------------------------------------------------
+// FrankaRidgeback dynamics (PinocchioDynamics::calculate/step, pinocchio_dynamics.cpp:153-260)
+// in world coordinates: a = M(q)^-1 tau_u by a zero-bias articulated-body pass (equal to the
+// reference's aba(q, v, tau_u + nle(q, v)) in exact arithmetic).  Per-body data the backward
+// and forward passes need (world pose, U, 1/D, u) lives in an LDS stack, lane-strided.
+// ---------------------------------------------------------------------------------------------
+constexpr int STK = 20;   // doubles per body: R[9] p[3] U[6] Dinv u
+
+template <int NT>
+struct Stack {
+    double *base;
+    int lane;
+    __device__ __forceinline__ double &at(int body, int e) const { return base[(body * STK + e) * NT + lane]; }
+};
+
+// Kinematics cached by calculate() for the *next* cost evaluation (the one-step lag).
+struct Kin {
+    double ee[3];   // panda_grasp_joint position
+    double am[3];   // arm_mount_joint position
+    double vl[3];   // EE spatial velocity, linear part, WORLD (at the world origin)
+    double jj[6];   // J_a J_a^T packed (00, 01, 02, 11, 12, 22), J_a = WORLD linear rows, arm cols
+};
+
+// World pose of body i from its parent's world pose and q_i; writes it to the stack.
+template <int NT>
+__device__ __forceinline__ void body_pose(const DevModel &M, int i, double qi, const double *Rpar,
+                                          const double *ppar, double *Rw, double *pw, const Stack<NT> &st)
+{
+    const DevBody &B = M.b[i];
+    double Rl[9], pl[3];
+    const int kind = FR_KIND[i];
+    if (kind == KIND_RZ) {
+        double s, c;
+        sincos(qi, &s, &c);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            Rl[3 * r + 0] = B.R[3 * r + 0] * c + B.R[3 * r + 1] * s;
+            Rl[3 * r + 1] = B.R[3 * r + 0] * (-s) + B.R[3 * r + 1] * c;
+            Rl[3 * r + 2] = B.R[3 * r + 2];
+            pl[r] = B.p[r];
+        }
+    } else {
+        const int col = (kind == KIND_PX) ? 0 : 1;
+        const double qq = (kind == KIND_PNY) ? -qi : qi;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) Rl[3 * r + k] = B.R[3 * r + k];
+            pl[r] = B.p[r] + B.R[3 * r + col] * qq;
+        }
+    }
+    if (FR_PARENT[i] < 0) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) Rw[k] = Rl[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) pw[k] = pl[k];
+    } else {
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                Rw[3 * r + c] = (Rpar[3 * r + 0] * Rl[c] + Rpar[3 * r + 1] * Rl[3 + c]) + Rpar[3 * r + 2] * Rl[6 + c];
+            pw[r] = ppar[r] + ((Rpar[3 * r + 0] * pl[0] + Rpar[3 * r + 1] * pl[1]) + Rpar[3 * r + 2] * pl[2]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) st.at(i, k) = Rw[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) st.at(i, 9 + k) = pw[k];
+}
+
+// World motion subspace S_i = (linear, angular) from the body's world pose.
+__device__ __forceinline__ void body_S(int i, const double *Rw, const double *pw, double *S)
+{
+    const int kind = FR_KIND[i];
+    if (kind == KIND_RZ) {
+        double w0 = Rw[2], w1 = Rw[5], w2 = Rw[8];
+        S[0] = pw[1] * w2 - pw[2] * w1;
+        S[1] = pw[2] * w0 - pw[0] * w2;
+        S[2] = pw[0] * w1 - pw[1] * w0;
+        S[3] = w0;
+        S[4] = w1;
+        S[5] = w2;
+    } else {
+        const int col = (kind == KIND_PX) ? 0 : 1;
+        const double sg = (kind == KIND_PNY) ? -1.0 : 1.0;
+        S[0] = sg * Rw[col];
+        S[1] = sg * Rw[3 + col];
+        S[2] = sg * Rw[6 + col];
+        S[3] = 0.0;
+        S[4] = 0.0;
+        S[5] = 0.0;
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void load_pose(const Stack<NT> &st, int i, double *Rw, double *pw)
+{
+#pragma unroll
+    for (int k = 0; k < 9; k++) Rw[k] = st.at(i, k);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pw[k] = st.at(i, 9 + k);
+}
+
+// Spatial inertia of body i at the world origin, packed upper triangle of the 6x6
+// [[m E, -m[c]x], [m[c]x, I_w + m(|c|^2 E - c c^T)]].
+__device__ __forceinline__ void world_inertia(const DevBody &B, const double *R, const double *p, double *P)
+{
+    double c[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) c[r] = ((R[3 * r] * B.c[0] + R[3 * r + 1] * B.c[1]) + R[3 * r + 2] * B.c[2]) + p[r];
+    // Ic full from xx, xy, yy, xz, yz, zz
+    const double I00 = B.Ic[0], I01 = B.Ic[1], I11 = B.Ic[2], I02 = B.Ic[3], I12 = B.Ic[4], I22 = B.Ic[5];
+    double RI[9];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        RI[3 * r + 0] = (R[3 * r] * I00 + R[3 * r + 1] * I01) + R[3 * r + 2] * I02;
+        RI[3 * r + 1] = (R[3 * r] * I01 + R[3 * r + 1] * I11) + R[3 * r + 2] * I12;
+        RI[3 * r + 2] = (R[3 * r] * I02 + R[3 * r + 1] * I12) + R[3 * r + 2] * I22;
+    }
+    double Iw[6];   // 00 01 02 11 12 22
+    int k = 0;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int s = r; s < 3; s++, k++)
+            Iw[k] = (RI[3 * r] * R[3 * s] + RI[3 * r + 1] * R[3 * s + 1]) + RI[3 * r + 2] * R[3 * s + 2];
+    const double m = B.mass;
+    const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
+    const double cc2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+    // row 0
+    P[0] = m; P[1] = 0.0; P[2] = 0.0; P[3] = 0.0; P[4] = mc2; P[5] = -mc1;
+    // row 1
+    P[6] = m; P[7] = 0.0; P[8] = -mc2; P[9] = 0.0; P[10] = mc0;
+    // row 2
+    P[11] = m; P[12] = mc1; P[13] = -mc0; P[14] = 0.0;
+    // rows 3..5 (angular block)
+    P[15] = Iw[0] + (m * cc2 - mc0 * c[0]);
+    P[16] = Iw[1] - mc0 * c[1];
+    P[17] = Iw[2] - mc0 * c[2];
+    P[18] = Iw[3] + (m * cc2 - mc1 * c[1]);
+    P[19] = Iw[4] - mc1 * c[2];
+    P[20] = Iw[5] + (m * cc2 - mc2 * c[2]);
+}
+
+__device__ __forceinline__ constexpr int pidx(int r, int c)
+{
+    return (r <= c) ? (r * 6 - r * (r - 1) / 2 + (c - r)) : (c * 6 - c * (c - 1) / 2 + (r - c));
+}
+
+// Forward kinematics at (q, qd): world poses (to the stack), the cost's kinematic cache.
+template <int NT>
+__device__ __forceinline__ void fk_pass(const DevModel &M, const double *q, const double *qd, const Stack<NT> &st, Kin &kin)
+{
+    double Rw[9], pw[3], R9[9], p9[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) kin.vl[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) kin.jj[k] = 0.0;
+    double Rprev[9], pprev[3];
+#pragma unroll
+    for (int i = 0; i < FR_NB; i++) {
+        const double *Rpar = (FR_PARENT[i] == 9 && i != 10) ? R9 : Rprev;
+        const double *ppar = (FR_PARENT[i] == 9 && i != 10) ? p9 : pprev;
+        body_pose<NT>(M, i, q[i], Rpar, ppar, Rw, pw, st);
+        double S[6];
+        body_S(i, Rw, pw, S);
+        if (i <= FR_EE_PARENT) {
+            if (i == 0) {
+#pragma unroll
+                for (int k = 0; k < 3; k++) kin.vl[k] = qd[i] * S[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; k++) kin.vl[k] = kin.vl[k] + qd[i] * S[k];
+            }
+        }
+        if (i >= FR_ARM0 && i < FR_ARM1) {
+            kin.jj[0] += S[0] * S[0]; kin.jj[1] += S[0] * S[1]; kin.jj[2] += S[0] * S[2];
+            kin.jj[3] += S[1] * S[1]; kin.jj[4] += S[1] * S[2]; kin.jj[5] += S[2] * S[2];
+        }
+        if (i == FR_AM_PARENT) {
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+                kin.am[r] = pw[r] + ((Rw[3 * r] * M.am_p[0] + Rw[3 * r + 1] * M.am_p[1]) + Rw[3 * r + 2] * M.am_p[2]);
+        }
+        if (i == FR_EE_PARENT) {
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+                kin.ee[r] = pw[r] + ((Rw[3 * r] * M.ee_p[0] + Rw[3 * r + 1] * M.ee_p[1]) + Rw[3 * r + 2] * M.ee_p[2]);
+#pragma unroll
+            for (int k = 0; k < 9; k++) R9[k] = Rw[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) p9[k] = pw[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; k++) Rprev[k] = Rw[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) pprev[k] = pw[k];
+    }
+}
+
+// Articulated-body passes over the poses on the stack: qdd = M(q)^-1 tau.
+template <int NT>
+__device__ __forceinline__ void aba_pass(const DevModel &M, const double *tau, const Stack<NT> &st, double *qdd)
+{
+    double acc[21], accp[6];
+    {
+        double R[9], p[3];
+        load_pose<NT>(st, 9, R, p);
+        world_inertia(M.b[9], R, p, acc);   // Ia_9 starts as body 9's own inertia
+#pragma unroll
+        for (int k = 0; k < 6; k++) accp[k] = 0.0;
+    }
+#pragma unroll
+    for (int i = FR_NB - 1; i >= 0; i--) {
+        double Ia[21], pA[6], R[9], p[3], S[6];
+        load_pose<NT>(st, i, R, p);
+        body_S(i, R, p, S);
+        if (i >= 10) {
+            world_inertia(M.b[i], R, p, Ia);
+#pragma unroll
+            for (int k = 0; k < 6; k++) pA[k] = 0.0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 21; k++) Ia[k] = acc[k];
+#pragma unroll
+            for (int k = 0; k < 6; k++) pA[k] = accp[k];
+        }
+        double U[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            double a = Ia[pidx(r, 0)] * S[0];
+#pragma unroll
+            for (int c = 1; c < 6; c++) a += Ia[pidx(r, c)] * S[c];
+            U[r] = a;
+        }
+        double Dd = S[0] * U[0];
+#pragma unroll
+        for (int r = 1; r < 6; r++) Dd += S[r] * U[r];
+        const double Dinv = 1.0 / Dd;
+        double sp = S[0] * pA[0];
+#pragma unroll
+        for (int r = 1; r < 6; r++) sp += S[r] * pA[r];
+        const double u = tau[i] - sp;
+#pragma unroll
+        for (int r = 0; r < 6; r++) st.at(i, 12 + r) = U[r];
+        st.at(i, 18) = Dinv;
+        st.at(i, 19) = u;
+        if (i > 0) {
+            if (i <= 9) {   // the parent's accumulator starts from the parent's own inertia
+                double Rq[9], pq[3];
+                load_pose<NT>(st, i - 1, Rq, pq);
+                world_inertia(M.b[i - 1], Rq, pq, acc);
+#pragma unroll
+                for (int k = 0; k < 6; k++) accp[k] = 0.0;
+            }
+            const double ud = u * Dinv;
+            int k = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double Ud = U[r] * Dinv;
+#pragma unroll
+                for (int c = r; c < 6; c++, k++) acc[k] += Ia[k] - Ud * U[c];
+            }
+#pragma unroll
+            for (int r = 0; r < 6; r++) accp[r] += pA[r] + U[r] * ud;
+        }
+    }
+    double a9[6], a[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) a[r] = 0.0;
+#pragma unroll
+    for (int i = 0; i < FR_NB; i++) {
+        double ap[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++) ap[r] = (i == 11) ? a9[r] : a[r];
+        double R[9], p[3], S[6];
+        load_pose<NT>(st, i, R, p);
+        body_S(i, R, p, S);
+        double ua = st.at(i, 12) * ap[0];
+#pragma unroll
+        for (int r = 1; r < 6; r++) ua += st.at(i, 12 + r) * ap[r];
+        const double dd = st.at(i, 18) * (st.at(i, 19) - ua);
+        qdd[i] = dd;
+#pragma unroll
+        for (int r = 0; r < 6; r++) a[r] = ap[r] + S[r] * dd;
+        if (i == 9) {
+#pragma unroll
+            for (int r = 0; r < 6; r++) a9[r] = a[r];
+        }
+    }
+}
+
+// AssistedManipulation::get_cost (assisted_manipulation.cpp:37-72) at state x = (q, qd) with
+// the lagged kinematic cache.
+__device__ __forceinline__ double fr_cost(const DevCost &Cs, const StepConst &sc, const double *q, const double *qd, const Kin &kin)
+{
+    double cost = 0.0;
+    if (Cs.en_joint) {   // joint_limit_cost (:74-88)
+        double jc = 0.0;
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) {
+            double c = left_barrier(Cs.lower[i], q[i]) + right_barrier(Cs.upper[i], q[i]);
+            jc += c;
+        }
+        cost += jc;
+    }
+    if (Cs.en_self) cost += Cs.self_collision;   // self_collision_cost (:90-158), link positions = 0
+    if (Cs.en_work) {   // workspace_cost (:160-209)
+        double wc = 0.0;
+        double s, c;
+        sincos(q[2], &s, &c);
+        const double r22 = (1.0 - c) + c;
+        const double fw0 = c, fw1 = s, fw2 = 0.0;
+        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
+        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
+        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
+        const double rb0 = kin.am[0] + off0, rb1 = kin.am[1] + off1, rb2 = kin.am[2] + off2;
+        const double t0 = kin.ee[0] - rb0, t1 = kin.ee[1] - rb1, t2 = kin.ee[2] - rb2;
+        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
+        wc += left_barrier(Cs.ws_infront, proj);
+        const double reach = sqrt((t0 * t0 + t1 * t1) + t2 * t2);
+        wc += right_barrier(Cs.ws_reach, reach);
+        const double n1 = sqrt(t0 * t0 + t1 * t1);
+        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
+        const double yaw = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
+        if (!isnan(yaw)) {
+            const double ay = fabs(yaw);
+            wc += (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
+        }
+        wc += left_barrier(Cs.ws_above, kin.ee[2] - rb2);
+        cost += wc;
+    }
+    if (Cs.en_vel) {   // velocity_cost (:224-235)
+        double vc = 0.0;
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) {
+            const double v = fabs(qd[i]);
+            vc += Cs.vel_q[i] * (v * v);
+        }
+        cost += vc;
+    }
+    if (Cs.en_traj) {   // trajectory_cost (:237-290)
+        double tc = 0.0;
+        if (sc.active) {
+            tc += sc.pos_cost;
+            double proj = ((kin.vl[0] * sc.target[0] + kin.vl[1] * sc.target[1]) + kin.vl[2] * sc.target[2]) / sc.tt;
+            const double p0 = proj * sc.target[0], p1 = proj * sc.target[1], p2 = proj * sc.target[2];
+            proj = copysign(1.0, proj) * sqrt((p0 * p0 + p1 * p1) + p2 * p2);
+            const double err = fabs(sc.vtarget - proj);
+            tc += (Cs.traj_vel_c + Cs.traj_vel_l * fabs(err)) + Cs.traj_vel_q * err * err;
+        }
+        cost += tc;
+    }
+    if (Cs.en_manip) {   // manipulability_cost (:292-319)
+        const double m00 = kin.jj[0], m01 = kin.jj[1], m02 = kin.jj[2], m11 = kin.jj[3], m12 = kin.jj[4], m22 = kin.jj[5];
+        const double h0 = m00 * (m11 * m22 - m12 * m12);
+        const double h1 = m01 * (m01 * m22 - m12 * m02);
+        const double h2 = m02 * (m01 * m12 - m11 * m02);
+        const double det = (h0 - h1) + h2;
+        double vol = sqrt(det);
+        if (isnan(vol)) vol = 1e-5;
+        else vol = (vol < 1e-5) ? 1e-5 : ((1e5 < vol) ? 1e5 : vol);
+        const double iv = 1.0 / vol;
+        cost += (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
+    }
+    return cost;
+}
+
+// eps = T z for one draw.  z from the Philox stream keyed by (seed, update, draw).
+__device__ __forceinline__ void philox_draw(const SampleParams &P, int64_t draw, const double *T, int C, double *eps)
+{
+    float z[16];
+#pragma unroll
+    for (int blk = 0; blk < 4; blk++) {
+        if (4 * blk >= C) break;
+        mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};
+        mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+        mppi_dev::box_muller(r.x, r.y, z[4 * blk + 0], z[4 * blk + 1]);
+        mppi_dev::box_muller(r.z, r.w, z[4 * blk + 2], z[4 * blk + 3]);
+    }
+    if (P.tdiag) {
+        for (int c = 0; c < C; c++) eps[c] = T[c * C + c] * (double)z[c];
+    } else {
+        for (int i = 0; i < C; i++) {
+            double s = 0.0;
+            for (int j = 0; j < C; j++) s += T[i * C + j] * (double)z[j];
+            eps[i] = s;
+        }
+    }
+}
+
+// The eps column (k) of rollout g as Trajectory::sample leaves it (mppi.cpp:242-269).
+// `col` holds the previous contents of the column on entry.
+__device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, int rank, int64_t k, int H, int C,
+                                              const double *Uprev, const double *inj, const double *T,
+                                              const double *noise, int64_t Rpad, int64_t lr, double *eps)
+{
+    if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
+        for (int c = 0; c < C; c++) eps[c] = -Uprev[k * C + c];
+        return;
+    }
+    int64_t draw = -1;
+    if (rank < P.keep) {
+        if (P.shift_by > 0) {
+            if (k < P.shifted) {
+                for (int c = 0; c < C; c++) eps[c] = noise[((k + P.shift_by) * C + c) * Rpad + lr];
+                return;
+            }
+            draw = (int64_t)rank * (H - P.shifted) + (k - P.shifted);
+        } else {
+            for (int c = 0; c < C; c++) eps[c] = noise[(k * C + c) * Rpad + lr];
+            return;
+        }
+    } else {
+        draw = P.keep_draws + (int64_t)(rank - P.keep) * H + k;
+    }
+    if (P.injected) {
+        for (int c = 0; c < C; c++) eps[c] = inj[draw * C + c];
+    } else {
+        philox_draw(P, draw, T, C, eps);
+    }
+}
+
+// t0 + k dt exactly as the reference's double expression (mppi.cpp:430, 437): window times are
+// compared with ==/< (filter.cpp:94-106), so no FMA contraction here.
+__device__ __forceinline__ double step_time(double t0, int k, double dt)
+{
+#pragma clang fp contract(off)
+    return t0 + (double)k * dt;
+}
+
+constexpr int FR_NT = 64;   // one wave per workgroup; the LDS stack takes 120 KiB of the CU's 160
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Rank of each sampled rollout (indices 2..R-1) in the stable order of the previous costs.
+// NaN sorts last (the reference's comparator is not a strict weak order with NaN: UB).
+// grid (ceil(S/256), ceil(S/256)), 256 threads; rank[] zeroed beforehand.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rank_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
+{
+    __shared__ double kj[256];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t j0 = (int64_t)blockIdx.y * 256;
+    const int64_t jl = j0 + threadIdx.x;
+    kj[threadIdx.x] = (jl < S) ? cost[2 + jl] : 0.0;
+    __syncthreads();
+    if (i >= S) return;
+    const double ki = cost[2 + i];
+    const bool ni = isnan(ki);
+    int cnt = 0;
+    const int jn = (int)((S - j0) < 256 ? (S - j0) : 256);
+    for (int t = 0; t < jn; t++) {
+        const double k = kj[t];
+        const int64_t j = j0 + t;
+        const bool nj = isnan(k);
+        bool less;
+        if (ni) less = nj ? (j < i) : true;
+        else less = nj ? false : ((k < ki) || (k == ki && j < i));
+        cnt += less ? 1 : 0;
+    }
+    if (cnt) atomicAdd(&rank[2 + i], cnt);
+}
+
+// U*_shifted <- U* shifted left by shift_by with the last column replicated (mppi.cpp:197-207).
+__global__ void shift_kernel(const double *__restrict__ U, double *__restrict__ Us, int H, int C, int64_t shift_by)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= H * C || shift_by <= 0) return;
+    const int k = t / C, c = t % C;
+    const int64_t shifted = (H - shift_by) > 0 ? (H - shift_by) : 0;
+    Us[t] = (k < shifted) ? U[(k + shift_by) * C + c] : U[(H - 1) * C + c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// FrankaRidgeback rollouts: one lane per rollout (first version).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
+{
+    __shared__ double stack_mem[FR_NB * STK * FR_NT];
+    const int lane = threadIdx.x;
+    const int64_t lr = (int64_t)blockIdx.x * FR_NT + lane;   // local rollout
+    const bool live = lr < a.count;
+    const int64_t g = a.optimal ? -1 : a.begin + lr;            // global rollout index
+    Stack<FR_NT> st{stack_mem, lane};
+    const DevModel &M = *a.model;
+    const DevCost &Cs = *a.cost;
+    const int H = a.H;
+    const int rank = (live && g >= 2) ? a.rank[g] : 0;
+
+    double q[FR_NB], qd[FR_NB];
+#pragma unroll
+    for (int i = 0; i < FR_NB; i++) {
+        q[i] = a.x0[i];
+        qd[i] = a.x0[FR_NB + i];
+    }
+    Kin kin;
+    fk_pass<FR_NT>(M, q, qd, st, kin);   // set_state -> calculate() at (q0, v0) (:142-151)
+    double J = 0.0;
+    bool alive = live;
+    for (int k = 0; k < H; k++) {
+        double eps[FR_C];
+        if (a.optimal || g == 0) {
+#pragma unroll
+            for (int c = 0; c < FR_C; c++) eps[c] = 0.0;
+        } else if (live) {
+            sample_column(a.sp, g, rank, k, H, FR_C, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
+#pragma unroll
+            for (int c = 0; c < FR_C; c++) a.noise[((int64_t)k * FR_C + c) * a.Rpad + lr] = eps[c];
+        }
+        if (!alive) continue;
+        const StepConst &sc = a.steps[k];
+        const double step_cost = sc.gamma_k * fr_cost(Cs, sc, q, qd, kin);
+        if (!a.optimal && isnan(step_cost)) {   // rollout cost NaN, stop (mppi.cpp:331-334)
+            J = NAN;
+            alive = false;
+            continue;
+        }
+        J += step_cost;
+        if (k == H - 1) break;   // the final step's dynamics are never observed
+        double u[FR_C];
+#pragma unroll
+        for (int c = 0; c < FR_C; c++) u[c] = a.Ushift[k * FR_C + c] + eps[c];
+        // PinocchioDynamics::step (:226-260)
+        double s, c;
+        sincos(q[2], &s, &c);
+        qd[0] = c * u[0] + (-s) * u[1];
+        qd[1] = s * u[0] + c * u[1];
+        qd[2] = u[2];
+        double tau[FR_NB];
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) tau[i] = (i >= 3 && i < 10) ? u[i] : 0.0;
+        fk_pass<FR_NT>(M, q, qd, st, kin);
+        double qdd[FR_NB];
+        aba_pass<FR_NT>(M, tau, st, qdd);
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) qd[i] = qd[i] + qdd[i] * a.dt;
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) q[i] = q[i] + qd[i] * a.dt;
+    }
+    if (!live) return;
+    if (a.optimal) *a.cost_out = J;
+    else a.cost_out[g] = J;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Point-mass rollouts (config 2).  State (p, v), control = force.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
+{
+    const int64_t lr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lr >= a.count) return;
+    const int64_t g = a.optimal ? -1 : a.begin + lr;
+    const int rank = (g >= 2) ? a.rank[g] : 0;
+    const DevPointMass &P = *a.pm;
+    double x[6];
+    for (int i = 0; i < 6; i++) x[i] = a.x0[i];
+    double J = 0.0;
+    bool alive = true;
+    for (int k = 0; k < a.H; k++) {
+        double eps[3];
+        if (a.optimal || g == 0) {
+            eps[0] = eps[1] = eps[2] = 0.0;
+        } else {
+            sample_column(a.sp, g, rank, k, a.H, 3, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
+            for (int c = 0; c < 3; c++) a.noise[((int64_t)k * 3 + c) * a.Rpad + lr] = eps[c];
+        }
+        if (!alive) continue;
+        double u[3];
+        for (int c = 0; c < 3; c++) u[c] = a.Ushift[k * 3 + c] + eps[c];
+        double cost = 0.0;
+        for (int i = 0; i < 3; i++) {
+            const double d = x[i] - P.target[i];
+            cost += P.q[i] * (d * d);
+        }
+        for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
+        const double sc = a.steps[k].gamma_k * cost;
+        if (!a.optimal && isnan(sc)) {
+            J = NAN;
+            alive = false;
+            continue;
+        }
+        J += sc;
+        for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
+        for (int i = 0; i < 3; i++) x[i] = x[i] + x[3 + i] * a.dt;
+    }
+    if (a.optimal) *a.cost_out = J;
+    else a.cost_out[g] = J;
+}
+
+// ---------------------------------------------------------------------------------------------
+// optimise(): min / max over non-NaN costs, status, softmin weights (mppi.cpp:344-408).
+// One workgroup of 1024 threads.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict__ cost, int64_t R, double cost_scale,
+                                                       double *__restrict__ weights, Status *__restrict__ status)
+{
+    __shared__ double smn[1024], smx[1024];
+    __shared__ long long scnt[1024];
+    const int t = threadIdx.x;
+    double mn = INFINITY, mx = -INFINITY;
+    long long cnt = 0;
+    for (int64_t i = t; i < R; i += 1024) {
+        const double c = cost[i];
+        if (isnan(c)) continue;
+        cnt++;
+        mn = (c < mn) ? c : mn;
+        mx = (c > mx) ? c : mx;
+    }
+    smn[t] = mn;
+    smx[t] = mx;
+    scnt[t] = cnt;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (t < s) {
+            smn[t] = (smn[t + s] < smn[t]) ? smn[t + s] : smn[t];
+            smx[t] = (smx[t + s] > smx[t]) ? smx[t + s] : smx[t];
+            scnt[t] += scnt[t + s];
+        }
+        __syncthreads();
+    }
+    const double minimum = smn[0], maximum = smx[0];
+    const long long valid = scnt[0];
+    __syncthreads();
+    if (valid <= 1) {   // minmax_element over <= 1 element: it1 == it2 -> throw
+        if (t == 0) { status->all_nan = 1; status->early = 1; status->minimum = minimum; status->maximum = maximum; }
+        return;
+    }
+    const double difference = maximum - minimum;
+    if (difference < 1e-6) {   // early return, weights/gradient stale (mppi.cpp:373-375)
+        if (t == 0) { status->all_nan = 0; status->early = 1; status->minimum = minimum; status->maximum = maximum; }
+        return;
+    }
+    double tot = 0.0;
+    for (int64_t i = t; i < R; i += 1024) {
+        const double c = cost[i];
+        double l = 0.0;
+        if (!isnan(c)) {
+            l = exp(-cost_scale * (c - minimum) / difference);
+            tot += l;
+        }
+        weights[i] = l;
+    }
+    smn[t] = tot;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (t < s) smn[t] += smn[t + s];
+        __syncthreads();
+    }
+    const double total = smn[0];
+    for (int64_t i = t; i < R; i += 1024) weights[i] = weights[i] / total;
+    if (t == 0) { status->all_nan = 0; status->early = 0; status->minimum = minimum; status->maximum = maximum; status->total = total; }
+}
+
+// Partial gradient over the local shard: gpart[k*C + c] = sum_lr w[begin+lr] eps[k][c][lr]
+// (mppi.cpp:415-418).  One workgroup of 256 per (k, c) row; the row is contiguous in HBM.
+__global__ __launch_bounds__(256) void gradient_kernel(const double *__restrict__ noise, const double *__restrict__ weights,
+                                                       int64_t begin, int64_t count, int64_t Rpad, const Status *__restrict__ status,
+                                                       double *__restrict__ gpart)
+{
+    __shared__ double red[256];
+    if (status->early) return;
+    const int64_t row = blockIdx.x;
+    const double *n = noise + row * Rpad;
+    const double *w = weights + begin;
+    double s = 0.0;
+    for (int64_t r = threadIdx.x; r < count; r += 256) s += w[r] * n[r];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gpart[row] = red[0];
+}
+
+// U* += step * gradient; Savitzky-Golay; clamp (mppi.cpp:421-447).  One workgroup.
+// SG: one thread per control dimension runs its MovingExtendedWindow (filter.cpp:19-116).
+__global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
+{
+    const Status &stt = *a.status;
+    if (stt.early) return;
+    const int HC = a.H * a.C;
+    for (int t = threadIdx.x; t < HC; t += blockDim.x) {
+        a.gradient[t] = a.gpart[t];
+        a.Ushift[t] += a.gpart[t] * a.gradient_step;
+    }
+    __syncthreads();
+    if (a.sg_window > 0) {
+        const int c = threadIdx.x;
+        if (c < a.C) {
+            const int w = a.sg_window;
+            const int W = a.H + 2 * w + 1;
+            double *uu = a.sg_uu + (int64_t)c * W;
+            double *tt = a.sg_tt + (int64_t)c * W;
+            int64_t start_idx = a.sg_start[c];
+            double last_trim = a.sg_last_trim[c];
+            const double t0 = a.t0;
+            int err = 0;
+            // trim(t0)
+            if (t0 < last_trim) err = 1;
+            if (!err) {
+                last_trim = t0;
+                int64_t trim_idx = start_idx;
+                for (int64_t i = 0; i < start_idx; i++)
+                    if (tt[i] >= t0) { trim_idx = i; break; }
+                const int64_t offset = trim_idx - w;
+                if (offset > 0) {   // std::rotate left by offset, then extend with the last kept value
+                    for (int64_t i = 0; i < W - offset; i++) { tt[i] = tt[i + offset]; uu[i] = uu[i + offset]; }
+                    const double tl = tt[W - offset - 1], ul = uu[W - offset - 1];
+                    for (int64_t i = W - offset; i < W; i++) { tt[i] = tl; uu[i] = ul; }
+                }
+                start_idx = w;
+                tt[start_idx] = t0;
+                // add_measurement for each step
+                for (int k = 0; k < a.H && !err; k++) {
+                    const double tk = step_time(t0, k, a.dt);
+                    if (tk < tt[start_idx]) { err = 1; break; }
+                    const double v = a.Ushift[k * a.C + c];
+                    uu[start_idx] = v;
+                    tt[start_idx] = tk;
+                    for (int64_t i = start_idx + 1; i < W; i++) { uu[i] = v; tt[i] = tk; }
+                    start_idx++;
+                }
+                // apply for each step: extract centred at lower_bound(t), then set(idx - 1)
+                for (int k = 0; k < a.H && !err; k++) {
+                    const double tk = step_time(t0, k, a.dt);
+                    int64_t lo = 0, hi = W;
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi) / 2;
+                        if (tt[mid] < tk) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    const int64_t idx = lo;
+                    double res = a.sg_weights[0] * uu[idx - w];
+                    for (int j = 1; j < 2 * w + 1; j++) res += a.sg_weights[j] * uu[idx - w + j];
+                    res = res / 1.0;
+                    a.Ushift[k * a.C + c] = res;
+                    uu[idx - 1] = res;
+                }
+            }
+            a.sg_start[c] = start_idx;
+            a.sg_last_trim[c] = last_trim;
+            if (err) a.status_w->sg_error = 1;
+        }
+        __syncthreads();
+    }
+    if (a.control_bound) {
+        for (int t = threadIdx.x; t < HC; t += blockDim.x) {
+            const int c = t % a.C;
+            double u = a.Ushift[t];
+            u = smin(u, a.cmax[c]);
+            u = smax(u, a.cmin[c]);
+            a.Ushift[t] = u;
+        }
+    }
+}
+
+// Publish U* <- U*_shifted and pack the host-visible block [U (H*C), optimal cost, status].
+__global__ void publish_kernel(const double *__restrict__ Us, double *__restrict__ U, int HC, const double *__restrict__ opt_cost,
+                               const Status *__restrict__ status, double *__restrict__ out)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = !status->all_nan && !status->sg_error;
+    if (t < HC) {
+        if (ok) U[t] = Us[t];
+        out[t] = ok ? Us[t] : U[t];
+    }
+    if (t == 0) {
+        out[HC + 0] = *opt_cost;
+        out[HC + 1] = (double)status->all_nan;
+        out[HC + 2] = (double)status->early;
+        out[HC + 3] = (double)status->sg_error;
+        out[HC + 4] = status->minimum;
+        out[HC + 5] = status->maximum;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launch wrappers (host).
+// ---------------------------------------------------------------------------------------------
+namespace mppi_eng {
+
+hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s)
+{
+    if (S <= 0) return hipSuccess;
+    const unsigned nb = (unsigned)((S + 255) / 256);
+    hipLaunchKernelGGL(rank_kernel, dim3(nb, nb), dim3(256), 0, s, cost, S, rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift_by, hipStream_t s)
+{
+    const int n = H * C;
+    hipLaunchKernelGGL(shift_kernel, dim3((n + 255) / 256), dim3(256), 0, s, U, Us, H, C, shift_by);
+    return hipGetLastError();
+}
+
+hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s)
+{
+    const unsigned nb = (unsigned)((a.count + FR_NT - 1) / FR_NT);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(fr_rollout_kernel, dim3(nb), dim3(FR_NT), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
+{
+    const unsigned nb = (unsigned)((a.count + 255) / 256);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(pm_rollout_kernel, dim3(nb), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s)
+{
+    hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(1024), 0, s, cost, R, cost_scale, weights, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
+                           int rows, const Status *status, double *gpart, hipStream_t s)
+{
+    hipLaunchKernelGGL(gradient_kernel, dim3(rows), dim3(256), 0, s, noise, weights, begin, count, Rpad, status, gpart);
+    return hipGetLastError();
+}
+
+hipError_t launch_finish(const FinishArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_publish(const double *Us, double *U, int HC, const double *opt_cost, const Status *status, double *out,
+                          hipStream_t s)
+{
+    hipLaunchKernelGGL(publish_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, Us, U, HC, opt_cost, status, out);
+    return hipGetLastError();
+}
+
+}  // namespace mppi_eng

@@ -1,0 +1,87 @@
+// kernels.hpp — launch interface of kernels.hip for the host runtime (engine.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "engine_types.hpp"
+
+namespace mppi_eng {
+
+// Device-side outcome of optimise() (mppi.cpp:344-375) and of the smoothing filter.
+struct Status {
+    int all_nan;     // <= 1 valid rollout: "all nan rollouts" (mppi.cpp:369-370)
+    int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
+    int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
+    int pad;
+    double minimum, maximum, total;
+};
+
+struct FrRolloutArgs {
+    const DevModel *model;
+    const DevCost *cost;
+    const StepConst *steps;   // [H]
+    const double *x0;         // [X]
+    const double *Ushift;     // [H][C]  U* shifted to this update
+    const double *Uprev;      // [H][C]  U* of the previous update (rollout 1 = -U*)
+    double *noise;            // [H][C][Rpad], local rollouts
+    const int *rank;          // [R] stable-order rank of rollouts 2..R-1
+    const double *inj;        // injected eps stream [draws][C]
+    const double *T;          // [C][C] noise transform (row-major)
+    double *cost_out;         // [R] (global index) or the optimal-cost scalar
+    SampleParams sp;
+    int64_t begin, count, Rpad;
+    double dt;
+    int H;
+    int optimal;
+};
+
+struct PmRolloutArgs {
+    const DevPointMass *pm;
+    const StepConst *steps;
+    const double *x0;
+    const double *Ushift;
+    const double *Uprev;
+    double *noise;
+    const int *rank;
+    const double *inj;
+    const double *T;
+    double *cost_out;
+    SampleParams sp;
+    int64_t begin, count, Rpad;
+    double dt;
+    int H;
+    int optimal;
+};
+
+struct FinishArgs {
+    const Status *status;
+    Status *status_w;
+    const double *gpart;
+    double *gradient;
+    double *Ushift;
+    const double *cmin, *cmax;
+    double gradient_step;
+    int control_bound;
+    int H, C;
+    double t0, dt;
+    // Savitzky-Golay state (window 0 = disabled)
+    int sg_window;
+    const double *sg_weights;   // [2w+1]
+    double *sg_uu, *sg_tt;      // [C][H + 2w + 1]
+    int64_t *sg_start;          // [C]
+    double *sg_last_trim;       // [C]
+};
+
+hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s);
+hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift_by, hipStream_t s);
+hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
+hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
+hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s);
+hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
+                           int rows, const Status *status, double *gpart, hipStream_t s);
+hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
+hipError_t launch_publish(const double *Us, double *U, int HC, const double *opt_cost, const Status *status, double *out,
+                          hipStream_t s);
+
+}  // namespace mppi_eng

@@ -1,0 +1,347 @@
+"""mppi::Trajectory and its plugin surface on the MI355X engine.
+
+Mirrors src/controller/mppi.hpp of the reference: `Trajectory.create(configuration, dynamics,
+cost)` returns None on a validation failure (the reference returns nullptr and prints to stderr,
+mppi.cpp:17-69); `update(state, time)` runs one MPPI iteration on the device; `get(control,
+time)` / `__call__(time)` interpolate the published optimal control; the accessors return the
+quantities logger::MPPI records (logging/mppi.cpp:84-136).
+
+The dynamics and cost are *descriptors* (POD parameter blocks) rather than virtual objects: the
+kernels evaluate them on the device.  FrankaRidgebackDynamics / AssistedManipulation replace
+FrankaRidgeback::PinocchioDynamics / FrankaRidgeback::AssistedManipulation;
+PointMassDynamics / QuadraticCost are the bring-up plugins of SURVEY §8a a16.
+"""
+import ctypes as C
+import sys
+
+import numpy as np
+
+from . import abi
+from ._lib import load
+from .config import Configuration
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("%s: %s" % (abi.STATUS_NAMES.get(status, status), message))
+        self.status = status
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+# ---- plugin descriptors -------------------------------------------------------------------
+class Dynamics:
+    """mppi::Dynamics (mppi.hpp:30-85) as a device descriptor."""
+    control_dof = None
+    state_dof = None
+
+    def descriptor(self):
+        raise NotImplementedError
+
+    def get_control_dof(self):
+        return self.control_dof
+
+    def get_state_dof(self):
+        return self.state_dof
+
+
+class Cost:
+    """mppi::Cost (mppi.hpp:93-145) as a device descriptor."""
+    control_dof = None
+    state_dof = None
+
+    def descriptor(self):
+        raise NotImplementedError
+
+    def get_control_dof(self):
+        return self.control_dof
+
+    def get_state_dof(self):
+        return self.state_dof
+
+
+class FrankaRidgebackDynamics(Dynamics):
+    """FrankaRidgeback::PinocchioDynamics (pinocchio_dynamics.{hpp,cpp}).  `model` is a
+    mppi_frankaridgeback_desc; by default the body table generated from robot.urdf."""
+    control_dof = abi.MPPI_FR_CONTROL
+    state_dof = abi.MPPI_FR_STATE
+
+    def __init__(self, model=None):
+        if model is None:
+            model = abi.mppi_frankaridgeback_desc()
+            load().mppi_default_frankaridgeback(C.byref(model))
+        self.model = model
+
+    def descriptor(self):
+        d = abi.mppi_dynamics_desc()
+        d.kind = abi.MPPI_DYNAMICS_FRANKARIDGEBACK
+        d.frankaridgeback = self.model
+        return d
+
+
+class PointMassDynamics(Dynamics):
+    control_dof = 3
+    state_dof = 6
+
+    def __init__(self, mass=1.0):
+        self.mass = mass
+
+    def descriptor(self):
+        d = abi.mppi_dynamics_desc()
+        d.kind = abi.MPPI_DYNAMICS_POINT_MASS
+        d.point_mass.mass = self.mass
+        return d
+
+
+class AssistedManipulation(Cost):
+    """FrankaRidgeback::AssistedManipulation (objective/assisted_manipulation.{hpp,cpp}).
+    `configuration` is a mppi_assisted_manipulation_desc; by default DEFAULT_CONFIGURATION."""
+    control_dof = abi.MPPI_FR_CONTROL
+    state_dof = abi.MPPI_FR_STATE
+
+    def __init__(self, configuration=None):
+        if configuration is None:
+            configuration = abi.mppi_assisted_manipulation_desc()
+            load().mppi_default_assisted_manipulation(C.byref(configuration))
+        self.configuration = configuration
+
+    def descriptor(self):
+        c = abi.mppi_cost_desc()
+        c.kind = abi.MPPI_COST_ASSISTED_MANIPULATION
+        c.assisted_manipulation = self.configuration
+        return c
+
+
+class QuadraticCost(Cost):
+    control_dof = 3
+    state_dof = 6
+
+    def __init__(self, target=(1.0, 1.0, 1.0), q=(1.0, 1.0, 1.0), r=(0.01, 0.01, 0.01)):
+        self.target, self.q, self.r = target, q, r
+
+    def descriptor(self):
+        c = abi.mppi_cost_desc()
+        c.kind = abi.MPPI_COST_QUADRATIC
+        for i in range(3):
+            c.quadratic.target[i] = self.target[i]
+            c.quadratic.q[i] = self.q[i]
+            c.quadratic.r[i] = self.r[i]
+        return c
+
+
+def shard_range(rollout_count, world, rank):
+    b, e = C.c_int64(), C.c_int64()
+    st = load().mppi_shard_range(rollout_count, world, rank, C.byref(b), C.byref(e))
+    if st != abi.MPPI_OK:
+        raise EngineError(st, "invalid shard (%d, %d, %d)" % (rollout_count, world, rank))
+    return b.value, e.value
+
+
+def comm_unique_id():
+    buf = C.create_string_buffer(128)
+    st = load().mppi_comm_unique_id(buf)
+    if st != abi.MPPI_OK:
+        raise EngineError(st, "ncclGetUniqueId failed")
+    return buf.raw
+
+
+class Trajectory:
+    """mppi::Trajectory (mppi.hpp:267-658) on one MI355X device."""
+
+    def __init__(self, handle, configuration, dynamics, cost):
+        self._L = load()
+        self._h = handle
+        self.configuration = configuration
+        self.dynamics = dynamics
+        self.cost = cost
+        R, H, Cc, X = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        self._check(self._L.mppi_dims(self._h, C.byref(R), C.byref(H), C.byref(Cc), C.byref(X)))
+        self.R, self.H, self.C, self.X = R.value, H.value, Cc.value, X.value
+        self._rolled_out_state = np.asarray(configuration.initial_state, dtype=np.float64).copy()
+        self._rolled_out_state[:] = 0.0   # m_rollout_state.setZero() (mppi.cpp:121)
+        self._update_last = 0.0
+        self._update_count = 0
+
+    @staticmethod
+    def create(configuration: Configuration, dynamics: Dynamics, cost: Cost, device=0):
+        """Trajectory::create — None (and a message on stderr) on invalid input."""
+        L = load()
+        cfg, keep = configuration.to_c()
+        dd, cd = dynamics.descriptor(), cost.descriptor()
+        h = C.c_void_p()
+        st = L.mppi_create(C.byref(cfg), C.byref(dd), C.byref(cd), int(device), C.byref(h))
+        del keep
+        if st != abi.MPPI_OK:
+            print(L.mppi_last_error(None).decode(), file=sys.stderr)
+            return None
+        return Trajectory(h, configuration, dynamics, cost)
+
+    # -- lifecycle --------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mppi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st):
+        if st != abi.MPPI_OK:
+            raise EngineError(st, self._L.mppi_last_error(self._h).decode())
+
+    # -- multi-GPU ---------------------------------------------------------------------------
+    def comm_init(self, world, rank, unique_id):
+        self._check(self._L.mppi_comm_init(self._h, world, rank, unique_id))
+
+    def set_shard(self, world, rank):
+        self._check(self._L.mppi_set_shard(self._h, world, rank))
+
+    # -- parity hooks ------------------------------------------------------------------------
+    def set_noise_source(self, source, seed=0x5EED):
+        self._check(self._L.mppi_set_noise_source(self._h, int(source), int(seed)))
+
+    def inject_noise(self, eps):
+        e = np.ascontiguousarray(eps, dtype=np.float64).reshape(-1)
+        self._check(self._L.mppi_inject_noise(self._h, _p(e), e.size // self.C))
+
+    def noise_draws(self, time):
+        n = C.c_int64()
+        self._check(self._L.mppi_noise_draws(self._h, float(time), C.byref(n)))
+        return n.value
+
+    def set_index_semantics(self, semantics):
+        self._check(self._L.mppi_set_index_semantics(self._h, int(semantics)))
+
+    def set_forecast(self, wrench_Hx6):
+        if wrench_Hx6 is None:
+            self._check(self._L.mppi_set_forecast(self._h, None))
+            return
+        t = np.ascontiguousarray(wrench_Hx6, dtype=np.float64)
+        assert t.shape == (self.H, 6), t.shape
+        self._check(self._L.mppi_set_forecast(self._h, _p(t)))
+
+    # -- the hot path ------------------------------------------------------------------------
+    def update(self, state, time):
+        """Trajectory::update (mppi.cpp:154-187)."""
+        s = np.ascontiguousarray(state, dtype=np.float64)
+        assert s.size == self.X
+        self._check(self._L.mppi_update(self._h, _p(s), float(time)))
+        self._rolled_out_state = s.copy()
+        self._update_last = float(time)
+        self._update_count += 1
+
+    def update_phase1(self, state, time):
+        s = np.ascontiguousarray(state, dtype=np.float64)
+        self._check(self._L.mppi_update_phase1(self._h, _p(s), float(time)))
+        self._rolled_out_state = s.copy()
+
+    def update_phase2(self):
+        self._check(self._L.mppi_update_phase2(self._h))
+
+    def update_phase3(self, time):
+        self._check(self._L.mppi_update_phase3(self._h))
+        self._update_last = float(time)
+        self._update_count += 1
+
+    def device_costs_ptr(self):
+        return self._L.mppi_device_costs(self._h)
+
+    def device_gradient_ptr(self):
+        return self._L.mppi_device_gradient(self._h)
+
+    # -- queries -----------------------------------------------------------------------------
+    def get(self, time, control=None):
+        out = np.zeros(self.C) if control is None else control
+        self._check(self._L.mppi_get(self._h, float(time), _p(out)))
+        return out
+
+    def __call__(self, time):
+        return self.get(time)
+
+    def get_state_dof(self):
+        return self.X
+
+    def get_control_dof(self):
+        return self.C
+
+    def get_time_step(self):
+        return self.configuration.time_step
+
+    def get_step_count(self):
+        return self.H
+
+    def get_update_duration(self):
+        d = C.c_double()
+        self._check(self._L.mppi_update_duration(self._h, C.byref(d)))
+        return d.value
+
+    def get_update_last(self):
+        return self._update_last
+
+    def get_update_count(self):
+        return self._update_count
+
+    def get_rollout_count(self):
+        return self.R
+
+    def get_rolled_out_state(self):
+        return self._rolled_out_state
+
+    def _vec(self, fn, n):
+        out = np.zeros(n)
+        self._check(fn(self._h, _p(out)))
+        return out
+
+    def get_weights(self):
+        return self._vec(self._L.mppi_weights, self.R)
+
+    def get_gradient(self):
+        """C x H (Eigen column-major) returned as an (H, C) array: row k = column k."""
+        return self._vec(self._L.mppi_gradient, self.C * self.H).reshape(self.H, self.C)
+
+    def costs(self):
+        return self._vec(self._L.mppi_costs, self.R)
+
+    def noise(self):
+        return self._vec(self._L.mppi_noise, self.R * self.C * self.H).reshape(self.R, self.H, self.C)
+
+    def get_rollouts(self):
+        """[(noise (H, C), cost)] per rollout (mppi.hpp:422-424)."""
+        n, c = self.noise(), self.costs()
+        return [(n[r], c[r]) for r in range(self.R)]
+
+    def get_optimal_rollout(self):
+        return self._vec(self._L.mppi_optimal_control, self.C * self.H).reshape(self.H, self.C)
+
+    trajectory = get_optimal_rollout
+
+    def get_optimal_total_cost(self):
+        d = C.c_double()
+        self._check(self._L.mppi_optimal_cost(self._h, C.byref(d)))
+        return d.value
+
+    def argmin(self):
+        i = C.c_int64()
+        self._check(self._L.mppi_argmin(self._h, C.byref(i)))
+        return i.value
+
+    def smoothing_windows(self):
+        """(uu, tt, start_idx) of the per-dimension SG windows (SavitzkyGolayFilter::get_windows)."""
+        w = self.configuration.smoothing.window
+        W = self.H + 2 * w + 1
+        uu, tt = np.zeros((self.C, W)), np.zeros((self.C, W))
+        st = np.zeros(self.C, dtype=np.int64)
+        self._check(self._L.mppi_smoothing_windows(self._h, _p(uu), _p(tt),
+                                                   st.ctypes.data_as(C.POINTER(C.c_int64))))
+        return uu, tt, st
+
+    def kernel_times(self):
+        """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events)."""
+        out = (C.c_float * 5)()
+        self._check(self._L.mppi_kernel_times(self._h, out))
+        return list(out)

@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""MPPI rollout throughput on MI355X — BASELINE.json's metric.
+
+A "step" is one mppi::Trajectory::update() (reference src/controller/mppi.cpp:154-187, its own
+timing boundary) of the FrankaRidgeback Pinocchio dynamics + full AssistedManipulation cost,
+4096 samples x 64-step horizon per GPU (BASELINE configs[2]; configs[3] at N = 8), with the
+reference's cadence: updates at t = 0.05 j (5-step shift), keep-best 20, device Philox noise.
+value = samples x horizon x ranks / (max-over-ranks seconds per update).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+import assistedmanipulation_amd as am  # noqa: E402  (engine's ROCm runtime loads first)
+from assistedmanipulation_amd import abi  # noqa: E402
+
+SAMPLES_PER_GPU = 4096
+HORISON = 0.64            # 64 steps at dt = 0.01
+KEEP_BEST = 20
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; the rollout is fp64 VALU
+# Algorithmic FLOPs of one rollout-step of the minimal arithmetic the kernel executes
+# (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
+# FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins this value).
+FLOPS_PER_ROLLOUT_STEP = 6518.0
+# Noise tensor traffic per rollout-step: eps written by the rollout kernel and read by the
+# gradient reduction, fp64, C = 12  (2 * 12 * 8 B).
+BYTES_PER_ROLLOUT_STEP = 192.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--samples-per-gpu", type=int, default=SAMPLES_PER_GPU)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def cpu_baseline(threads, samples, horison):
+    """The oracle (fp64 restatement of the reference's CPU mppi.cpp path, Pinocchio-order
+    arithmetic, contiguous-block thread partition of mppi.cpp:272-307) on this host: a bounded
+    sample of the same workload (a few full updates)."""
+    from oracle import oracle as O
+    try:
+        libpath = O.build(native=True)   # g++ -O3 -march=native on the GPU box host
+    except Exception:
+        libpath = O.LIB_PATH
+    conf = am.frankaridgeback_configuration(rollouts=samples, horison=horison, keep_best_rollouts=KEEP_BEST,
+                                            threads=threads)
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, am.FrankaRidgebackDynamics().descriptor(), am.AssistedManipulation().descriptor(),
+                             lib_path=libpath)
+    orc.set_noise_source(False, 12345)
+    orc.set_forecast(am.constant_forecast(orc.H))
+    x = am.huddled_state()
+    orc.update(x, 0.0)   # warm-up
+    durs = []
+    t_total = 0.0
+    j = 1
+    while j <= 8 and (t_total < 10.0 or j <= 2):
+        orc.update(x, 0.05 * j)
+        d = orc.update_duration()
+        durs.append(d)
+        t_total += d
+        j += 1
+    med = float(np.median(durs))
+    return {"value": samples * orc.H / med, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d timed updates of the %dx%d FrankaRidgeback workload (median %.3f s/update), "
+                      "oracle/mppi_oracle.cpp fp64, %d threads, -march=native" % (len(durs), samples, orc.H, med, threads)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # bootstrap + barrier / max-over-ranks only (gloo)
+        dist.init_process_group("gloo")
+    S_total = args.samples_per_gpu * world
+    conf = am.frankaridgeback_configuration(rollouts=S_total, horison=HORISON, keep_best_rollouts=KEEP_BEST)
+    traj = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
+    if traj is None:
+        raise SystemExit("engine create failed")
+    if world > 1:
+        uid = [am.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        traj.comm_init(world, rank, uid[0])
+    traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    traj.set_forecast(am.constant_forecast(traj.H))
+    x = am.huddled_state()
+    j = 0
+    for _ in range(args.warmup):
+        traj.update(x, 0.05 * j)
+        j += 1
+    if dist:
+        dist.barrier()
+    kt = np.zeros(5)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        traj.update(x, 0.05 * j)   # returns after the device work (stream synchronised)
+        kt += np.array(traj.kernel_times())
+        j += 1
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = S_total * traj.H / (elapsed / args.steps)
+    kt /= args.steps
+    rollout_ms = float(kt[1])
+    count_local = traj.R // world + (1 if rank < traj.R % world else 0)
+    flops = FLOPS_PER_ROLLOUT_STEP * count_local * traj.H
+    achieved_tflops = flops / (rollout_ms * 1e-3) / 1e12
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    line = {
+        "metric": "MPPI rollouts/sec (samples x horizon steps/s), %dx%d FrankaRidgeback" % (S_total, traj.H),
+        "value": value,
+        "unit": "rollout-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (HUDDLED state, constant forecast wrench (20,0,0) N, Philox noise)",
+        "config": {"workload": "BASELINE configs[%d]: %d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, "
+                               "full AssistedManipulation cost stack%s" % (2 if world == 1 else 3, S_total, traj.H,
+                                                                          ", sample-sharded over RCCL" if world > 1 else ""),
+                   "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
+        "kernel_ms": {"sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
+        "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
+                     "kernel": "fr_rollout_kernel", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP},
+        "hbm": {"noise_tensor_GBs": BYTES_PER_ROLLOUT_STEP * count_local * traj.H / ((kt[1] + kt[2]) * 1e-3) / 1e9,
+                "peak_GBs": HBM_PEAK_GBS},
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.samples_per_gpu, HORISON)
+    print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

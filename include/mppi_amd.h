@@ -1,0 +1,295 @@
+/*
+ * mppi_amd.h — C-ABI of the MI355X-native MPPI trajectory engine.
+ *
+ * Drop-in boundary for the reference's `mppi::Trajectory` (src/controller/mppi.{hpp,cpp}
+ * of LuigiVan01/AssistedManipulation).  Every entry point is `extern "C"`, takes plain
+ * pointers and sizes, never throws, and returns an `mppi_status`.  The reference symbol each
+ * entry point replaces is cited next to it (paths relative to the reference's src/).
+ *
+ * Layout conventions (identical to the reference, which stores everything column-major with
+ * Eigen):
+ *   - a control trajectory is C x H, column-major: element (c, k) at [k * C + c];
+ *   - the per-rollout noise tensor handed across the ABI is R x (C x H): rollout r, element
+ *     (c, k) at [(r * H + k) * C + c]   (mppi.hpp:281 `Rollout::noise`);
+ *   - costs and weights are R-vectors indexed by rollout (R = rollouts + 2, mppi.hpp:306).
+ * Inside HBM the engine keeps its own layout; the ABI copies convert.
+ */
+#ifndef MPPI_AMD_H
+#define MPPI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPPI_AMD_ABI_VERSION 1
+
+#define MPPI_MAX_BODIES 16
+#define MPPI_MAX_CONTROL 16
+#define MPPI_MAX_STATE 48
+#define MPPI_FR_JOINTS 12       /* frankaridgeback/dof.hpp:36-61 DoF::JOINTS */
+#define MPPI_FR_STATE 31        /* dof.hpp:63 DoF::STATE */
+#define MPPI_FR_CONTROL 12      /* dof.hpp:70 DoF::CONTROL */
+
+typedef enum mppi_status {
+    MPPI_OK = 0,
+    MPPI_ERR_INVALID = 1,        /* Trajectory::create returns nullptr (mppi.cpp:17-69) */
+    MPPI_ERR_DEVICE = 2,         /* HIP runtime failure */
+    MPPI_ERR_ALL_NAN = 3,        /* optimise() throws "all nan rollouts" (mppi.cpp:369-370) */
+    MPPI_ERR_SMOOTHING = 4,      /* SavitzkyGolay window throws (filter.cpp:37-44, 73-82) */
+    MPPI_ERR_TIME = 5,           /* get() asserts monotonic time (mppi.cpp:483) */
+    MPPI_ERR_COMM = 6,           /* RCCL failure */
+    MPPI_ERR_NOISE = 7,          /* injected noise stream too short for this update */
+    MPPI_ERR_UNSUPPORTED = 8
+} mppi_status;
+
+/* ------------------------------------------------------------------------------------------
+ * Configuration — POD mirror of mppi::Configuration (mppi.hpp:181-249), field for field.
+ * Optional fields carry a has_* flag.  `threads` is validated (> 0) as the reference does
+ * (mppi.cpp:66-69) and otherwise ignored by the device engine.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct mppi_config {
+    const double *initial_state;   /* X doubles */
+    int64_t state_dof;             /* X (must match the dynamics) */
+    int64_t control_dof;           /* C (must match the dynamics) */
+    int64_t rollouts;              /* S */
+    int64_t keep_best_rollouts;    /* K */
+    double time_step;
+    double horison;                /* H = ceil(horison / time_step) (mppi.cpp:85) */
+    double gradient_step;
+    double cost_scale;
+    double cost_discount_factor;
+    const double *covariance;      /* C x C, column-major */
+    int32_t control_bound;
+    const double *control_min;     /* C */
+    const double *control_max;     /* C */
+    int32_t has_control_default;
+    const double *control_default; /* C, may be NULL when !has_control_default */
+    int32_t has_smoothing;
+    uint32_t smoothing_window;
+    uint32_t smoothing_order;
+    uint32_t threads;
+} mppi_config;
+
+/* ------------------------------------------------------------------------------------------
+ * Dynamics descriptors (replace the mppi::Dynamics plugin object, mppi.hpp:30-85).
+ * ---------------------------------------------------------------------------------------- */
+typedef enum mppi_dynamics_kind {
+    MPPI_DYNAMICS_FRANKARIDGEBACK = 1,  /* FrankaRidgeback::PinocchioDynamics (pinocchio_dynamics.cpp) */
+    MPPI_DYNAMICS_POINT_MASS = 2        /* build-defined bring-up plugin */
+} mppi_dynamics_kind;
+
+typedef enum mppi_joint_type {
+    MPPI_JOINT_REVOLUTE = 0,
+    MPPI_JOINT_PRISMATIC = 1
+} mppi_joint_type;
+
+/* One moving joint + the rigid body it carries, after fixed-joint merging, in Pinocchio's
+ * conventions.  Rotations are row-major 3x3. */
+typedef struct mppi_body {
+    int32_t parent;          /* parent body index, -1 = universe */
+    int32_t type;            /* mppi_joint_type */
+    double axis[3];          /* joint axis in the joint frame (unit) */
+    double rotation[9];      /* joint placement in the parent joint frame */
+    double translation[3];
+    double mass;
+    double lever[3];         /* centre of mass in the joint frame */
+    double inertia[6];       /* rotational inertia about the com, joint frame:
+                                xx, xy, yy, xz, yz, zz (Pinocchio Symmetric3 order) */
+} mppi_body;
+
+typedef struct mppi_frame {
+    int32_t parent;          /* body index the frame is rigidly attached to */
+    double rotation[9];      /* placement in that body's joint frame */
+    double translation[3];
+} mppi_frame;
+
+typedef struct mppi_frankaridgeback_desc {
+    int32_t nbodies;                         /* 12 */
+    mppi_body bodies[MPPI_MAX_BODIES];
+    mppi_frame end_effector;                 /* "panda_grasp_joint" (pinocchio_dynamics.hpp:58) */
+    mppi_frame arm_mount;                    /* "arm_mount_joint" (dynamics.cpp:26) */
+    double gravity[3];                       /* Pinocchio default (0, 0, -9.81) */
+} mppi_frankaridgeback_desc;
+
+typedef struct mppi_point_mass_desc {
+    double mass;                             /* state (p[3], v[3]), control = force[3] */
+} mppi_point_mass_desc;
+
+typedef struct mppi_dynamics_desc {
+    int32_t kind;                            /* mppi_dynamics_kind */
+    mppi_frankaridgeback_desc frankaridgeback;
+    mppi_point_mass_desc point_mass;
+} mppi_dynamics_desc;
+
+/* ------------------------------------------------------------------------------------------
+ * Cost descriptors (replace the mppi::Cost plugin object, mppi.hpp:93-145).
+ * ---------------------------------------------------------------------------------------- */
+typedef enum mppi_cost_kind {
+    MPPI_COST_ASSISTED_MANIPULATION = 1,     /* objective/assisted_manipulation.{hpp,cpp} */
+    MPPI_COST_QUADRATIC = 2                  /* point-mass bring-up cost */
+} mppi_cost_kind;
+
+typedef struct mppi_quadratic {              /* QuadraticCost (controller/cost.hpp:10-37) */
+    double constant_cost;
+    double linear_cost;
+    double quadratic_cost;
+} mppi_quadratic;
+
+typedef struct mppi_barrier {                /* Left/RightInverseBarrierFunction (cost.hpp:43-99) */
+    double bound;                            /* lower_bound (left) or upper_bound (right) */
+    double scale;
+    double maximum_cost;                     /* default 1e10 */
+} mppi_barrier;
+
+/* AssistedManipulation::Configuration (assisted_manipulation.hpp:16-131), field for field. */
+typedef struct mppi_assisted_manipulation_desc {
+    int32_t enable_joint_limit;
+    int32_t enable_self_collision_limit;
+    int32_t enable_workspace_limit;
+    int32_t enable_energy_limit;
+    int32_t enable_velocity_cost;
+    int32_t enable_trajectory_cost;
+    int32_t enable_manipulability_cost;
+    mppi_barrier lower_joint_limit[MPPI_FR_JOINTS];   /* left barriers */
+    mppi_barrier upper_joint_limit[MPPI_FR_JOINTS];   /* right barriers */
+    mppi_barrier self_collision_limit;                /* left */
+    double self_collision_radii[8];
+    mppi_barrier workspace_limit_above;               /* left */
+    mppi_barrier workspace_limit_infront;             /* left */
+    mppi_barrier workspace_limit_reach;               /* right */
+    mppi_quadratic workspace_cost_yaw;
+    mppi_barrier energy_limit_below;                  /* left */
+    mppi_barrier energy_limit_above;                  /* right */
+    mppi_quadratic velocity_cost[MPPI_FR_JOINTS];
+    double trajectory_target_scale;
+    double trajectory_target_maximum;
+    mppi_quadratic trajectory_position_cost;
+    double trajectory_position_threshold;
+    mppi_quadratic trajectory_velocity_cost;
+    double trajectory_velocity_minimum;
+    double trajectory_velocity_maximum;
+    double trajectory_velocity_dropoff;
+    mppi_quadratic manipulability_cost;
+    /* The reference's Actor hands the dynamics a DynamicsForecast handle (actor.cpp:85-89);
+     * without one trajectory_cost() returns 0 (assisted_manipulation.cpp:239-240). */
+    int32_t has_forecast;
+} mppi_assisted_manipulation_desc;
+
+typedef struct mppi_quadratic_cost_desc {    /* sum_i q_i (p_i - target_i)^2 + r_i u_i^2 */
+    double target[3];
+    double q[3];
+    double r[3];
+} mppi_quadratic_cost_desc;
+
+typedef struct mppi_cost_desc {
+    int32_t kind;                            /* mppi_cost_kind */
+    mppi_assisted_manipulation_desc assisted_manipulation;
+    mppi_quadratic_cost_desc quadratic;
+} mppi_cost_desc;
+
+/* ------------------------------------------------------------------------------------------
+ * Engine handle.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct mppi_handle mppi_handle;
+
+typedef enum mppi_noise_source {
+    MPPI_NOISE_DEVICE_PHILOX = 0,   /* eps = T z, z ~ N(0,1) from Philox4x32-10 keyed by (seed, draw) */
+    MPPI_NOISE_HOST_INJECTED = 1    /* eps columns supplied by mppi_inject_noise, consumed in
+                                       the reference's draw order (mppi.cpp:242-262) */
+} mppi_noise_source;
+
+typedef enum mppi_index_semantics {
+    MPPI_INDEX_WIDE = 0,            /* 64-bit rollout indices (documented deviation, R > 255) */
+    MPPI_INDEX_COMPAT_UINT8 = 1     /* reference std::uint8_t indices (mppi.hpp:639,642); R <= 255 */
+} mppi_index_semantics;
+
+/* Library identity / build info. */
+int mppi_abi_version(void);
+const char *mppi_build_info(void);
+
+/* Defaults: the FrankaRidgeback body table generated from robot.urdf
+ * (include/mppi_amd_frankaridgeback.h) and AssistedManipulation::DEFAULT_CONFIGURATION
+ * (assisted_manipulation.hpp:133-206). */
+void mppi_default_frankaridgeback(mppi_frankaridgeback_desc *out);
+void mppi_default_assisted_manipulation(mppi_assisted_manipulation_desc *out);
+
+/* Trajectory::create (mppi.hpp:321-326, mppi.cpp:11-77).  Validation failures return
+ * MPPI_ERR_INVALID with the reference's message available from mppi_last_error(NULL).
+ * `device` is the HIP device ordinal the handle binds to. */
+mppi_status mppi_create(const mppi_config *config, const mppi_dynamics_desc *dynamics,
+                        const mppi_cost_desc *cost, int device, mppi_handle **out);
+void mppi_destroy(mppi_handle *h);
+/* Last error message of a handle (or of the last failed mppi_create when h == NULL). */
+const char *mppi_last_error(const mppi_handle *h);
+
+/* Multi-GPU sample sharding.  Rollouts [begin, end) of this rank are the ones
+ * mppi_shard_range assigns; rollouts 0 and 1 always live on rank 0.  world == 1 disables it. */
+mppi_status mppi_shard_range(int64_t rollout_count, int world, int rank, int64_t *begin,
+                             int64_t *end);
+/* Unique id for RCCL bootstrap (128 bytes, ncclUniqueId), produced on rank 0 and broadcast by
+ * the caller (e.g. torch.distributed) before mppi_comm_init on every rank. */
+mppi_status mppi_comm_unique_id(char out[128]);
+mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char unique_id[128]);
+/* Shard without an engine communicator: the caller runs the two all-reduces between the
+ * update phases (mppi_update_phase1..3).  Must precede the first update. */
+mppi_status mppi_set_shard(mppi_handle *h, int world, int rank);
+
+/* Parity hooks. */
+mppi_status mppi_set_noise_source(mppi_handle *h, int source, uint64_t seed);
+/* Supply eps columns (C doubles each) for the next update(s); consumed in draw order. */
+mppi_status mppi_inject_noise(mppi_handle *h, const double *eps, int64_t columns);
+/* Number of eps columns the next update at `time` will draw (K*shift + (S-K)*H). */
+mppi_status mppi_noise_draws(mppi_handle *h, double time, int64_t *columns);
+mppi_status mppi_set_index_semantics(mppi_handle *h, int semantics);
+
+/* Per-update forecast table: row k = predicted end-effector wrench (fx fy fz tx ty tz) at
+ * t0 + k*dt, k < H (KalmanForecast::forecast, forecast.cpp:342-367, sampled on the step grid). */
+mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6);
+
+/* Trajectory::update (mppi.hpp:339, mppi.cpp:154-187): sample, rollout, optimise, filter,
+ * publish.  Blocks until the update is complete on the device. */
+mppi_status mppi_update(mppi_handle *h, const double *state, double time);
+
+/* Phase-split update for callers that run the collectives themselves (multi-GPU with an
+ * external communicator, or two shards on one device in tests).  Between phase 1 and 2 the
+ * caller all-reduces (sum) mppi_device_costs(h); between phase 2 and 3 it all-reduces (sum)
+ * mppi_device_gradient(h).  Buffers are fp64 device pointers on mppi_stream(h). */
+mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time);
+mppi_status mppi_update_phase2(mppi_handle *h);
+mppi_status mppi_update_phase3(mppi_handle *h);
+void *mppi_device_costs(mppi_handle *h);     /* R doubles */
+void *mppi_device_gradient(mppi_handle *h);  /* C*H doubles */
+void *mppi_stream(mppi_handle *h);           /* hipStream_t */
+
+/* Trajectory::get (mppi.cpp:481-512): thread-safe against a concurrent update(). */
+mppi_status mppi_get(mppi_handle *h, double time, double *control);
+
+/* Observables (logger::MPPI::log reads these, logging/mppi.cpp:84-136). Host copies in the
+ * reference layouts. */
+mppi_status mppi_costs(mppi_handle *h, double *costs_R);
+mppi_status mppi_weights(mppi_handle *h, double *weights_R);
+mppi_status mppi_gradient(mppi_handle *h, double *gradient_CxH);
+mppi_status mppi_optimal_control(mppi_handle *h, double *control_CxH);
+mppi_status mppi_optimal_cost(mppi_handle *h, double *cost);
+mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout);
+mppi_status mppi_update_duration(mppi_handle *h, double *seconds);
+mppi_status mppi_noise(mppi_handle *h, double *noise_R_C_H);
+mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
+                      int64_t *control_C, int64_t *state_X);
+
+/* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control
+ * dimension the value and time buffers (C x (H + 2w + 1), row per dimension) and start index. */
+mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64_t *start_idx);
+
+/* Kernel timing of the last update (HIP events on the engine stream), milliseconds:
+ * [0] sample/rank, [1] rollout, [2] weight-reduce, [3] optimal rollout, [4] whole update. */
+mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPPI_AMD_H */
