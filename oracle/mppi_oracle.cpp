@@ -1081,6 +1081,10 @@ struct Trajectory {
     std::vector<double> Tg;         // gaussian transform (row-major)
     std::string err;
     CostTerms optimal_terms{};
+    // sharded mode (rehearses the engine's multi-GPU exchange): only rollouts [shard_begin,
+    // shard_end) are rolled out, then `allreduce` sums the cost vector and the partial gradient.
+    int64_t shard_begin = 0, shard_end = -1;
+    void (*allreduce)(double *, int64_t) = nullptr;
 
     bool draw(double *out)
     {
@@ -1213,9 +1217,11 @@ struct Trajectory {
 
     void rollout()
     {
-        int64_t each = R / (int64_t)threads, distribute = R % (int64_t)threads;
+        const int64_t b0 = shard_begin, e0 = shard_end < 0 ? R : shard_end;
+        const int64_t n = e0 - b0;
+        int64_t each = n / (int64_t)threads, distribute = n % (int64_t)threads;
         std::vector<std::pair<int64_t, int64_t>> ranges;
-        int64_t start = 0;
+        int64_t start = b0;
         for (unsigned t = 0; t < threads; t++) {
             int64_t stop = start + each;
             if (distribute > 0) { stop += 1; distribute -= 1; }
@@ -1223,11 +1229,15 @@ struct Trajectory {
             ranges.emplace_back(start, stop);
             start = stop;
         }
+        if (shard_end >= 0)
+            for (int64_t r = 0; r < R; r++)
+                if (r < b0 || r >= e0) cost[(size_t)r] = 0.0;
         pool->run([&](unsigned t) {
             if (t >= ranges.size()) return;
             for (int64_t r = ranges[t].first; r < ranges[t].second; r++)
                 cost[(size_t)r] = rollout_one(noise[(size_t)r].data(), false, nullptr, dyn_d[t], dyn_f[t]);
         });
+        if (allreduce) allreduce(cost.data(), R);
     }
 
     int optimise()
@@ -1253,9 +1263,16 @@ struct Trajectory {
             weights[(size_t)i] = l;
         }
         for (auto &w : weights) w = w / total;
-        for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] = noise[0][(size_t)j] * weights[0];
-        for (int64_t i = 1; i < R; i++)
-            for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] += noise[(size_t)i][(size_t)j] * weights[(size_t)i];
+        if (shard_end < 0) {
+            for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] = noise[0][(size_t)j] * weights[0];
+            for (int64_t i = 1; i < R; i++)
+                for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] += noise[(size_t)i][(size_t)j] * weights[(size_t)i];
+        } else {   // partial sum over the shard, then summed across shards
+            for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] = 0.0;
+            for (int64_t i = shard_begin; i < shard_end; i++)
+                for (int64_t j = 0; j < C * H; j++) gradient[(size_t)j] += noise[(size_t)i][(size_t)j] * weights[(size_t)i];
+            if (allreduce) allreduce(gradient.data(), C * H);
+        }
         for (int64_t j = 0; j < C * H; j++) Ushift[(size_t)j] += gradient[(size_t)j] * cfg.gradient_step;
         if (sg) {
             try {
@@ -1452,6 +1469,14 @@ void oracle_smoothing_windows(void *h, double *uu, double *tt, int64_t *start_id
         start_idx[c] = (int64_t)w.start_idx;
         o += w.uu.size();
     }
+}
+
+void oracle_set_shard(void *h, int64_t begin, int64_t end, void (*allreduce)(double *, int64_t))
+{
+    Trajectory *t = (Trajectory *)h;
+    t->shard_begin = begin;
+    t->shard_end = end;
+    t->allreduce = allreduce;
 }
 
 // Optimal rollout's per-term totals (BaseTest reads them by downcasting, base.cpp:141-146).

@@ -15,6 +15,7 @@ from assistedmanipulation_amd import abi
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 _lib = None
+ALLREDUCE_FN = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int64)
 
 
 def build(native=False):
@@ -59,6 +60,7 @@ def lib(path=None):
     L.oracle_update_duration.restype = C.c_double
     L.oracle_update_duration.argtypes = [vp]
     L.oracle_set_threads.argtypes = [vp, C.c_uint]
+    L.oracle_set_shard.argtypes = [vp, i64, i64, ALLREDUCE_FN]
     L.oracle_smoothing_windows.argtypes = [vp, dp, dp, C.POINTER(C.c_int64)]
     L.oracle_kinematics.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc), dp, dp, dp, C.c_int, dp]
     L.oracle_rollout.restype = C.c_double
@@ -167,6 +169,12 @@ class OracleTrajectory:
             t = np.ascontiguousarray(table, dtype=np.float64)
             self._forecast_keep = t
             self._L.oracle_set_forecast(self._h, _p(t))
+
+    def set_shard(self, begin, end, allreduce):
+        """Sharded mode: roll out [begin, end) only; `allreduce(ptr, n)` sums n doubles in place
+        across ranks (called for the cost vector and the partial gradient)."""
+        self._allreduce_cb = ALLREDUCE_FN(allreduce)
+        self._L.oracle_set_shard(self._h, begin, end, self._allreduce_cb)
 
     def set_threads(self, n):
         self._L.oracle_set_threads(self._h, n)

@@ -1,0 +1,468 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors that pin the CPU oracle (run in the build container, where the
+reference tree is mounted; the outputs in tests/golden/*.npz are committed and used offline).
+
+This is an INDEPENDENT float64 numpy restatement, deliberately built differently from
+oracle/mppi_oracle.cpp so that agreement means something:
+
+  * robot model: robot.urdf parsed again here, links kept separate (no fixed-joint inertia
+    merging), rpy -> matrix by direct Rz Ry Rx products (not the urdfdom quaternion path);
+  * dynamics: mass matrix by composite Jacobians, M = sum_l m_l Jv_l^T Jv_l + Jw_l^T I_l Jw_l
+    over every link with mass, then a = solve(M, tau_u) (LU) — instead of RNEA + ABA;
+  * WORLD Jacobian / frame velocity: per-joint p x a, and checked against finite differences of
+    the end-effector pose (v_O = v_point - omega x p);
+  * cost and the MPPI update loop (sample / rollout / optimise / SG / clamp / filter) rewritten
+    in plain Python from the reference sources (mppi.cpp, assisted_manipulation.cpp, cost.hpp,
+    filter.cpp, gram_savitzky_golay.cpp).
+
+The reference itself cannot be built here (Eigen3 + Pinocchio are absent), so
+the Pinocchio boundary is pinned by this model plus physics identities (tests/test_oracle_cpu.py).
+"""
+import math
+import os
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+URDF = "/root/reference/src/frankaridgeback/model/robot.urdf"
+
+
+# ------------------------------------------------------------------------------------------
+# robot model (links unmerged)
+# ------------------------------------------------------------------------------------------
+def rpy_matrix(r, p, y):
+    cr, sr, cp, sp, cy, sy = math.cos(r), math.sin(r), math.cos(p), math.sin(p), math.cos(y), math.sin(y)
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1.0]])
+    Ry = np.array([[cp, 0, sp], [0, 1.0, 0], [-sp, 0, cp]])
+    Rx = np.array([[1.0, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    return Rz @ Ry @ Rx
+
+
+def origin_T(el):
+    T = np.eye(4)
+    o = el.find("origin") if el is not None else None
+    if o is not None:
+        xyz = [float(v) for v in o.get("xyz", "0 0 0").split()]
+        rpy = [float(v) for v in o.get("rpy", "0 0 0").split()]
+        T[:3, :3] = rpy_matrix(*rpy)
+        T[:3, 3] = xyz
+    return T
+
+
+class Robot:
+    def __init__(self, path=URDF):
+        root = ET.parse(path).getroot()
+        self.links = {l.get("name"): l for l in root.findall("link")}
+        self.joints = {j.get("name"): j for j in root.findall("joint")}
+        self.parent_joint = {}
+        for name, j in self.joints.items():
+            self.parent_joint[j.find("child").get("link")] = name
+        # moving joints in DoF order (frankaridgeback/dof.hpp)
+        self.dof = ["x_base_joint", "y_base_joint", "pivot_joint"] + ["panda_joint%d" % i for i in range(1, 8)] + \
+                   ["panda_finger_joint1", "panda_finger_joint2"]
+        self.root = [l for l in self.links if l not in self.parent_joint][0]
+        self.inertial = {}
+        for name, l in self.links.items():
+            i = l.find("inertial")
+            if i is None:
+                continue
+            m = float(i.find("mass").get("value"))
+            if m == 0.0:
+                continue
+            T = origin_T(i)
+            e = i.find("inertia")
+            g = lambda k: float(e.get(k, "0"))
+            I = np.array([[g("ixx"), g("ixy"), g("ixz")], [g("ixy"), g("iyy"), g("iyz")], [g("ixz"), g("iyz"), g("izz")]])
+            self.inertial[name] = (m, T[:3, 3].copy(), T[:3, :3] @ I @ T[:3, :3].T)
+
+    def chain(self, link):
+        """joints from the root to `link`."""
+        out = []
+        while link in self.parent_joint:
+            j = self.parent_joint[link]
+            out.append(j)
+            link = self.joints[j].find("parent").get("link")
+        return out[::-1]
+
+    def link_pose(self, q, link):
+        """World pose of a link frame, and the world axis/origin of every moving joint on the way."""
+        T = np.eye(4)
+        axes = {}
+        for jn in self.chain(link):
+            j = self.joints[jn]
+            T = T @ origin_T(j)
+            t = j.get("type")
+            if t in ("revolute", "prismatic"):
+                a = np.array([float(v) for v in j.find("axis").get("xyz").split()])
+                qi = q[self.dof.index(jn)]
+                axes[jn] = (T[:3, :3] @ a, T[:3, 3].copy(), t)
+                M = np.eye(4)
+                if t == "revolute":
+                    a = a / np.linalg.norm(a)
+                    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+                    M[:3, :3] = np.eye(3) + math.sin(qi) * K + (1 - math.cos(qi)) * K @ K
+                else:
+                    M[:3, 3] = a * qi
+                T = T @ M
+        return T, axes
+
+    def mass_matrix(self, q):
+        n = len(self.dof)
+        M = np.zeros((n, n))
+        for link, (m, c_local, I_local) in self.inertial.items():
+            T, axes = self.link_pose(q, link)
+            R, p = T[:3, :3], T[:3, 3]
+            c = p + R @ c_local
+            Iw = R @ I_local @ R.T
+            Jv = np.zeros((3, n))
+            Jw = np.zeros((3, n))
+            for jn, (a, o, t) in axes.items():
+                k = self.dof.index(jn)
+                if t == "revolute":
+                    Jv[:, k] = np.cross(a, c - o)
+                    Jw[:, k] = a
+                else:
+                    Jv[:, k] = a
+            M += m * Jv.T @ Jv + Jw.T @ Iw @ Jw
+        return M
+
+    def frame(self, q, link):
+        T, axes = self.link_pose(q, link)
+        return T
+
+    def world_jacobian(self, q, link):
+        """Spatial (WORLD, at the world origin) Jacobian columns of the joints supporting link."""
+        _, axes = self.link_pose(q, link)
+        J = np.zeros((6, len(self.dof)))
+        for jn, (a, o, t) in axes.items():
+            k = self.dof.index(jn)
+            if t == "revolute":
+                J[:3, k] = np.cross(o, a)
+                J[3:, k] = a
+            else:
+                J[:3, k] = a
+        return J
+
+
+def fd_world_velocity(rob, q, v, link, h=1e-6):
+    """Spatial velocity at the world origin from finite differences of the link pose."""
+    T1 = rob.frame(q - h * v, link)
+    T2 = rob.frame(q + h * v, link)
+    T0 = rob.frame(q, link)
+    vp = (T2[:3, 3] - T1[:3, 3]) / (2 * h)
+    dR = (T2[:3, :3] - T1[:3, :3]) / (2 * h)
+    W = dR @ T0[:3, :3].T
+    w = np.array([W[2, 1], W[0, 2], W[1, 0]])
+    return np.concatenate([vp - np.cross(w, T0[:3, 3]), w])
+
+
+# ------------------------------------------------------------------------------------------
+# dynamics step + cost (pinocchio_dynamics.cpp:226-260, assisted_manipulation.cpp)
+# ------------------------------------------------------------------------------------------
+EE_LINK, AM_LINK = "panda_grasp", "franka_mount_link"
+
+
+def kin(rob, q, v):
+    ee = rob.frame(q, EE_LINK)[:3, 3]
+    am = rob.frame(q, AM_LINK)[:3, 3]
+    J = rob.world_jacobian(q, EE_LINK)
+    vee = J @ v
+    J = J.copy()
+    c, s = math.cos(q[2]), math.sin(q[2])
+    J[:3, :3] = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+    return dict(ee=ee, am=am, J=J, vee=vee)
+
+
+def left(bound, scale, v, mx=1e10):
+    if v <= bound:
+        return mx + scale * (bound - v) ** 2
+    return min(scale / (v - bound), mx)
+
+
+def right(bound, scale, v, mx=1e10):
+    if v >= bound:
+        return mx + scale * (v - bound) ** 2
+    return min(scale / (bound - v), mx)
+
+
+LOWER = [(-2.0, 0.0), (-2.0, 0.0), (-6.28, 0.0), (-2.8, 10.0), (-1.745, 10.0), (-2.8, 10.0), (-3.0718, 10.0),
+         (-2.7925, 10.0), (0.349, 10.0), (-2.967, 10.0), (0.0, 0.0), (0.0, 0.0)]
+UPPER = [(2.0, 0.0), (2.0, 0.0), (6.28, 0.0), (2.8, 10.0), (1.745, 10.0), (2.8, 10.0), (0.0, 10.0), (2.7925, 10.0),
+         (4.53785, 10.0), (2.967, 10.0), (0.5, 0.0), (0.5, 0.0)]
+VEL = [1000.0, 1000.0, 100.0, 0.5, 1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 0.0, 0.0]
+RADII = [0.75, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1]
+PAIRS = [(3, l) for l in (6, 7, 8, 9, 10)] + [(4, l) for l in (6, 7, 8, 9, 10)] + [(5, l) for l in (7, 8, 9, 10)] + \
+        [(6, l) for l in (8, 9, 10)] + [(7, l) for l in (9, 10)] + [(8, 10)]
+
+
+def cost(x, k_cache, force):
+    q, v = x[:12], x[12:24]
+    c = 0.0
+    c += sum(left(*LOWER[i], q[i]) + right(*UPPER[i], q[i]) for i in range(12))
+    c += sum(1e10 + (RADII[a - 3] + RADII[b - 3]) ** 2 for a, b in PAIRS)   # link positions == 0
+    ee, am = k_cache["ee"], k_cache["am"]
+    f = np.array([math.cos(x[2]), math.sin(x[2]), 0.0])
+    robot = am + np.array([0.1 * math.cos(x[2]), 0.1 * math.sin(x[2]), 0.15])
+    d = ee - robot
+    ws = left(0.0, 1.0, d @ f / (f @ f)) + right(1.0, 1.0, np.linalg.norm(d))
+    cosang = (d[:2] @ f[:2]) / np.linalg.norm(d[:2]) / np.linalg.norm(f[:2])
+    yaw = math.acos(cosang) if -1.0 <= cosang <= 1.0 else float("nan")
+    if not math.isnan(yaw):
+        ws += 400.0 * yaw * yaw
+    ws += left(0.0, 1.0, ee[2] - robot[2])
+    c += ws
+    c += sum(VEL[i] * v[i] ** 2 for i in range(12))
+    target = np.clip(0.01 * np.asarray(force[:3]), -1.0, 1.0)
+    dist = np.linalg.norm(target)
+    if dist > 0.0:
+        tc = 100.0 + 500.0 * dist * dist
+        proj = (k_cache["vee"][:3] @ target) / (target @ target)
+        proj = math.copysign(1.0, proj) * np.linalg.norm(target * proj)
+        vt = min(max(math.exp(2.0 * dist) - 1.0, 0.1), 5.0)
+        tc += 500.0 * (vt - proj) ** 2
+        c += tc
+    Ja = k_cache["J"][:3, 3:10]
+    det = np.linalg.det(Ja @ Ja.T)
+    vol = math.sqrt(det) if det >= 0 else float("nan")
+    vol = 1e-5 if math.isnan(vol) else min(max(vol, 1e-5), 1e5)
+    c += 10.0 * (1.0 / vol) ** 2
+    return c
+
+
+def step(rob, x, u, dt):
+    q, v = x[:12].copy(), x[12:24].copy()
+    c, s = math.cos(q[2]), math.sin(q[2])
+    v[0] = c * u[0] - s * u[1]
+    v[1] = s * u[0] + c * u[1]
+    v[2] = u[2]
+    tau = np.zeros(12)
+    tau[3:10] = u[3:10]
+    a = np.linalg.solve(rob.mass_matrix(q), tau)
+    kc = kin(rob, q, v)     # computed before integration: the one-step lag
+    v = v + a * dt
+    q = q + v * dt
+    xn = x.copy()
+    xn[:12], xn[12:24] = q, v
+    return xn, kc
+
+
+def rollout(rob, x0, U, eps, dt, forecast, optimal=False):
+    x = x0.copy()
+    kc = kin(rob, x[:12], x[12:24])
+    J = 0.0
+    for k in range(U.shape[0]):
+        u = U[k] + (0.0 if eps is None else eps[k])
+        sc = cost(x, kc, forecast[k])
+        if not optimal and math.isnan(sc):
+            return float("nan")
+        J += sc
+        if k < U.shape[0] - 1:
+            x, kc = step(rob, x, u, dt)
+    return J
+
+
+# ------------------------------------------------------------------------------------------
+# Savitzky-Golay (gram_savitzky_golay.cpp + filter.cpp)
+# ------------------------------------------------------------------------------------------
+def sg_weights(m, n):
+    """Least-squares polynomial smoothing weights at the centre of 2m+1 points (closed form via
+    a Vandermonde pseudo-inverse — a different route than the Gram-polynomial recursion)."""
+    x = np.arange(-m, m + 1, dtype=np.float64)
+    V = np.vander(x, n + 1, increasing=True)
+    return np.linalg.pinv(V)[0]
+
+
+class Window:
+    def __init__(self, H, w):
+        self.w, self.W = w, H + 2 * w + 1
+        self.uu = [0.0] * self.W
+        self.tt = [-1.0] * self.W
+        self.start = w
+        self.last = -1.0
+
+    def trim(self, t):
+        assert t >= self.last
+        self.last = t
+        ti = self.start
+        for i in range(self.start):
+            if self.tt[i] >= t:
+                ti = i
+                break
+        off = ti - self.w
+        self.tt = self.tt[off:] + self.tt[:off]
+        self.uu = self.uu[off:] + self.uu[:off]
+        if off > 0:
+            self.tt[self.W - off:] = [self.tt[self.W - off - 1]] * off
+            self.uu[self.W - off:] = [self.uu[self.W - off - 1]] * off
+        self.start = self.w
+        self.tt[self.w] = t
+
+    def add(self, u, t):
+        assert not t < self.tt[self.start]
+        for i in range(self.start, self.W):
+            self.uu[i], self.tt[i] = u, t
+        self.start += 1
+
+    def lower(self, t):
+        lo, hi = 0, self.W
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if self.tt[mid] < t:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo
+
+
+# ------------------------------------------------------------------------------------------
+# mppi::Trajectory (mppi.cpp) restated in Python
+# ------------------------------------------------------------------------------------------
+class MPPI:
+    def __init__(self, rob, S, K, H, dt, var, cmin, cmax, x0, smoothing=None):
+        self.rob, self.S, self.K, self.H, self.dt = rob, S, K, H, dt
+        self.R = S + 2
+        self.C = len(var)
+        self.noise = np.zeros((self.R, H, self.C))
+        self.cost = np.zeros(self.R)
+        self.w = np.zeros(self.R)
+        self.g = np.zeros((H, self.C))
+        self.U = np.zeros((H, self.C))
+        self.Us = np.zeros((H, self.C))
+        self.cmin, self.cmax = np.asarray(cmin), np.asarray(cmax)
+        self.last_shift = 0.0
+        self.windows = [Window(H, smoothing[0]) for _ in range(self.C)] if smoothing else None
+        self.sgw = sg_weights(*smoothing) if smoothing else None
+        self.opt_cost = 0.0
+
+    def draws(self, t):
+        sb = int((t - self.last_shift) / self.dt)
+        return (self.S - self.K) * self.H + (self.K * min(sb, self.H) if sb > 0 else 0)
+
+    def update(self, x0, t, eps, forecast):
+        it = iter(eps)
+        sb = int((t - self.last_shift) / self.dt)
+        if sb > 0:
+            self.last_shift = t
+            shifted = self.H - sb
+            self.Us[:shifted] = self.U[sb:]
+            self.Us[shifted:] = self.U[-1]
+        order = sorted(range(2, self.R), key=lambda r: (math.isnan(self.cost[r]), 0.0 if math.isnan(self.cost[r]) else self.cost[r], r))
+        keep, res = order[:self.K], order[self.K:]
+        if sb > 0:
+            for r in keep:
+                self.noise[r, :shifted] = self.noise[r, sb:].copy()
+                for k in range(shifted, self.H):
+                    self.noise[r, k] = next(it)
+        for r in res:
+            for k in range(self.H):
+                self.noise[r, k] = next(it)
+        self.noise[1] = -self.U
+        for r in range(self.R):
+            self.cost[r] = rollout(self.rob, x0, self.Us, self.noise[r], self.dt, forecast)
+        ok = ~np.isnan(self.cost)
+        mn, mx = self.cost[ok].min(), self.cost[ok].max()
+        if mx - mn >= 1e-6:
+            lik = np.where(ok, np.exp(-10.0 * (np.where(ok, self.cost, mn) - mn) / (mx - mn)), 0.0)
+            self.w = lik / lik.sum()
+            self.g = np.tensordot(self.w, self.noise, axes=1)
+            self.Us = self.Us + 2.0 * self.g
+            if self.windows:
+                for c, win in enumerate(self.windows):
+                    win.trim(t)
+                    for k in range(self.H):
+                        win.add(self.Us[k, c], t + k * self.dt)
+                    for k in range(self.H):
+                        tk = t + k * self.dt
+                        idx = win.lower(tk)
+                        v = np.array(win.uu[idx - win.w: idx + win.w + 1])
+                        r = float(self.sgw @ v)
+                        self.Us[k, c] = r
+                        win.uu[idx - 1] = r
+            self.Us = np.maximum(np.minimum(self.Us, self.cmax), self.cmin)
+        self.opt_cost = rollout(self.rob, x0, self.Us, None, self.dt, forecast, optimal=True)
+        self.U = self.Us.copy()
+
+
+VAR = np.array([0.1, 0.1, 0.2] + [7.5] * 7 + [0.0, 0.0])
+CMIN = np.array([-0.5, -0.5, -1.0] + [-100.0] * 7 + [-0.05, -0.05])
+CMAX = -CMIN
+
+
+def huddled():
+    x = np.zeros(31)
+    x[:12] = [0.2, 0.2, math.pi / 4, 0.0, math.pi / 5, 0.0, -math.pi / 2, 0.0, 2, math.pi / 4, 0.025, 0.025]
+    x[30] = 100.0
+    return x
+
+
+def gen_kinematics(rob, n=24, seed=1):
+    rng = np.random.default_rng(seed)
+    x0 = huddled()
+    qs, vs, taus, outs = [], [], [], []
+    for i in range(n):
+        q = x0[:12] + rng.normal(0, 0.6, 12) * (1 if i else 0)
+        q[10:] = np.abs(q[10:]) * 0.05 + 0.01
+        v = rng.normal(0, 1.0, 12)
+        tau = np.zeros(12)
+        tau[3:10] = rng.normal(0, 5.0, 7)
+        M = rob.mass_matrix(q)
+        a = np.linalg.solve(M, tau)
+        k = kin(rob, q, v)
+        fd = fd_world_velocity(rob, q, v, EE_LINK)
+        assert np.allclose(fd, k["vee"], atol=1e-6), (fd, k["vee"])
+        qs.append(q); vs.append(v); taus.append(tau)
+        outs.append(np.concatenate([a, k["ee"], k["am"], k["J"].reshape(-1), k["vee"], M.reshape(-1)]))
+    return np.array(qs), np.array(vs), np.array(taus), np.array(outs)
+
+
+def gen_updates(rob, S, K, H, updates, seed, smoothing=None):
+    dt = 0.01
+    m = MPPI(rob, S, K, H, dt, VAR, CMIN, CMAX, huddled(), smoothing)
+    rng = np.random.default_rng(seed)
+    sd = np.sqrt(VAR)
+    forecast = np.zeros((H, 6))
+    forecast[:, 0] = 20.0
+    x = huddled()
+    rec = {k: [] for k in ("eps", "costs", "weights", "gradient", "U", "opt_cost", "time")}
+    for j in range(updates):
+        t = 0.05 * j
+        n = m.draws(t)
+        eps = rng.standard_normal((n, 12)) * sd
+        m.update(x, t, eps, forecast)
+        rec["eps"].append(eps)
+        rec["costs"].append(m.cost.copy())
+        rec["weights"].append(m.w.copy())
+        rec["gradient"].append(m.g.copy())
+        rec["U"].append(m.U.copy())
+        rec["opt_cost"].append(m.opt_cost)
+        rec["time"].append(t)
+        print("  update %d: min cost %.6e argmin %d" % (j, np.nanmin(m.cost), int(np.nanargmin(m.cost))))
+    out = dict(S=S, K=K, H=H, x0=huddled(), forecast=forecast,
+               eps=np.concatenate(rec["eps"]), eps_counts=np.array([len(e) for e in rec["eps"]]),
+               costs=np.array(rec["costs"]), weights=np.array(rec["weights"]), gradient=np.array(rec["gradient"]),
+               U=np.array(rec["U"]), opt_cost=np.array(rec["opt_cost"]), time=np.array(rec["time"]),
+               smoothing=np.array(smoothing if smoothing else (0, 0)))
+    return out
+
+
+def main():
+    rob = Robot()
+    print("kinematics fixtures")
+    q, v, tau, out = gen_kinematics(rob)
+    np.savez_compressed(os.path.join(HERE, "kinematics.npz"), q=q, v=v, tau=tau, out=out)
+    print("SG weights")
+    np.savez_compressed(os.path.join(HERE, "sg_weights.npz"), w10_1=sg_weights(10, 1), w5_2=sg_weights(5, 2),
+                        w3_3=sg_weights(3, 3))
+    print("update fixtures: 16 x 8")
+    np.savez_compressed(os.path.join(HERE, "update_s16_h8.npz"), **gen_updates(rob, 16, 4, 8, 4, seed=21))
+    print("update fixtures: 24 x 16 with SG(4, 1)")
+    np.savez_compressed(os.path.join(HERE, "update_s24_h16_sg.npz"), **gen_updates(rob, 24, 6, 16, 4, seed=22, smoothing=(4, 1)))
+    if "--config1" in sys.argv:
+        print("update fixtures: config 1 (128 x 32)")
+        np.savez_compressed(os.path.join(HERE, "update_s128_h32.npz"), **gen_updates(rob, 128, 20, 32, 3, seed=12345))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+"""CPU tests: the oracle against the independent numpy golden vectors and physics identities.
+
+The reference cannot be built (no Eigen / Pinocchio), so the oracle is pinned by
+tests/golden/*.npz, produced by tests/golden/gen_golden.py: an unmerged-link numpy model with a
+composite-Jacobian mass matrix, LU solve and finite-difference frame velocities, plus an
+independent Python restatement of the MPPI update loop.
+"""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+
+import assistedmanipulation_amd as am
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def model():
+    return O.default_model()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kinematics_against_numpy_model(model, mode):
+    g = load("kinematics.npz")
+    for q, v, tau, out in zip(g["q"], g["v"], g["tau"], g["out"]):
+        k = O.kinematics(model, q, v, tau, mode)
+        a_ref = out[:12]
+        assert np.max(np.abs(k["a"] - a_ref)) <= 1e-9 * max(1.0, np.max(np.abs(a_ref))), (k["a"], a_ref)
+        np.testing.assert_allclose(k["ee"], out[12:15], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(k["arm_mount"], out[15:18], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(k["J"], out[18:90].reshape(6, 12), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(k["v_ee"], out[90:96], rtol=0, atol=1e-11)
+
+
+def test_aba_of_nle_is_zero(model):
+    """aba(q, v, nle(q, v)) = 0 — the reference's step reduces to M^-1 tau_u."""
+    rng = np.random.default_rng(4)
+    for _ in range(10):
+        q = am.huddled_state()[:12] + rng.normal(0, 0.5, 12)
+        v = rng.normal(0, 2.0, 12)
+        k = O.kinematics(model, q, v, np.zeros(12), 0)
+        assert np.max(np.abs(k["a"])) < 1e-9
+
+
+def test_gravity_torque_matches_potential_gradient(model):
+    """nle(q, 0) = dV/dq with V = sum m g z_com (numpy model, finite differences)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from gen_golden import Robot
+    rob = Robot()
+    q = am.huddled_state()[:12]
+
+    def V(qq):
+        e = 0.0
+        for link, (m, c, I) in rob.inertial.items():
+            T = rob.frame(qq, link)
+            e += m * 9.81 * (T[:3, 3] + T[:3, :3] @ c)[2]
+        return e
+    h = 1e-6
+    grad = np.array([(V(q + h * np.eye(12)[i]) - V(q - h * np.eye(12)[i])) / (2 * h) for i in range(12)])
+    k = O.kinematics(model, q, np.zeros(12), np.zeros(12), 0)
+    np.testing.assert_allclose(k["nle"], grad, rtol=0, atol=1e-6)
+
+
+def test_sg_weights_against_least_squares():
+    g = load("sg_weights.npz")
+    np.testing.assert_allclose(O.sg_weights(10, 0, 1, 0), g["w10_1"], rtol=0, atol=1e-14)
+    np.testing.assert_allclose(O.sg_weights(5, 0, 2, 0), g["w5_2"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(O.sg_weights(3, 0, 3, 0), g["w3_3"], rtol=0, atol=1e-13)
+    # window 10, order 1 (base.hpp:96-99) is the uniform 21-tap average (SURVEY finding 8)
+    np.testing.assert_allclose(g["w10_1"], np.full(21, 1 / 21), rtol=0, atol=1e-15)
+
+
+FIXTURES = ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s128_h32.npz"]
+
+
+@pytest.mark.parametrize("fixture", FIXTURES)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_full_updates_against_numpy_restatement(model, fixture, mode):
+    path = os.path.join(GOLDEN, fixture)
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated")
+    g = np.load(path, allow_pickle=False)
+    S, K, H = int(g["S"]), int(g["K"]), int(g["H"])
+    w, order = (int(x) for x in g["smoothing"])
+    conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=K,
+                                            smoothing=am.Smoothing(w, order) if w else None, threads=4)
+    assert conf.steps == H
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, am.FrankaRidgebackDynamics().descriptor(), am.AssistedManipulation().descriptor(),
+                             mode=mode, compat_uint8=1)
+    orc.set_forecast(g["forecast"])
+    offs = np.concatenate([[0], np.cumsum(g["eps_counts"])])
+    for j, t in enumerate(g["time"]):
+        assert orc.noise_draws(t) == g["eps_counts"][j]
+        orc.inject_noise(g["eps"][offs[j]:offs[j + 1]])
+        orc.update(g["x0"], float(t))
+        c = orc.costs()
+        np.testing.assert_allclose(c, g["costs"][j], rtol=1e-12, atol=0)
+        assert int(np.nanargmin(c)) == int(np.nanargmin(g["costs"][j]))
+        np.testing.assert_allclose(orc.weights(), g["weights"][j], rtol=0, atol=1e-10)
+        np.testing.assert_allclose(orc.gradient(), g["gradient"][j], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(orc.optimal_control(), g["U"][j], rtol=0, atol=1e-8)
+        assert abs(orc.optimal_cost() - g["opt_cost"][j]) <= 1e-12 * abs(g["opt_cost"][j])
+
+
+def test_flop_count_constant(model):
+    """bench.py's FLOPS_PER_ROLLOUT_STEP is the oracle's FLOP count of the minimal arithmetic."""
+    import bench
+    n = O.count_flops(model, O.default_cost(), am.huddled_state(), 64)
+    assert n == bench.FLOPS_PER_ROLLOUT_STEP
+
+
+def test_fp32_dynamics_diverge_fp64_do_not(model):
+    """The precision decision: fp32 rollouts flip barrier-breach counts; fp64 with a
+    different operation order does not."""
+    conf = am.frankaridgeback_configuration(rollouts=64, horison=0.32)
+    cc, keep = conf.to_c()
+    d, c = am.FrankaRidgebackDynamics().descriptor(), am.AssistedManipulation().descriptor()
+    trajs = [O.OracleTrajectory(cc, d, c, scalar=s, mode=m) for s, m in ((0, 0), (0, 1), (1, 1))]
+    rng = np.random.default_rng(12345)
+    sd = np.sqrt(np.diag(conf.covariance))
+    x = am.huddled_state()
+    worst64, worst32 = 0.0, 0.0
+    for t in trajs:
+        t.set_forecast(am.constant_forecast(t.H))
+    for j in range(4):
+        n = trajs[0].noise_draws(0.05 * j)
+        eps = rng.standard_normal((n, 12)) * sd
+        for t in trajs:
+            t.inject_noise(eps)
+            t.update(x, 0.05 * j)
+        ref = trajs[0].costs()
+        span = np.nanmax(ref) - np.nanmin(ref)
+        worst64 = max(worst64, np.nanmax(np.abs(trajs[1].costs() - ref)) / span)
+        worst32 = max(worst32, np.nanmax(np.abs(trajs[2].costs() - ref)) / span)
+    assert worst64 < 1e-12
+    assert worst32 > 1e-3

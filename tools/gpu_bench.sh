@@ -1,0 +1,7 @@
+# GPU bench + kernel-trace profile (run via gpurun from the repo root).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err && echo "bench ok" && cat gpurun_out/bench.json && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err && echo "prof ok" && find gpurun_out/prof -name '*stats*' | head
