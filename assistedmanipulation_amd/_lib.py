@@ -43,6 +43,7 @@ PROTOTYPES = {
     "mppi_device_costs": (C.c_void_p, [_h]),
     "mppi_device_gradient": (C.c_void_p, [_h]),
     "mppi_stream": (C.c_void_p, [_h]),
+    "mppi_synchronize": (C.c_int, [_h]),
     "mppi_get": (C.c_int, [_h, C.c_double, _dp]),
     "mppi_costs": (C.c_int, [_h, _dp]),
     "mppi_weights": (C.c_int, [_h, _dp]),

@@ -42,7 +42,10 @@ struct DeviceBuf {
 struct mppi_handle {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
+    bool opt_pending = false;
     float kernel_ms[5] = {0, 0, 0, 0, 0};
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
@@ -80,13 +83,14 @@ struct mppi_handle {
     StepConst *d_steps = nullptr;
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_weights = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
-    double *d_cmin = nullptr, *d_cmax = nullptr;
+    double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr;
     size_t inj_capacity = 0;   // doubles
     int *d_rank = nullptr;
     Status *d_status = nullptr;
     double *d_sg_w = nullptr, *d_sg_uu = nullptr, *d_sg_tt = nullptr, *d_sg_last = nullptr;
     int64_t *d_sg_start = nullptr;
     double *h_out = nullptr;     // pinned [HC + 8]
+    double *h_opt = nullptr;     // pinned: optimal cost copied back on the side stream
     double *h_stage = nullptr;   // pinned staging for the state
     std::vector<void *> allocations;
     std::string err;
@@ -408,9 +412,14 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 
     CREATE_TRY(hipSetDevice(device));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
     for (auto &e : h->ev) CREATE_TRY(hipEventCreate(&e));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_pub, hipEventDisableTiming));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
+    CREATE_TRY(hipEventCreate(&h->ev_opt_end));
     const size_t HC = (size_t)(h->H * h->C);
     CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
+    CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_U, HC));
     CREATE_TRY(dalloc(h, &h->d_Us, HC));
     CREATE_TRY(dalloc(h, &h->d_costs, (size_t)h->R));
@@ -427,6 +436,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_steps, (size_t)h->H));
     CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocDefault));
     CREATE_TRY(hipHostMalloc((void **)&h->h_stage, 64 * sizeof(double), hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc((void **)&h->h_opt, 8 * sizeof(double), hipHostMallocDefault));
+    h->h_opt[0] = 0.0;
     CREATE_TRY(hipMemcpy(h->d_T, h->T.data(), h->T.size() * sizeof(double), hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_cmin, h->cmin.data(), (size_t)Cd * sizeof(double), hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_cmax, h->cmax.data(), (size_t)Cd * sizeof(double), hipMemcpyHostToDevice));
@@ -531,10 +542,16 @@ void mppi_destroy(mppi_handle *h)
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->h_stage) (void)hipHostFree(h->h_stage);
+    if (h->h_opt) (void)hipHostFree(h->h_opt);
+    if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
+    if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
+    if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
+    if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -619,6 +636,7 @@ mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6)
     if (wrench_Hx6) h->forecast.assign(wrench_Hx6, wrench_Hx6 + 6 * h->H);
     else h->forecast.clear();
     HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream_opt));   // the pending optimal rollout reads d_steps
     return upload_steps(h);
 }
 
@@ -759,45 +777,56 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     f.sg_last_trim = h->d_sg_last;
     HIP_TRY(launch_finish(f, h->stream));
     HIP_TRY(hipEventRecord(h->ev[3], h->stream));
-    // filter(): cost of the optimal control (mppi.cpp:450-479)
+    const int HC = (int)(h->H * h->C);
+    // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+    HIP_TRY(launch_publish(h->d_Us, h->d_U, HC, h->d_opt, h->d_status, h->d_out, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->d_x0_opt, h->d_x0, (size_t)h->X * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
+    // filter(): cost of the published U* (mppi.cpp:450-479) on the side stream
+    HIP_TRY(hipStreamWaitEvent(h->stream_opt, h->ev_pub, 0));
+    HIP_TRY(hipEventRecord(h->ev[4], h->stream_opt));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         FrRolloutArgs a{};
         a.model = h->d_model;
         a.cost = h->d_cost;
         a.steps = h->d_steps;
-        a.x0 = h->d_x0;
-        a.Ushift = h->d_Us;
+        a.x0 = h->d_x0_opt;
+        a.Ushift = h->d_U;
         a.Uprev = h->d_U;
         a.cost_out = h->d_opt;
+        a.status = h->d_status;
         a.count = 1;
         a.Rpad = 64;
         a.dt = h->dt;
         a.H = (int)h->H;
         a.optimal = 1;
-        HIP_TRY(launch_fr_rollout(a, h->stream));
+        HIP_TRY(launch_fr_rollout(a, h->stream_opt));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
         a.steps = h->d_steps;
-        a.x0 = h->d_x0;
-        a.Ushift = h->d_Us;
+        a.x0 = h->d_x0_opt;
+        a.Ushift = h->d_U;
         a.Uprev = h->d_U;
         a.cost_out = h->d_opt;
+        a.status = h->d_status;
         a.count = 1;
         a.Rpad = 64;
         a.dt = h->dt;
         a.H = (int)h->H;
         a.optimal = 1;
-        HIP_TRY(launch_pm_rollout(a, h->stream));
+        HIP_TRY(launch_pm_rollout(a, h->stream_opt));
     }
-    HIP_TRY(hipEventRecord(h->ev[4], h->stream));
-    const int HC = (int)(h->H * h->C);
-    HIP_TRY(launch_publish(h->d_Us, h->d_U, HC, h->d_opt, h->d_status, h->d_out, h->stream));
-    HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipEventRecord(h->ev_opt_end, h->stream_opt));
+    HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream_opt));
+    HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream_opt));
+    h->opt_pending = true;
     HIP_TRY(hipEventRecord(h->ev[5], h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->phase_open = false;
-    for (int i = 0; i < 4; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
+    for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
     (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
@@ -807,7 +836,6 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         std::lock_guard<std::mutex> lock(h->mtx);   // publish under lock (mppi.cpp:178-182)
         h->last_rollout_time = h->rollout_time;
         std::memcpy(h->U_host.data(), h->h_out, (size_t)HC * sizeof(double));
-        h->opt_cost = h->h_out[HC];
     }
     h->update_duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - h->t_start).count();
     h->update_last = h->rollout_time;
@@ -883,9 +911,29 @@ mppi_status mppi_optimal_control(mppi_handle *h, double *out)
     return MPPI_OK;
 }
 
+static mppi_status wait_optimal(mppi_handle *h)
+{
+    if (!h->opt_pending) return MPPI_OK;
+    HIP_TRY(hipEventSynchronize(h->ev_opt_done));
+    (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
+    h->opt_cost = h->h_opt[0];
+    h->opt_pending = false;
+    return MPPI_OK;
+}
+
+mppi_status mppi_synchronize(mppi_handle *h)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return wait_optimal(h);
+}
+
 mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
 {
     if (!h || !cost) return MPPI_ERR_INVALID;
+    mppi_status st = wait_optimal(h);
+    if (st != MPPI_OK) return st;
     std::lock_guard<std::mutex> lock(h->mtx);
     *cost = h->opt_cost;
     return MPPI_OK;
@@ -953,6 +1001,8 @@ mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64
 mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
 {
     if (!h || !ms5) return MPPI_ERR_INVALID;
+    mppi_status st = wait_optimal(h);
+    if (st != MPPI_OK) return st;
     std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
     return MPPI_OK;
 }

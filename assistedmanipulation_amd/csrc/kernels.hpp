@@ -29,6 +29,7 @@ struct FrRolloutArgs {
     const double *inj;        // injected eps stream [draws][C]
     const double *T;          // [C][C] noise transform (row-major)
     double *cost_out;         // [R] (global index) or the optimal-cost scalar
+    const Status *status;     // optimal mode: skipped when the update failed (no filter())
     SampleParams sp;
     int64_t begin, count, Rpad;
     double dt;
@@ -47,6 +48,7 @@ struct PmRolloutArgs {
     const double *inj;
     const double *T;
     double *cost_out;
+    const Status *status;
     SampleParams sp;
     int64_t begin, count, Rpad;
     double dt;

@@ -235,6 +235,10 @@ class Trajectory:
         self._update_last = float(time)
         self._update_count += 1
 
+    def synchronize(self):
+        """Wait for all device work of this handle (including the overlapped filter())."""
+        self._check(self._L.mppi_synchronize(self._h))
+
     def update_phase1(self, state, time):
         s = np.ascontiguousarray(state, dtype=np.float64)
         self._check(self._L.mppi_update_phase1(self._h, _p(s), float(time)))

@@ -264,6 +264,11 @@ void *mppi_device_costs(mppi_handle *h);     /* R doubles */
 void *mppi_device_gradient(mppi_handle *h);  /* C*H doubles */
 void *mppi_stream(mppi_handle *h);           /* hipStream_t */
 
+/* filter() (the optimal rollout, mppi.cpp:450-479) runs on a side stream overlapped with the
+ * next update's sampling and rollouts; mppi_optimal_cost and mppi_kernel_times wait for it,
+ * and mppi_synchronize waits for all device work of the handle. */
+mppi_status mppi_synchronize(mppi_handle *h);
+
 /* Trajectory::get (mppi.cpp:481-512): thread-safe against a concurrent update(). */
 mppi_status mppi_get(mppi_handle *h, double time, double *control);
 
