@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -83,7 +84,8 @@ struct mppi_handle {
     StepConst *d_steps = nullptr;
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_weights = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
-    double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr;
+    double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
+    bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
     size_t inj_capacity = 0;   // doubles
     int *d_rank = nullptr;
     Status *d_status = nullptr;
@@ -396,6 +398,10 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     h->begin = 0;
     h->count = h->R;
     h->U_host.assign((size_t)(h->H * h->C), 0.0);
+    {
+        const char *kv = std::getenv("MPPI_FR_KERNEL");
+        h->coop = !(kv && std::string(kv) == "lane");
+    }
     noise_transform((int)Cd, cfg->covariance, h->T, h->tdiag);
     if (h->H < 1 || h->H > (1 << 20)) { delete h; return fail(nullptr, MPPI_ERR_INVALID, "horizon steps out of range"); }
 
@@ -426,6 +432,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_weights, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
+    CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
     CREATE_TRY(dalloc(h, &h->d_out, HC + 8));
@@ -712,7 +719,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.dt = h->dt;
         a.H = (int)h->H;
         a.optimal = 0;
-        HIP_TRY(launch_fr_rollout(a, h->stream));
+        a.status = h->d_status;
+        HIP_TRY(h->coop ? launch_fr_coop(a, h->stream) : launch_fr_rollout(a, h->stream));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -745,8 +753,8 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
-    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)(h->H * h->C), h->d_status, h->d_gpart,
-                            h->stream));
+    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
+                            h->d_gsplit, h->d_gpart, h->stream));
     return MPPI_OK;
 }
 
@@ -802,7 +810,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         a.dt = h->dt;
         a.H = (int)h->H;
         a.optimal = 1;
-        HIP_TRY(launch_fr_rollout(a, h->stream_opt));
+        HIP_TRY(h->coop ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -969,9 +977,10 @@ mppi_status mppi_noise(mppi_handle *h, double *out)
     std::vector<double> dev((size_t)(HC * h->Rpad));
     HIP_TRY(hipMemcpy(dev.data(), h->d_noise, dev.size() * sizeof(double), hipMemcpyDeviceToHost));
     std::memset(out, 0, (size_t)(h->R * HC) * sizeof(double));
-    for (int64_t lr = 0; lr < h->count; lr++) {
+    for (int64_t lr = 0; lr < h->count; lr++) {   // device [H][Rpad][C] -> reference [R][H][C]
         double *o = out + (h->begin + lr) * HC;
-        for (int64_t j = 0; j < HC; j++) o[j] = dev[(size_t)(j * h->Rpad + lr)];
+        for (int64_t k = 0; k < h->H; k++)
+            for (int64_t c = 0; c < h->C; c++) o[k * h->C + c] = dev[(size_t)((k * h->Rpad + lr) * h->C + c)];
     }
     return MPPI_OK;
 }

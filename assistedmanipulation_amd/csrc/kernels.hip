@@ -476,12 +476,12 @@ __device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, 
     if (rank < P.keep) {
         if (P.shift_by > 0) {
             if (k < P.shifted) {
-                for (int c = 0; c < C; c++) eps[c] = noise[((k + P.shift_by) * C + c) * Rpad + lr];
+                for (int c = 0; c < C; c++) eps[c] = noise[((k + P.shift_by) * Rpad + lr) * C + c];
                 return;
             }
             draw = (int64_t)rank * (H - P.shifted) + (k - P.shifted);
         } else {
-            for (int c = 0; c < C; c++) eps[c] = noise[(k * C + c) * Rpad + lr];
+            for (int c = 0; c < C; c++) eps[c] = noise[(k * Rpad + lr) * C + c];
             return;
         }
     } else {
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
         } else if (live) {
             sample_column(a.sp, g, rank, k, H, FR_C, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
 #pragma unroll
-            for (int c = 0; c < FR_C; c++) a.noise[((int64_t)k * FR_C + c) * a.Rpad + lr] = eps[c];
+            for (int c = 0; c < FR_C; c++) a.noise[((int64_t)k * a.Rpad + lr) * FR_C + c] = eps[c];
         }
         if (!alive) continue;
         const StepConst &sc = *opaque(&a.steps[k]);
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
             eps[0] = eps[1] = eps[2] = 0.0;
         } else {
             sample_column(a.sp, g, rank, k, a.H, 3, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
-            for (int c = 0; c < 3; c++) a.noise[((int64_t)k * 3 + c) * a.Rpad + lr] = eps[c];
+            for (int c = 0; c < 3; c++) a.noise[((int64_t)k * a.Rpad + lr) * 3 + c] = eps[c];
         }
         if (!alive) continue;
         double u[3];
@@ -728,26 +728,51 @@ __global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict_
     if (t == 0) { status->all_nan = 0; status->early = 0; status->minimum = minimum; status->maximum = maximum; status->total = total; }
 }
 
-// Partial gradient over the local shard: gpart[k*C + c] = sum_lr w[begin+lr] eps[k][c][lr]
-// (mppi.cpp:415-418).  One workgroup of 256 per (k, c) row; the row is contiguous in HBM.
+// Partial gradient over the local shard (mppi.cpp:415-418), noise layout [H][Rpad][C]:
+// stage 1, grid (H, GRAD_SPLIT): each block sums a contiguous range of rollouts of step k, one
+// rollout's C contiguous components per thread (coalesced 8*C-byte rows), into gsplit[s][k][c];
+// stage 2 adds the GRAD_SPLIT partials in a fixed order (deterministic, no atomics).
+template <int C>
 __global__ __launch_bounds__(256) void gradient_kernel(const double *__restrict__ noise, const double *__restrict__ weights,
-                                                       int64_t begin, int64_t count, int64_t Rpad, const Status *__restrict__ status,
-                                                       double *__restrict__ gpart)
+                                                       int64_t begin, int64_t count, int64_t Rpad, int H,
+                                                       const Status *__restrict__ status, double *__restrict__ gsplit)
 {
-    __shared__ double red[256];
+    __shared__ double red[256 * (C <= 4 ? 4 : 12)];
     if (status->early) return;
-    const int64_t row = blockIdx.x;
-    const double *n = noise + row * Rpad;
+    const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
+    const int64_t chunk = (count + ns - 1) / ns;
+    const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < count) ? r0 + chunk : count;
     const double *w = weights + begin;
-    double s = 0.0;
-    for (int64_t r = threadIdx.x; r < count; r += 256) s += w[r] * n[r];
-    red[threadIdx.x] = s;
+    double acc[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) acc[c] = 0.0;
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+        const double wr = w[r];
+        const double *n = noise + ((int64_t)k * Rpad + r) * C;
+#pragma unroll
+        for (int c = 0; c < C; c++) acc[c] += wr * n[c];
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++) red[c * 256 + threadIdx.x] = acc[c];
     __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h)
+#pragma unroll
+            for (int c = 0; c < C; c++) red[c * 256 + threadIdx.x] += red[c * 256 + threadIdx.x + h];
         __syncthreads();
     }
-    if (threadIdx.x == 0) gpart[row] = red[0];
+    if ((int)threadIdx.x < C) gsplit[((int64_t)s * H + k) * C + threadIdx.x] = red[threadIdx.x * 256];
+}
+
+__global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
+                                    double *__restrict__ gpart)
+{
+    if (status->early) return;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= HC) return;
+    double s = gsplit[t];
+    for (int i = 1; i < ns; i++) s += gsplit[(int64_t)i * HC + t];
+    gpart[t] = s;
 }
 
 // U* += step * gradient; Savitzky-Golay; clamp (mppi.cpp:421-447).  One workgroup.
@@ -895,9 +920,18 @@ hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, doub
 }
 
 hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int rows, const Status *status, double *gpart, hipStream_t s)
+                           int H, int C, const Status *status, double *gsplit, double *gpart, hipStream_t s)
 {
-    hipLaunchKernelGGL(gradient_kernel, dim3(rows), dim3(256), 0, s, noise, weights, begin, count, Rpad, status, gpart);
+    if (C == FR_C)
+        hipLaunchKernelGGL(gradient_kernel<FR_C>, dim3(H, GRAD_SPLIT), dim3(256), 0, s, noise, weights, begin, count, Rpad, H,
+                           status, gsplit);
+    else
+        hipLaunchKernelGGL(gradient_kernel<3>, dim3(H, GRAD_SPLIT), dim3(256), 0, s, noise, weights, begin, count, Rpad, H,
+                           status, gsplit);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int HC = H * C;
+    hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, gsplit, GRAD_SPLIT, HC, status, gpart);
     return hipGetLastError();
 }
 

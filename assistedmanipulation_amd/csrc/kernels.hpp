@@ -80,8 +80,10 @@ hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s);
+constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
 hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int rows, const Status *status, double *gpart, hipStream_t s);
+                           int H, int C, const Status *status, double *gsplit, double *gpart, hipStream_t s);
+hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
 hipError_t launch_publish(const double *Us, double *U, int HC, const double *opt_cost, const Status *status, double *out,
                           hipStream_t s);

@@ -156,7 +156,7 @@ def main():
                    "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
         "kernel_ms": {"sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
         "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
-                     "kernel": "fr_rollout_kernel", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
+                     "kernel": "fr_rollout_kernel" if os.environ.get("MPPI_FR_KERNEL") == "lane" else "fr_coop_kernel", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
                      "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP},
         "hbm": {"noise_tensor_GBs": BYTES_PER_ROLLOUT_STEP * count_local * traj.H / ((kt[1] + kt[2]) * 1e-3) / 1e9,
