@@ -82,7 +82,7 @@ struct mppi_handle {
     DevCost *d_cost = nullptr;
     DevPointMass *d_pm = nullptr;
     StepConst *d_steps = nullptr;
-    double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_weights = nullptr;
+    double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
@@ -286,10 +286,21 @@ mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
     return MPPI_OK;
 }
 
+void dfree(mppi_handle *h, double *&p)
+{
+    if (!p) return;
+    (void)hipFree(p);
+    h->allocations.erase(std::find(h->allocations.begin(), h->allocations.end(), (void *)p));
+    p = nullptr;
+}
+
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
+    dfree(h, h->d_noise);
+    dfree(h, h->d_noise_prev);
     h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
     HIP_TRY(dalloc(h, &h->d_noise, (size_t)(h->H * h->C * h->Rpad)));
+    HIP_TRY(dalloc(h, &h->d_noise_prev, (size_t)(h->H * h->C * h->Rpad)));
     return MPPI_OK;
 }
 
@@ -465,6 +476,14 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         std::memcpy(m.ee_p, d.end_effector.translation, sizeof(m.ee_p));
         std::memcpy(m.am_R, d.arm_mount.rotation, sizeof(m.am_R));
         std::memcpy(m.am_p, d.arm_mount.translation, sizeof(m.am_p));
+        {
+            const double *R10 = m.b[10].R, *R11 = m.b[11].R, *p10 = m.b[10].p, *p11 = m.b[11].p;
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++)
+                    m.f11_R[3 * r + c] = (R10[r] * R11[c] + R10[3 + r] * R11[3 + c]) + R10[6 + r] * R11[6 + c];
+                m.f11_p[r] = (R10[r] * (p11[0] - p10[0]) + R10[3 + r] * (p11[1] - p10[1])) + R10[6 + r] * (p11[2] - p10[2]);
+            }
+        }
         CREATE_TRY(dalloc(h, &h->d_model, 1));
         CREATE_TRY(hipMemcpy(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
         const mppi_assisted_manipulation_desc &a = cost->assisted_manipulation;
@@ -683,11 +702,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         const size_t need = (size_t)(draws * h->C);
         if (h->inj_pending.size() < need) return fail(h, MPPI_ERR_NOISE, "injected noise stream too short: need " + std::to_string(draws) + " columns");
         if (need > h->inj_capacity) {
-            if (h->d_inj) {
-                (void)hipFree(h->d_inj);
-                h->allocations.erase(std::find(h->allocations.begin(), h->allocations.end(), (void *)h->d_inj));
-                h->d_inj = nullptr;
-            }
+            dfree(h, h->d_inj);
             HIP_TRY(dalloc(h, &h->d_inj, need));
             h->inj_capacity = need;
         }
@@ -698,6 +713,23 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->stream));
     HIP_TRY(launch_shift(h->d_U, h->d_Us, (int)h->H, (int)h->C, h->shift_by, h->stream));
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
+    {   // eps of this update into the other buffer; the kept rollouts read the previous one
+        std::swap(h->d_noise, h->d_noise_prev);
+        SampleArgs sa{};
+        sa.rank = h->d_rank;
+        sa.Uprev = h->d_U;
+        sa.inj = h->d_inj;
+        sa.T = h->d_T;
+        sa.prev = h->d_noise_prev;
+        sa.noise = h->d_noise;
+        sa.sp = sp;
+        sa.begin = h->begin;
+        sa.count = h->count;
+        sa.Rpad = h->Rpad;
+        sa.H = (int)h->H;
+        sa.C = (int)h->C;
+        HIP_TRY(launch_sample(sa, h->stream));
+    }
     HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         FrRolloutArgs a{};
@@ -706,13 +738,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.steps = h->d_steps;
         a.x0 = h->d_x0;
         a.Ushift = h->d_Us;
-        a.Uprev = h->d_U;
         a.noise = h->d_noise;
-        a.rank = h->d_rank;
-        a.inj = h->d_inj;
-        a.T = h->d_T;
         a.cost_out = h->d_costs;
-        a.sp = sp;
         a.begin = h->begin;
         a.count = h->count;
         a.Rpad = h->Rpad;
@@ -727,13 +754,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.steps = h->d_steps;
         a.x0 = h->d_x0;
         a.Ushift = h->d_Us;
-        a.Uprev = h->d_U;
         a.noise = h->d_noise;
-        a.rank = h->d_rank;
-        a.inj = h->d_inj;
-        a.T = h->d_T;
         a.cost_out = h->d_costs;
-        a.sp = sp;
         a.begin = h->begin;
         a.count = h->count;
         a.Rpad = h->Rpad;
@@ -802,7 +824,6 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         a.steps = h->d_steps;
         a.x0 = h->d_x0_opt;
         a.Ushift = h->d_U;
-        a.Uprev = h->d_U;
         a.cost_out = h->d_opt;
         a.status = h->d_status;
         a.count = 1;
@@ -817,7 +838,6 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         a.steps = h->d_steps;
         a.x0 = h->d_x0_opt;
         a.Ushift = h->d_U;
-        a.Uprev = h->d_U;
         a.cost_out = h->d_opt;
         a.status = h->d_status;
         a.count = 1;

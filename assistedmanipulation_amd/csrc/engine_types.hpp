@@ -34,6 +34,9 @@ struct DevModel {
     DevBody b[FR_NB];
     double ee_R[9], ee_p[3];
     double am_R[9], am_p[3];
+    // placement of body 11 relative to body 10's placement, (R10^T R11, R10^T (p11 - p10)): the
+    // cooperative kernel's prefix scan reaches finger 11 through finger 10 (fr_coop.hip)
+    double f11_R[9], f11_p[3];
 };
 
 struct DevBarrier {

@@ -546,6 +546,29 @@ __global__ void shift_kernel(const double *__restrict__ U, double *__restrict__ 
     Us[t] = (k < shifted) ? U[(k + shift_by) * C + c] : U[(H - 1) * C + c];
 }
 
+// sample(): eps column k of local rollout lr (mppi.cpp:242-269).  Rollout 0 is the zero-noise
+// rollout; rollout 1 carries -U*; kept rollouts shift the previous update's eps; the rest draw.
+// grid (ceil(count / 256), H); consecutive threads write consecutive C-vectors of step k.
+template <int C>
+__global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
+{
+    const int64_t lr = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (lr >= a.count) return;
+    const int k = blockIdx.y;
+    const int64_t g = a.begin + lr;
+    double eps[C];
+    if (g == 0) {
+#pragma unroll
+        for (int c = 0; c < C; c++) eps[c] = 0.0;
+    } else {
+        const int rank = (g >= 2) ? a.rank[g] : 0;
+        sample_column(a.sp, g, rank, k, a.H, C, a.Uprev, a.inj, a.T, a.prev, a.Rpad, lr, eps);
+    }
+    double *o = a.noise + ((int64_t)k * a.Rpad + lr) * C;
+#pragma unroll
+    for (int c = 0; c < C; c++) o[c] = eps[c];
+}
+
 // ---------------------------------------------------------------------------------------------
 // FrankaRidgeback rollouts: one lane per rollout (first version).
 // ---------------------------------------------------------------------------------------------
@@ -561,7 +584,6 @@ __global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
     const DevModel &M = *a.model;
     const DevCost &Cs = *a.cost;
     const int H = a.H;
-    const int rank = (live && g >= 2) ? a.rank[g] : 0;
 
     double q[FR_NB], qd[FR_NB];
 #pragma unroll
@@ -575,14 +597,8 @@ __global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
     bool alive = live;
     for (int k = 0; k < H; k++) {
         double eps[FR_C];
-        if (a.optimal || g == 0) {
 #pragma unroll
-            for (int c = 0; c < FR_C; c++) eps[c] = 0.0;
-        } else if (live) {
-            sample_column(a.sp, g, rank, k, H, FR_C, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
-#pragma unroll
-            for (int c = 0; c < FR_C; c++) a.noise[((int64_t)k * a.Rpad + lr) * FR_C + c] = eps[c];
-        }
+        for (int c = 0; c < FR_C; c++) eps[c] = (a.optimal || !live) ? 0.0 : a.noise[((int64_t)k * a.Rpad + lr) * FR_C + c];
         if (!alive) continue;
         const StepConst &sc = *opaque(&a.steps[k]);
         const double step_cost = sc.gamma_k * fr_cost(Cs, sc, q, qd, kin);
@@ -627,7 +643,6 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
     if (lr >= a.count) return;
     if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;
     const int64_t g = a.optimal ? -1 : a.begin + lr;
-    const int rank = (g >= 2) ? a.rank[g] : 0;
     const DevPointMass &P = *a.pm;
     double x[6];
     for (int i = 0; i < 6; i++) x[i] = a.x0[i];
@@ -635,12 +650,7 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
     bool alive = true;
     for (int k = 0; k < a.H; k++) {
         double eps[3];
-        if (a.optimal || g == 0) {
-            eps[0] = eps[1] = eps[2] = 0.0;
-        } else {
-            sample_column(a.sp, g, rank, k, a.H, 3, a.Uprev, a.inj, a.T, a.noise, a.Rpad, lr, eps);
-            for (int c = 0; c < 3; c++) a.noise[((int64_t)k * a.Rpad + lr) * 3 + c] = eps[c];
-        }
+        for (int c = 0; c < 3; c++) eps[c] = a.optimal ? 0.0 : a.noise[((int64_t)k * a.Rpad + lr) * 3 + c];
         if (!alive) continue;
         double u[3];
         for (int c = 0; c < 3; c++) u[c] = a.Ushift[k * 3 + c] + eps[c];
@@ -894,6 +904,16 @@ hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift
 {
     const int n = H * C;
     hipLaunchKernelGGL(shift_kernel, dim3((n + 255) / 256), dim3(256), 0, s, U, Us, H, C, shift_by);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample(const SampleArgs &a, hipStream_t s)
+{
+    if (a.count <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.count + 255) / 256), (unsigned)a.H);
+    if (a.C == FR_C) hipLaunchKernelGGL(sample_kernel<FR_C>, grid, dim3(256), 0, s, a);
+    else if (a.C == 3) hipLaunchKernelGGL(sample_kernel<3>, grid, dim3(256), 0, s, a);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

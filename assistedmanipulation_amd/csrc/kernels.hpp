@@ -23,18 +23,26 @@ struct FrRolloutArgs {
     const StepConst *steps;   // [H]
     const double *x0;         // [X]
     const double *Ushift;     // [H][C]  U* shifted to this update
-    const double *Uprev;      // [H][C]  U* of the previous update (rollout 1 = -U*)
-    double *noise;            // [H][C][Rpad], local rollouts
-    const int *rank;          // [R] stable-order rank of rollouts 2..R-1
-    const double *inj;        // injected eps stream [draws][C]
-    const double *T;          // [C][C] noise transform (row-major)
+    const double *noise;      // [H][Rpad][C] eps of the local rollouts (sample_kernel)
     double *cost_out;         // [R] (global index) or the optimal-cost scalar
     const Status *status;     // optimal mode: skipped when the update failed (no filter())
-    SampleParams sp;
     int64_t begin, count, Rpad;
     double dt;
     int H;
     int optimal;
+};
+
+// sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
+struct SampleArgs {
+    const int *rank;          // [R] stable-order rank of rollouts 2..R-1
+    const double *Uprev;      // [H][C]  U* of the previous update (rollout 1 = -U*)
+    const double *inj;        // injected eps stream [draws][C]
+    const double *T;          // [C][C] noise transform (row-major)
+    const double *prev;       // [H][Rpad][C] eps of the previous update (kept rollouts shift it)
+    double *noise;            // [H][Rpad][C] eps of this update
+    SampleParams sp;
+    int64_t begin, count, Rpad;
+    int H, C;
 };
 
 struct PmRolloutArgs {
@@ -42,14 +50,9 @@ struct PmRolloutArgs {
     const StepConst *steps;
     const double *x0;
     const double *Ushift;
-    const double *Uprev;
-    double *noise;
-    const int *rank;
-    const double *inj;
-    const double *T;
+    const double *noise;      // [H][Rpad][3]
     double *cost_out;
     const Status *status;
-    SampleParams sp;
     int64_t begin, count, Rpad;
     double dt;
     int H;
@@ -77,6 +80,7 @@ struct FinishArgs {
 
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s);
 hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift_by, hipStream_t s);
+hipError_t launch_sample(const SampleArgs &a, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s);
