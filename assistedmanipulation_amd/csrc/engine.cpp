@@ -711,7 +711,6 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     }
     HIP_TRY(hipMemsetAsync(h->d_rank, 0, (size_t)h->R * sizeof(int), h->stream));
     HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->stream));
-    HIP_TRY(launch_shift(h->d_U, h->d_Us, (int)h->H, (int)h->C, h->shift_by, h->stream));
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
@@ -722,13 +721,14 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         sa.T = h->d_T;
         sa.prev = h->d_noise_prev;
         sa.noise = h->d_noise;
+        sa.Us = h->d_Us;
         sa.sp = sp;
         sa.begin = h->begin;
         sa.count = h->count;
         sa.Rpad = h->Rpad;
         sa.H = (int)h->H;
         sa.C = (int)h->C;
-        HIP_TRY(launch_sample(sa, h->stream));
+        HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
     }
     HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
@@ -775,8 +775,9 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
+    // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
-                            h->d_gsplit, h->d_gpart, h->stream));
+                            h->d_gsplit, h->d_gpart, h->world > 1, h->stream));
     return MPPI_OK;
 }
 
@@ -784,10 +785,14 @@ mppi_status mppi_update_phase3(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipMemsetAsync(&h->d_status->sg_error, 0, sizeof(int), h->stream));
+    const int HC = (int)(h->H * h->C);
+    // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     FinishArgs f{};
     f.status = h->d_status;
     f.status_w = h->d_status;
+    f.gsplit = h->d_gsplit;
+    f.ns = h->world > 1 ? 0 : GRAD_SPLIT;
     f.gpart = h->d_gpart;
     f.gradient = h->d_grad;
     f.Ushift = h->d_Us;
@@ -805,12 +810,11 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     f.sg_tt = h->d_sg_tt;
     f.sg_start = h->d_sg_start;
     f.sg_last_trim = h->d_sg_last;
+    f.U = h->d_U;
+    f.opt_cost = h->d_opt;
+    f.out = h->d_out;
     HIP_TRY(launch_finish(f, h->stream));
     HIP_TRY(hipEventRecord(h->ev[3], h->stream));
-    const int HC = (int)(h->H * h->C);
-    // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
-    HIP_TRY(launch_publish(h->d_Us, h->d_U, HC, h->d_opt, h->d_status, h->d_out, h->stream));
     HIP_TRY(hipMemcpyAsync(h->d_x0_opt, h->d_x0, (size_t)h->X * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipEventRecord(h->ev_pub, h->stream));

@@ -52,22 +52,25 @@ constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 stor
 // subspaces (6) per body slot.  Scratch array (a separate object, so the compiler may move the
 // backward pass's inertia reads over its scratch writes): U (per lane and body), 1/D and u
 // (row-uniform, per body), qdd and tau per body.
+// Row strides are 128 B modulo 256 B: ds_read_b64 serves lanes 0..31 (rows 0, 1) and 32..63 in
+// one bank cycle each with bank (a/4) mod 64, so rows 0/1 (2/3) must sit half a bank sweep apart.
 constexpr int L_I = 0;
 constexpr int L_S = 274;                    // 16-byte aligned
-constexpr int LDS_KIN = L_S + NSLOT * 6;    // 352
+constexpr int LDS_KIN = 368;                // >= L_S + NSLOT * 6, = 16 (mod 32) doubles
 constexpr int L_U = 0;
 constexpr int L_DU = L_U + FR_NB * ROW;
 constexpr int L_QDD = L_DU + FR_NB * 2;
 constexpr int L_TAU = L_QDD + ROW;
-constexpr int LDS_SCR = L_TAU + ROW;
-static_assert(L_I + NSLOT * 21 <= L_S, "inertia slots overlap S");
+constexpr int LDS_SCR = 272;                // >= L_TAU + ROW, = 16 (mod 32) doubles
+static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * 6 <= LDS_KIN && L_TAU + ROW <= LDS_SCR, "LDS row layout");
+static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16, "row stride bank offset");
 
 // Per-block body table (doubles per body): scan placement R p (body 11: relative to body 10),
 // mass, com, inertia, frame offset (EE on body 9, arm mount on body 2), the placement's
 // translation axis Ma = R a_t (prismatic joints; 0 for revolute), the joint axis a in the body
 // frame, and 1.0 for revolute joints.
 constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 25, T_AX = 28;   // [31]: 1.0 for revolute
-constexpr int MB = 32;
+constexpr int MB = 33;   // odd: lanes reading their own body's entry hit distinct banks
 constexpr int LDS_MODEL = FR_NB * MB;
 
 // ---- DPP helpers (fp64 as two dwords) ------------------------------------------------------

@@ -4,7 +4,7 @@
 // sequence issued by engine.cpp:
 //
 //   rank_kernel      stable order of the previous costs            (sample(), mppi.cpp:222-231)
-//   shift_kernel     U*_shifted <- shift(U*)                        (sample(), mppi.cpp:194-217)
+//   sample_kernel    eps of every (step, rollout); U*_shifted <- shift(U*) (sample(), mppi.cpp:189-270)
 //   fr_rollout_kernel / pm_rollout_kernel
 //                    per rollout: eps columns (kept-shift / fresh draw / -U*), fp64 horizon
 //                    rollout of the dynamics with the per-step cost fused, cost[r]
@@ -509,64 +509,115 @@ constexpr int FR_NT = 64;   // one wave per workgroup; the LDS stack takes 120 K
 // ---------------------------------------------------------------------------------------------
 // Rank of each sampled rollout (indices 2..R-1) in the stable order of the previous costs.
 // NaN sorts last (the reference's comparator is not a strict weak order with NaN: UB).
-// grid (ceil(S/256), ceil(S/256)), 256 threads; rank[] zeroed beforehand.
+// Costs become order-preserving 64-bit keys (-0 == +0, NaN above +inf); rank_i counts keys below
+// key_i plus equal keys at lower indices.  Grid (ceil(S/256), ceil(S/256)): block (x, y) ranks
+// its 256 rollouts against the 256 of tile y staged in LDS; off the diagonal tile the index
+// tie-break is block-uniform, so one compare per pair.  rank[] zeroed beforehand.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t cost_key(double c)
+{
+    const double z = c + 0.0;   // -0 -> +0
+    const uint64_t b = (uint64_t)__double_as_longlong(z);
+    const uint64_t k = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    return isnan(c) ? ~0ull : k;
+}
+
 __global__ __launch_bounds__(256) void rank_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
 {
-    __shared__ double kj[256];
+    __shared__ uint64_t kj[256];
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t j0 = (int64_t)blockIdx.y * 256;
     const int64_t jl = j0 + threadIdx.x;
-    kj[threadIdx.x] = (jl < S) ? cost[2 + jl] : 0.0;
+    kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
     __syncthreads();
     if (i >= S) return;
-    const double ki = cost[2 + i];
-    const bool ni = isnan(ki);
-    int cnt = 0;
+    const uint64_t ki = cost_key(cost[2 + i]);
     const int jn = (int)((S - j0) < 256 ? (S - j0) : 256);
-    for (int t = 0; t < jn; t++) {
-        const double k = kj[t];
-        const int64_t j = j0 + t;
-        const bool nj = isnan(k);
-        bool less;
-        if (ni) less = nj ? (j < i) : true;
-        else less = nj ? false : ((k < ki) || (k == ki && j < i));
-        cnt += less ? 1 : 0;
+    int cnt = 0;
+    if (blockIdx.y < blockIdx.x) {          // every j < i: equal keys count
+        for (int t = 0; t < jn; t++) cnt += (kj[t] <= ki) ? 1 : 0;
+    } else if (blockIdx.y > blockIdx.x) {   // every j > i
+        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki) ? 1 : 0;
+    } else {
+        const int il = threadIdx.x;
+        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki || (kj[t] == ki && t < il)) ? 1 : 0;
     }
     if (cnt) atomicAdd(&rank[2 + i], cnt);
 }
 
-// U*_shifted <- U* shifted left by shift_by with the last column replicated (mppi.cpp:197-207).
-__global__ void shift_kernel(const double *__restrict__ U, double *__restrict__ Us, int H, int C, int64_t shift_by)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= H * C || shift_by <= 0) return;
-    const int k = t / C, c = t % C;
-    const int64_t shifted = (H - shift_by) > 0 ? (H - shift_by) : 0;
-    Us[t] = (k < shifted) ? U[(k + shift_by) * C + c] : U[(H - 1) * C + c];
-}
 
 // sample(): eps column k of local rollout lr (mppi.cpp:242-269).  Rollout 0 is the zero-noise
 // rollout; rollout 1 carries -U*; kept rollouts shift the previous update's eps; the rest draw.
-// grid (ceil(count / 256), H); consecutive threads write consecutive C-vectors of step k.
-template <int C>
+// Diagonal noise transform: one thread per (step, rollout, Philox block of 4 components), so
+// consecutive threads write consecutive 32-byte pieces of step k's [Rpad][C] slab.  Full
+// transform: one thread per (step, rollout) (eps = T z needs all C normals of the draw).
+// grid (ceil(count * NB / 256), H).  Block (0, k) also writes U*_shifted row k (mppi.cpp:197-207).
+template <int C, bool DIAG>
 __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
 {
-    const int64_t lr = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (lr >= a.count) return;
+    constexpr int NB = DIAG ? (C + 3) / 4 : 1;   // thread pieces per (step, rollout)
     const int k = blockIdx.y;
+    if (blockIdx.x == 0 && a.sp.shift_by > 0 && (int)threadIdx.x < C) {
+        const int c = threadIdx.x;
+        const int64_t sh = a.sp.shift_by, kept = a.sp.shifted;
+        a.Us[k * C + c] = (k < kept) ? a.Uprev[(k + sh) * C + c] : a.Uprev[(a.H - 1) * C + c];
+    }
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t lr = tid / NB;
+    if (lr >= a.count) return;
+    const int blk = (int)(tid - lr * NB);
+    const int c0 = DIAG ? 4 * blk : 0;
+    constexpr int CW = DIAG ? (C < 4 ? C : 4) : C;
+    const int cw = DIAG ? ((C - c0) < 4 ? (C - c0) : 4) : C;
     const int64_t g = a.begin + lr;
-    double eps[C];
+    double eps[CW];
     if (g == 0) {
 #pragma unroll
-        for (int c = 0; c < C; c++) eps[c] = 0.0;
-    } else {
+        for (int c = 0; c < CW; c++) eps[c] = 0.0;
+    } else if (!DIAG) {
         const int rank = (g >= 2) ? a.rank[g] : 0;
         sample_column(a.sp, g, rank, k, a.H, C, a.Uprev, a.inj, a.T, a.prev, a.Rpad, lr, eps);
-    }
-    double *o = a.noise + ((int64_t)k * a.Rpad + lr) * C;
+    } else {
+        const SampleParams &P = a.sp;
+        int64_t draw = -1;
+        const double *src = nullptr;
+        double sgn = 1.0;
+        if (g == 1) {
+            src = a.Uprev + (int64_t)k * C + c0;
+            sgn = -1.0;
+        } else {
+            const int rank = a.rank[g];
+            if (rank < P.keep) {
+                if (P.shift_by > 0) {
+                    if (k < P.shifted) src = a.prev + (((int64_t)k + P.shift_by) * a.Rpad + lr) * C + c0;
+                    else draw = (int64_t)rank * (a.H - P.shifted) + (k - P.shifted);
+                } else {
+                    src = a.prev + ((int64_t)k * a.Rpad + lr) * C + c0;
+                }
+            } else {
+                draw = P.keep_draws + (int64_t)(rank - P.keep) * a.H + k;
+            }
+        }
+        if (src) {
 #pragma unroll
-    for (int c = 0; c < C; c++) o[c] = eps[c];
+            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? sgn * src[c] : 0.0;
+        } else if (P.injected) {
+#pragma unroll
+            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.inj[draw * C + c0 + c] : 0.0;
+        } else {
+            mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};
+            mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
+            float z[4];
+            mppi_dev::box_muller(r.x, r.y, z[0], z[1]);
+            mppi_dev::box_muller(r.z, r.w, z[2], z[3]);
+#pragma unroll
+            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.T[(c0 + c) * C + c0 + c] * (double)z[c] : 0.0;
+        }
+    }
+    double *o = a.noise + ((int64_t)k * a.Rpad + lr) * C + c0;
+#pragma unroll
+    for (int c = 0; c < CW; c++)
+        if (c < cw) o[c] = eps[c];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -678,37 +729,53 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
 // optimise(): min / max over non-NaN costs, status, softmin weights (mppi.cpp:344-408).
 // One workgroup of 1024 threads.
 // ---------------------------------------------------------------------------------------------
+// Block-wide reductions for one 1024-thread workgroup: wave butterflies, then 16 wave partials.
+__device__ __forceinline__ double wave_min(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = smin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = smax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict__ cost, int64_t R, double cost_scale,
                                                        double *__restrict__ weights, Status *__restrict__ status)
 {
-    __shared__ double smn[1024], smx[1024];
-    __shared__ long long scnt[1024];
-    const int t = threadIdx.x;
-    double mn = INFINITY, mx = -INFINITY;
-    long long cnt = 0;
+    __shared__ double smn[16], smx[16], ssum[16];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    double mn = INFINITY, mx = -INFINITY, cnt = 0.0;
     for (int64_t i = t; i < R; i += 1024) {
         const double c = cost[i];
         if (isnan(c)) continue;
-        cnt++;
+        cnt += 1.0;
         mn = (c < mn) ? c : mn;
         mx = (c > mx) ? c : mx;
     }
-    smn[t] = mn;
-    smx[t] = mx;
-    scnt[t] = cnt;
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    cnt = wave_sum(cnt);
+    if (l == 0) { smn[w] = mn; smx[w] = mx; ssum[w] = cnt; }
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (t < s) {
-            smn[t] = (smn[t + s] < smn[t]) ? smn[t + s] : smn[t];
-            smx[t] = (smx[t + s] > smx[t]) ? smx[t + s] : smx[t];
-            scnt[t] += scnt[t + s];
-        }
-        __syncthreads();
+    double minimum = smn[0], maximum = smx[0], valid = ssum[0];
+#pragma unroll
+    for (int i = 1; i < 16; i++) {
+        minimum = smin(minimum, smn[i]);
+        maximum = smax(maximum, smx[i]);
+        valid += ssum[i];
     }
-    const double minimum = smn[0], maximum = smx[0];
-    const long long valid = scnt[0];
     __syncthreads();
-    if (valid <= 1) {   // minmax_element over <= 1 element: it1 == it2 -> throw
+    if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
         if (t == 0) { status->all_nan = 1; status->early = 1; status->minimum = minimum; status->maximum = maximum; }
         return;
     }
@@ -720,20 +787,19 @@ __global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict_
     double tot = 0.0;
     for (int64_t i = t; i < R; i += 1024) {
         const double c = cost[i];
-        double l = 0.0;
+        double e = 0.0;
         if (!isnan(c)) {
-            l = exp(-cost_scale * (c - minimum) / difference);
-            tot += l;
+            e = exp(-cost_scale * (c - minimum) / difference);
+            tot += e;
         }
-        weights[i] = l;
+        weights[i] = e;
     }
-    smn[t] = tot;
+    tot = wave_sum(tot);
+    if (l == 0) ssum[w] = tot;
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (t < s) smn[t] += smn[t + s];
-        __syncthreads();
-    }
-    const double total = smn[0];
+    double total = ssum[0];
+#pragma unroll
+    for (int i = 1; i < 16; i++) total += ssum[i];
     for (int64_t i = t; i < R; i += 1024) weights[i] = weights[i] / total;
     if (t == 0) { status->all_nan = 0; status->early = 0; status->minimum = minimum; status->maximum = maximum; status->total = total; }
 }
@@ -789,12 +855,22 @@ __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, i
 // SG: one thread per control dimension runs its MovingExtendedWindow (filter.cpp:19-116).
 __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 {
+    __shared__ int sg_err;
     const Status &stt = *a.status;
-    if (stt.early) return;
     const int HC = a.H * a.C;
+    if (threadIdx.x == 0) sg_err = 0;
+    __syncthreads();
+    if (!stt.early) {
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
-        a.gradient[t] = a.gpart[t];
-        a.Ushift[t] += a.gpart[t] * a.gradient_step;
+        double g;
+        if (a.ns > 0) {   // stage 2 of the gradient, fixed order
+            g = a.gsplit[t];
+            for (int i = 1; i < a.ns; i++) g += a.gsplit[(int64_t)i * HC + t];
+        } else {
+            g = a.gpart[t];
+        }
+        a.gradient[t] = g;
+        a.Ushift[t] += g * a.gradient_step;
     }
     __syncthreads();
     if (a.sg_window > 0) {
@@ -852,7 +928,7 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
             }
             a.sg_start[c] = start_idx;
             a.sg_last_trim[c] = last_trim;
-            if (err) a.status_w->sg_error = 1;
+            if (err) sg_err = 1;
         }
         __syncthreads();
     }
@@ -865,27 +941,27 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
             a.Ushift[t] = u;
         }
     }
+    }
+    __syncthreads();
+    // publish (mppi.cpp:178-182): U* <- U*_shifted unless the update threw
+    const bool ok = !stt.all_nan && !sg_err;
+    for (int t = threadIdx.x; t < HC; t += blockDim.x) {
+        const double v = ok ? a.Ushift[t] : a.U[t];
+        if (ok) a.U[t] = v;
+        a.out[t] = v;
+    }
+    if (threadIdx.x == 0) {
+        a.status_w->sg_error = sg_err;
+        a.out[HC + 0] = *a.opt_cost;
+        a.out[HC + 1] = (double)stt.all_nan;
+        a.out[HC + 2] = (double)stt.early;
+        a.out[HC + 3] = (double)sg_err;
+        a.out[HC + 4] = stt.minimum;
+        a.out[HC + 5] = stt.maximum;
+    }
 }
 
-// Publish U* <- U*_shifted and pack the host-visible block [U (H*C), optimal cost, status].
-__global__ void publish_kernel(const double *__restrict__ Us, double *__restrict__ U, int HC, const double *__restrict__ opt_cost,
-                               const Status *__restrict__ status, double *__restrict__ out)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool ok = !status->all_nan && !status->sg_error;
-    if (t < HC) {
-        if (ok) U[t] = Us[t];
-        out[t] = ok ? Us[t] : U[t];
-    }
-    if (t == 0) {
-        out[HC + 0] = *opt_cost;
-        out[HC + 1] = (double)status->all_nan;
-        out[HC + 2] = (double)status->early;
-        out[HC + 3] = (double)status->sg_error;
-        out[HC + 4] = status->minimum;
-        out[HC + 5] = status->maximum;
-    }
-}
+
 
 // ---------------------------------------------------------------------------------------------
 // Launch wrappers (host).
@@ -900,20 +976,21 @@ hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift_by, hipStream_t s)
+hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s)
 {
-    const int n = H * C;
-    hipLaunchKernelGGL(shift_kernel, dim3((n + 255) / 256), dim3(256), 0, s, U, Us, H, C, shift_by);
-    return hipGetLastError();
-}
-
-hipError_t launch_sample(const SampleArgs &a, hipStream_t s)
-{
-    if (a.count <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((a.count + 255) / 256), (unsigned)a.H);
-    if (a.C == FR_C) hipLaunchKernelGGL(sample_kernel<FR_C>, grid, dim3(256), 0, s, a);
-    else if (a.C == 3) hipLaunchKernelGGL(sample_kernel<3>, grid, dim3(256), 0, s, a);
-    else return hipErrorInvalidValue;
+    if (a.count <= 0 && a.sp.shift_by <= 0) return hipSuccess;
+    const int nb = tdiag ? (a.C + 3) / 4 : 1;
+    const int64_t nx = (a.count * nb + 255) / 256;
+    const dim3 grid((unsigned)(nx > 0 ? nx : 1), (unsigned)a.H);
+    if (a.C == FR_C) {
+        if (tdiag) hipLaunchKernelGGL((sample_kernel<FR_C, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((sample_kernel<FR_C, false>), grid, dim3(256), 0, s, a);
+    } else if (a.C == 3) {
+        if (tdiag) hipLaunchKernelGGL((sample_kernel<3, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((sample_kernel<3, false>), grid, dim3(256), 0, s, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -940,7 +1017,7 @@ hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, doub
 }
 
 hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int H, int C, const Status *status, double *gsplit, double *gpart, hipStream_t s)
+                           int H, int C, const Status *status, double *gsplit, double *gpart, bool sum_splits, hipStream_t s)
 {
     if (C == FR_C)
         hipLaunchKernelGGL(gradient_kernel<FR_C>, dim3(H, GRAD_SPLIT), dim3(256), 0, s, noise, weights, begin, count, Rpad, H,
@@ -950,6 +1027,7 @@ hipError_t launch_gradient(const double *noise, const double *weights, int64_t b
                            status, gsplit);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (!sum_splits) return hipSuccess;   // finish_kernel adds the splits itself
     const int HC = H * C;
     hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, gsplit, GRAD_SPLIT, HC, status, gpart);
     return hipGetLastError();
@@ -961,11 +1039,5 @@ hipError_t launch_finish(const FinishArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_publish(const double *Us, double *U, int HC, const double *opt_cost, const Status *status, double *out,
-                          hipStream_t s)
-{
-    hipLaunchKernelGGL(publish_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, Us, U, HC, opt_cost, status, out);
-    return hipGetLastError();
-}
 
 }  // namespace mppi_eng

@@ -40,6 +40,7 @@ struct SampleArgs {
     const double *T;          // [C][C] noise transform (row-major)
     const double *prev;       // [H][Rpad][C] eps of the previous update (kept rollouts shift it)
     double *noise;            // [H][Rpad][C] eps of this update
+    double *Us;               // [H][C] U*_shifted, written when shift_by > 0
     SampleParams sp;
     int64_t begin, count, Rpad;
     int H, C;
@@ -62,7 +63,9 @@ struct PmRolloutArgs {
 struct FinishArgs {
     const Status *status;
     Status *status_w;
-    const double *gpart;
+    const double *gsplit;       // [ns][H][C] gradient stage-1 partials (ns > 0: summed here)
+    int ns;
+    const double *gpart;        // [H][C] summed (all-reduced when sharded) gradient, ns == 0
     double *gradient;
     double *Ushift;
     const double *cmin, *cmax;
@@ -76,20 +79,22 @@ struct FinishArgs {
     double *sg_uu, *sg_tt;      // [C][H + 2w + 1]
     int64_t *sg_start;          // [C]
     double *sg_last_trim;       // [C]
+    // publish: U* <- U*_shifted and the host-visible block [U (H*C), optimal cost, status]
+    double *U;
+    const double *opt_cost;
+    double *out;
 };
 
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s);
-hipError_t launch_shift(const double *U, double *Us, int H, int C, int64_t shift_by, hipStream_t s);
-hipError_t launch_sample(const SampleArgs &a, hipStream_t s);
+hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s);
 constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
 hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int H, int C, const Status *status, double *gsplit, double *gpart, hipStream_t s);
+                           int H, int C, const Status *status, double *gsplit, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
-hipError_t launch_publish(const double *Us, double *U, int HC, const double *opt_cost, const Status *status, double *out,
-                          hipStream_t s);
+
 
 }  // namespace mppi_eng
