@@ -56,6 +56,7 @@ PROTOTYPES = {
     "mppi_dims": (C.c_int, [_h, _i64p, _i64p, _i64p, _i64p]),
     "mppi_smoothing_windows": (C.c_int, [_h, _dp, _dp, _i64p]),
     "mppi_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float)]),
+    "mppi_kernel_times_nowait": (C.c_int, [_h, C.POINTER(C.c_float)]),
 }
 
 _lib = None

@@ -1040,4 +1040,13 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
     return MPPI_OK;
 }
 
+mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
+{
+    if (!h || !ms5) return MPPI_ERR_INVALID;
+    if (h->opt_pending && hipEventQuery(h->ev_opt_end) == hipSuccess)
+        (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
+    std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
+    return MPPI_OK;
+}
+
 }  // extern "C"

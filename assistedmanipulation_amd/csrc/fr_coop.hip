@@ -68,10 +68,13 @@ static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16, "row stride bank offset"
 // Per-block body table (doubles per body): scan placement R p (body 11: relative to body 10),
 // mass, com, inertia, frame offset (EE on body 9, arm mount on body 2), the placement's
 // translation axis Ma = R a_t (prismatic joints; 0 for revolute), the joint axis a in the body
-// frame, and 1.0 for revolute joints.
-constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 25, T_AX = 28;   // [31]: 1.0 for revolute
-constexpr int MB = 33;   // odd: lanes reading their own body's entry hit distinct banks
-constexpr int LDS_MODEL = FR_NB * MB;
+// frame, 1/0 for revolute / prismatic (and its complement), the joint-limit barriers and the
+// velocity weight of the cost, and the lane masks of the kinematic sums.  Row 12 serves lanes
+// 12..15: body 0's geometry with every mask and weight zero.
+constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 25, T_AX = 28, T_ROT = 31, T_NROT = 32;
+constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42;
+constexpr int MB = 43;   // odd: lanes reading their own body's entry hit distinct banks
+constexpr int LDS_MODEL = (FR_NB + 1) * MB;
 
 // ---- DPP helpers (fp64 as two dwords) ------------------------------------------------------
 // mov_dpp with bound_ctrl: lanes whose source lies outside the row read 0.
@@ -82,8 +85,9 @@ __device__ __forceinline__ double dmov(double x)
     const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
+// row_newbcast:N as one v_mov_b64_dpp (gfx950's 64-bit DPP supports row_newbcast only)
 template <int N>
-__device__ __forceinline__ double bcast(double x) { return dmov<0x150 + N>(x); }   // row_newbcast:N
+__device__ __forceinline__ double bcast(double x) { return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + N, 0xF, 0xF, true); }
 template <int S>
 __device__ __forceinline__ double shr(double x) { return dmov<0x110 + S>(x); }     // row_shr:S
 
@@ -224,13 +228,9 @@ __device__ __forceinline__ double manipulability_term(const DevCost &Cs, const d
     return (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
 }
 
-// Lane-constant data of the row's body j.
+// Lane-constant data of the row's body j (the doubles live in the body table).
 struct LaneConst {
-    double rz_c, rz_s;        // rotation flag as selects: (cos, sin) taken from sincos for revolute
-    double rotf, nrotf;       // 1/0 and 0/1 for revolute lanes
-    double fix11;             // -1 on lane 11 (finger 11 reaches body 9 through finger 10)
-    double wv, wa;            // frame-velocity (EE chain) and arm-Jacobian lane masks
-    int slot;                 // LDS body slot (dummy for lanes 12..15)
+    int slot;       // LDS body slot (dummy for lanes 12..15)
     bool is_rz;
 };
 
@@ -249,7 +249,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         D[3 * r + 2] = M[T_R + 3 * r + 2];
         p[r] = M[T_P + r] + M[T_MA + r] * q;
     }
-    p[1] = p[1] + L.fix11 * qprev;
+    p[1] = p[1] + M[T_FIX] * qprev;
     D[0] -= 1.0;
     D[4] -= 1.0;
     D[8] -= 1.0;
@@ -267,12 +267,13 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     double w[3], S[6];
 #pragma unroll
     for (int r = 0; r < 3; r++) w[r] = (R[3 * r] * M[T_AX] + R[3 * r + 1] * M[T_AX + 1]) + R[3 * r + 2] * M[T_AX + 2];
-    S[0] = (p[1] * w[2] - p[2] * w[1]) * L.rotf + w[0] * L.nrotf;
-    S[1] = (p[2] * w[0] - p[0] * w[2]) * L.rotf + w[1] * L.nrotf;
-    S[2] = (p[0] * w[1] - p[1] * w[0]) * L.rotf + w[2] * L.nrotf;
-    S[3] = w[0] * L.rotf;
-    S[4] = w[1] * L.rotf;
-    S[5] = w[2] * L.rotf;
+    const double rotf = M[T_ROT], nrotf = M[T_NROT];
+    S[0] = (p[1] * w[2] - p[2] * w[1]) * rotf + w[0] * nrotf;
+    S[1] = (p[2] * w[0] - p[0] * w[2]) * rotf + w[1] * nrotf;
+    S[2] = (p[0] * w[1] - p[1] * w[0]) * rotf + w[2] * nrotf;
+    S[3] = w[0] * rotf;
+    S[4] = w[1] * rotf;
+    S[5] = w[2] * rotf;
     world_inertia_to_lds(M, R, p, Lk + L_I + L.slot * 21);
 #pragma unroll
     for (int k = 0; k < 6; k++) Lk[L_S + L.slot * 6 + k] = S[k];
@@ -284,11 +285,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
-    const double wq = L.wv * qd;
+    const double wq = M[T_WV] * qd;
     double vl[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) vl[k] = rsum16(S[k] * wq);
-    const double w0 = L.wa * S[0], w1 = L.wa * S[1], w2 = L.wa * S[2];
+    const double wa = M[T_WA];
+    const double w0 = wa * S[0], w1 = wa * S[1], w2 = wa * S[2];
     double jj[6];
     jj[0] = rsum16(w0 * S[0]);
     jj[1] = rsum16(w0 * S[1]);
@@ -313,37 +315,49 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
     int off[6];
 #pragma unroll
     for (int c = 0; c < 6; c++) off[c] = pidx(r, c);
+    // operands of the next level are loaded one level ahead (LDS latency off the chain)
+    double An[6], Sn[6], Srn, taun;
+    auto fetch = [&](int i) {
+        const double *Ii = Lk + L_I + i * 21;
+        const double *Si = Lk + L_S + i * 6;
+#pragma unroll
+        for (int k = 0; k < 6; k++) An[k] = Ii[off[k]];
+#pragma unroll
+        for (int k = 0; k < 6; k++) Sn[k] = Si[k];
+        Srn = Si[r];
+        taun = Lw[L_TAU + i];
+    };
+    fetch(FR_NB - 1);
     double C[6], pA = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; k++) C[k] = 0.0;
 #pragma unroll
     for (int i = FR_NB - 1; i >= 0; i--) {
-        const double *Ii = Lk + L_I + i * 21;
-        const double *Si = Lk + L_S + i * 6;
         double A[6], S[6];
 #pragma unroll
-        for (int k = 0; k < 6; k++) S[k] = Si[k];
-        const double Sr = Si[r];
-        if (i >= 10) {
-#pragma unroll
-            for (int k = 0; k < 6; k++) A[k] = Ii[off[k]];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 6; k++) A[k] = Ii[off[k]] + C[k];
+        for (int k = 0; k < 6; k++) {
+            A[k] = (i >= 10) ? An[k] : An[k] + C[k];
+            S[k] = Sn[k];
         }
+        const double Sr = Srn, tau = taun;
+        if (i > 0) fetch(i - 1);
         const double pAr = (i >= 10) ? 0.0 : pA;
         const double U = ((A[0] * S[0] + A[1] * S[1]) + (A[2] * S[2] + A[3] * S[3])) + (A[4] * S[4] + A[5] * S[5]);
         const double D = rsum8(rmask * (Sr * U));
         const double sp = rsum8(rmask * (Sr * pAr));
         const double Dinv = frcp(D);
-        const double u = Lw[L_TAU + i] - sp;
+        const double u = tau - sp;
         Lw[L_U + i * ROW + j] = U;
         Lw[L_DU + 2 * i] = Dinv;
         Lw[L_DU + 2 * i + 1] = u;
         if (i > 0) {
             double Uall[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) Uall[k] = Lw[L_U + i * ROW + k];
+            Uall[0] = bcast<0>(U);
+            Uall[1] = bcast<1>(U);
+            Uall[2] = bcast<2>(U);
+            Uall[3] = bcast<3>(U);
+            Uall[4] = bcast<4>(U);
+            Uall[5] = bcast<5>(U);
             const double Ud = U * Dinv;
             const double ud = u * Dinv;
             if (i == 10) {
@@ -358,12 +372,19 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
         }
     }
     double acc = 0.0, a9 = 0.0;
+    double Srf = Lk[L_S + r], Uf = Lw[L_U + j], Dvf = Lw[L_DU], uf = Lw[L_DU + 1];
 #pragma unroll
     for (int i = 0; i < FR_NB; i++) {
+        const double Sr = Srf, Ui = Uf, Dv = Dvf, ui = uf;
+        if (i + 1 < FR_NB) {
+            Srf = Lk[L_S + (i + 1) * 6 + r];
+            Uf = Lw[L_U + (i + 1) * ROW + j];
+            Dvf = Lw[L_DU + 2 * (i + 1)];
+            uf = Lw[L_DU + 2 * (i + 1) + 1];
+        }
         const double ap = (i == 11) ? a9 : acc;
-        const double Sr = Lk[L_S + i * 6 + r];
-        const double ua = rsum8(rmask * (Lw[L_U + i * ROW + j] * ap));
-        const double dd = Lw[L_DU + 2 * i] * (Lw[L_DU + 2 * i + 1] - ua);
+        const double ua = rsum8(rmask * (Ui * ap));
+        const double dd = Dv * (ui - ua);
         acc = ap + Sr * dd;
         if (i == 9) a9 = acc;
         Lw[L_QDD + i] = dd;
@@ -374,9 +395,11 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
 
 // AssistedManipulation::get_cost at x_k with the kinematics of the previous calculate()
 // (assisted_manipulation.cpp:58-128, term order kept); row-uniform result.
-__device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, const DevBarrier &lo_b, const DevBarrier &up_b,
-                                                  double vel_w, double q, double qd, double sq, double cq, const CoopKin &kin)
+__device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, const double *M, double q, double qd, double sq,
+                                                  double cq, const CoopKin &kin)
 {
+    const DevBarrier lo_b{M[T_LO], M[T_LO + 1], M[T_LO + 2]}, up_b{M[T_UP], M[T_UP + 1], M[T_UP + 2]};
+    const double vel_w = M[T_VW];
     const double lane_joint = jl ? left_barrier(lo_b, q) + right_barrier(up_b, q) : 0.0;
     const double joint = rsum16(lane_joint);
     const double vq = fabs(qd);
@@ -428,8 +451,11 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     double *Lw = lds_scr + rowi * LDS_SCR;
     {   // stage the body table
         const DevModel &dm = *a.model;
+        const DevCost &dc = *a.cost;
         for (int t = lane; t < LDS_MODEL; t += COOP_NT) {
-            const int b = t / MB, f = t % MB;
+            const int row = t / MB, f = t % MB;
+            const bool dummy = row == FR_NB;
+            const int b = dummy ? 0 : row;
             const DevBody &db = dm.b[b];
             const int kind = FR_KIND[b];
             const double *Rs = (b == 11) ? dm.f11_R : db.R;
@@ -438,6 +464,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const double ax0 = (kind == KIND_PX) ? 1.0 : 0.0;
             const double ax1 = (kind == KIND_PY) ? 1.0 : ((kind == KIND_PNY) ? -1.0 : 0.0);
             const double ax2 = (kind == KIND_RZ) ? 1.0 : 0.0;
+            const double live = dummy ? 0.0 : 1.0;
             double v;
             if (f < T_P) v = Rs[f];
             else if (f < T_M) v = ps[f - T_P];
@@ -451,7 +478,14 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             } else if (f == T_AX) v = ax0;
             else if (f == T_AX + 1) v = ax1;
             else if (f == T_AX + 2) v = ax2;
-            else v = (kind == KIND_RZ) ? 1.0 : 0.0;
+            else if (f == T_ROT) v = (kind == KIND_RZ) ? live : 0.0;
+            else if (f == T_NROT) v = (kind == KIND_RZ) ? 0.0 : live;
+            else if (f < T_UP) v = live * ((f == T_LO) ? dc.lower[b].bound : (f == T_LO + 1) ? dc.lower[b].scale : dc.lower[b].max);
+            else if (f < T_VW) v = live * ((f == T_UP) ? dc.upper[b].bound : (f == T_UP + 1) ? dc.upper[b].scale : dc.upper[b].max);
+            else if (f == T_VW) v = live * dc.vel_q[b];
+            else if (f == T_WV) v = (!dummy && b <= FR_EE_PARENT) ? 1.0 : 0.0;
+            else if (f == T_WA) v = (!dummy && b >= FR_ARM0 && b < FR_ARM1) ? 1.0 : 0.0;
+            else v = (!dummy && b == 11) ? -1.0 : 0.0;   // T_FIX
             Lmodel[t] = v;
         }
         __syncthreads();
@@ -462,17 +496,10 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int H = a.H;
     const bool jl = j < FR_NB;   // lane owns a body / control component
     const int jb = jl ? j : 0;
-    const double *M = Lmodel + jb * MB;
+    const double *M = Lmodel + (jl ? j : FR_NB) * MB;
     const DevCost &Cs = *a.cost;
-    const DevBarrier lo_b = Cs.lower[jb], up_b = Cs.upper[jb];
-    const double vel_w = jl ? Cs.vel_q[jb] : 0.0;
     LaneConst L;
     L.is_rz = jl && FR_KIND[jb] == KIND_RZ;
-    L.rotf = L.is_rz ? 1.0 : 0.0;
-    L.nrotf = L.is_rz ? 0.0 : 1.0;
-    L.fix11 = (j == 11) ? -1.0 : 0.0;
-    L.wv = (j <= FR_EE_PARENT) ? 1.0 : 0.0;
-    L.wa = (j >= FR_ARM0 && j < FR_ARM1) ? 1.0 : 0.0;
     L.slot = jl ? j : FR_NB;
 
     double q = live && jl ? a.x0[jb] : 0.0;
@@ -494,7 +521,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
-        const double step_cost = a.steps[k].gamma_k * step_cost_terms(Cs, jl, lo_b, up_b, vel_w, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[k].gamma_k * step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
         {
@@ -518,7 +545,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         J += step_cost;
     }
     if (alive) {   // the final step's cost; its dynamics are never observed
-        const double step_cost = a.steps[H - 1].gamma_k * step_cost_terms(Cs, jl, lo_b, up_b, vel_w, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[H - 1].gamma_k * step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
         J = (!a.optimal && isnan(step_cost)) ? NAN : J + step_cost;
     }
     if (!live || j != 0) return;

@@ -344,8 +344,10 @@ class Trajectory:
                                                    st.ctypes.data_as(C.POINTER(C.c_int64))))
         return uu, tt, st
 
-    def kernel_times(self):
-        """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events)."""
+    def kernel_times(self, wait=True):
+        """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
+        wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's)."""
         out = (C.c_float * 5)()
-        self._check(self._L.mppi_kernel_times(self._h, out))
+        fn = self._L.mppi_kernel_times if wait else self._L.mppi_kernel_times_nowait
+        self._check(fn(self._h, out))
         return list(out)

@@ -33,9 +33,12 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; t
 # (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
 # FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins this value).
 FLOPS_PER_ROLLOUT_STEP = 6518.0
-# Noise tensor traffic per rollout-step: eps written by the rollout kernel and read by the
-# gradient reduction, fp64, C = 12  (2 * 12 * 8 B).
-BYTES_PER_ROLLOUT_STEP = 192.0
+# Algorithmic HBM bytes of the rollout kernel per rollout-step: its eps column (C = 12 fp64) read
+# once (the sampler writes it, the gradient reduction reads it again: separate kernels).
+BYTES_PER_ROLLOUT_STEP = 96.0
+# HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
+# tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
+PMC_JSON = os.path.join(HERE, "profiles", "r01_pmc_rollout.json")
 
 
 def parse():
@@ -113,14 +116,12 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         traj.update(x, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
+        kt += np.array(traj.kernel_times(wait=False))   # HIP-event times of this update
         j += 1
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
-    for _ in range(3):             # per-kernel HIP-event times, measured on untimed extra updates
-        traj.update(x, 0.05 * j)
-        kt += np.array(traj.kernel_times())
-        j += 1
-    kt /= 3
+    kt /= args.steps
+    kt[3] = traj.kernel_times()[3]   # the optimal rollout (side stream) of the last timed update
     if dist:
         dist.barrier()
         import torch
@@ -130,6 +131,10 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = S_total * traj.H / (elapsed / args.steps)
     rollout_ms = float(kt[1])
+    traffic = None
+    if os.path.exists(PMC_JSON) and world == 1 and args.samples_per_gpu == SAMPLES_PER_GPU:
+        with open(PMC_JSON) as f:
+            traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
     flops = FLOPS_PER_ROLLOUT_STEP * count_local * traj.H
     achieved_tflops = flops / (rollout_ms * 1e-3) / 1e12
@@ -157,9 +162,10 @@ def main():
         "kernel_ms": {"sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
         "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
                      "kernel": "fr_rollout_kernel" if os.environ.get("MPPI_FR_KERNEL") == "lane" else "fr_coop_kernel", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
+                     "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
                      "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP},
-        "hbm": {"noise_tensor_GBs": BYTES_PER_ROLLOUT_STEP * count_local * traj.H / ((kt[1] + kt[2]) * 1e-3) / 1e9,
+        "hbm": {"rollout_algorithmic_GBs": BYTES_PER_ROLLOUT_STEP * count_local * traj.H / (rollout_ms * 1e-3) / 1e9,
                 "peak_GBs": HBM_PEAK_GBS},
     }
     if not args.no_cpu_baseline:

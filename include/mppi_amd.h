@@ -292,6 +292,9 @@ mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64
 /* Kernel timing of the last update (HIP events on the engine stream), milliseconds:
  * [0] sample/rank, [1] rollout, [2] weight-reduce, [3] optimal rollout, [4] whole update. */
 mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
+/* As mppi_kernel_times without waiting for the side stream: [3] is the latest optimal rollout
+ * already finished (possibly an earlier update's).  For timing loops that keep filter() overlapped. */
+mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5);
 
 #ifdef __cplusplus
 }
