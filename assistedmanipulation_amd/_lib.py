@@ -10,7 +10,7 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmppi_amd.so")
+LIB_PATH = os.environ.get("MPPI_AMD_LIB") or os.path.join(HERE, "lib", "libmppi_amd.so")   # override: kernel A/B builds
 HEADER = os.path.join(os.path.dirname(HERE), "include", "mppi_amd.h")
 
 _dp = C.POINTER(C.c_double)

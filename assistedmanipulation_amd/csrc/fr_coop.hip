@@ -16,12 +16,12 @@
 //                 local transform carries -q10, so its prefix world_10 * local_10^-1 * local_11
 //                 is world_9 * local_11 without a second pass.
 //   kinematics    EE / arm-mount positions (row_newbcast 9 / 2); frame velocity J v and J_a J_a^T
-//                 by 16-lane butterflies, folded straight into the trajectory and manipulability
-//                 terms of the next step's cost.
-//   ABA           articulated inertia distributed by rows over each 8-lane half of the row;
-//                 world inertias / S / tau / U staged in LDS (row-uniform values are LDS
-//                 broadcasts, the three row sums per body are 8-lane butterflies).
-//   cost          joint-limit / velocity terms per lane + butterflies; workspace row-uniform.
+//                 as chains of v_fmac_f64_dpp row_newbcast (lane sums), folded straight into the
+//                 trajectory and manipulability terms of the next step's cost.
+//   ABA           articulated inertia distributed by rows (lane r < 6 holds row r); world
+//                 inertias / S / tau staged in LDS and read one level ahead; S.U, S.pA, the
+//                 rank-1 update A - U U^T / D and the forward U.a are v_fmac_f64_dpp broadcasts.
+//   cost          joint-limit / velocity terms per lane + lane sums; workspace row-uniform.
 //
 // The step is written branch-free (selects, not branches) so the cost of step k, the FK of
 // step k and the cost terms of step k + 1 share basic blocks with the ABA chain and the
@@ -91,22 +91,102 @@ __device__ __forceinline__ double bcast(double x) { return __builtin_amdgcn_upda
 template <int S>
 __device__ __forceinline__ double shr(double x) { return dmov<0x110 + S>(x); }     // row_shr:S
 
-// sum over the 16 lanes of a row; every lane gets the same bits
-__device__ __forceinline__ double rsum16(double x)
+// acc + sum_{r<6} x[lane r] * y[r]: six v_fmac_f64_dpp row_newbcast:r (broadcast and multiply-add
+// in one instruction; the compiler does not form 64-bit DPP FMAs).  The leading s_nop covers the
+// VALU/EXEC-write -> DPP-read hazards.  Outputs are early-clobber ("+&v"): the blocks write the
+// accumulator before their last read of x / y, so they must never share a register with an input
+// (x and the accumulator are both the constant 0.0 at the finger levels of the ABA).
+__device__ __forceinline__ double bfma6(double x, const double *y, double acc)
 {
-    x = x + dmov<0xB1>(x);    // quad_perm [1,0,3,2]
-    x = x + dmov<0x4E>(x);    // quad_perm [2,3,0,1]
-    x = x + dmov<0x141>(x);   // row_half_mirror
-    x = x + dmov<0x140>(x);   // row_mirror
-    return x;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %3 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %4 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+        : "+&v"(acc)
+        : "v"(x), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]));
+    return acc;
 }
-// sum over each 8-lane half of a row
-__device__ __forceinline__ double rsum8(double x)
+// c[k] += x[lane k] * y for k < 6 (the rank-1 update of the articulated inertia rows)
+__device__ __forceinline__ void bfma6_rank1(double x, double y, double *c)
 {
-    x = x + dmov<0xB1>(x);
-    x = x + dmov<0x4E>(x);
-    x = x + dmov<0x141>(x);
-    return x;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %6, %7 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %6, %7 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %6, %7 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %6, %7 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %6, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %6, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf"
+        : "+&v"(c[0]), "+&v"(c[1]), "+&v"(c[2]), "+&v"(c[3]), "+&v"(c[4]), "+&v"(c[5])
+        : "v"(x), "v"(y));
+}
+// sum over lanes [L0, L1) of x: v_fmac_f64_dpp row_newbcast:l with a unit multiplier (one asm
+// block per range so the hazard nop stays in front of the chain)
+template <int L0, int L1>
+__device__ __forceinline__ double bsum(double x, double one);
+template <>
+__device__ __forceinline__ double bsum<0, 6>(double x, double one)
+{
+    const double ones[6] = {one, one, one, one, one, one};
+    return bfma6(x, ones, 0.0);
+}
+template <>
+__device__ __forceinline__ double bsum<0, 10>(double x, double one)
+{
+    double acc = 0.0;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf"
+        : "+&v"(acc)
+        : "v"(x), "v"(one));
+    return acc;
+}
+template <>
+__device__ __forceinline__ double bsum<3, 10>(double x, double one)
+{
+    double acc = 0.0;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf"
+        : "+&v"(acc)
+        : "v"(x), "v"(one));
+    return acc;
+}
+template <>
+__device__ __forceinline__ double bsum<0, 12>(double x, double one)
+{
+    double acc = 0.0;
+    asm("s_nop 4\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:11 row_mask:0xf bank_mask:0xf"
+        : "+&v"(acc)
+        : "v"(x), "v"(one));
+    return acc;
 }
 // 1/d by v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; d finite, normal)
 __device__ __forceinline__ double frcp(double d)
@@ -285,19 +365,17 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
-    const double wq = M[T_WV] * qd;
-    double vl[3];
+    // frame velocity J v over the EE chain (bodies 0..9), J_a J_a^T over the arm (bodies 3..9)
+    double vl[3], jj[6];
+    const double one = 1.0;
 #pragma unroll
-    for (int k = 0; k < 3; k++) vl[k] = rsum16(S[k] * wq);
-    const double wa = M[T_WA];
-    const double w0 = wa * S[0], w1 = wa * S[1], w2 = wa * S[2];
-    double jj[6];
-    jj[0] = rsum16(w0 * S[0]);
-    jj[1] = rsum16(w0 * S[1]);
-    jj[2] = rsum16(w0 * S[2]);
-    jj[3] = rsum16(w1 * S[1]);
-    jj[4] = rsum16(w1 * S[2]);
-    jj[5] = rsum16(w2 * S[2]);
+    for (int k = 0; k < 3; k++) vl[k] = bsum<0, FR_EE_PARENT + 1>(S[k] * qd, one);
+    jj[0] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[0], one);
+    jj[1] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[1], one);
+    jj[2] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[2], one);
+    jj[3] = bsum<FR_ARM0, FR_ARM1>(S[1] * S[1], one);
+    jj[4] = bsum<FR_ARM0, FR_ARM1>(S[1] * S[2], one);
+    jj[5] = bsum<FR_ARM0, FR_ARM1>(S[2] * S[2], one);
     kin.traj = trajectory_term(Cs, sc_next, vl);
     kin.manip = manipulability_term(Cs, jj);
 }
@@ -309,14 +387,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 // LDS broadcasts.
 __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
 {
-    const int h = j & 7;
-    const int r = h < 6 ? h : 5;
-    const double rmask = h < 6 ? 1.0 : 0.0;
+    const int r = j < 6 ? j : 5;   // lanes 0..5 hold rows 0..5; the others mirror row 5, unused
     int off[6];
 #pragma unroll
     for (int c = 0; c < 6; c++) off[c] = pidx(r, c);
     // operands of the next level are loaded one level ahead (LDS latency off the chain)
-    double An[6], Sn[6], Srn, taun;
+    double An[6], Sn[6], taun;
     auto fetch = [&](int i) {
         const double *Ii = Lk + L_I + i * 21;
         const double *Si = Lk + L_S + i * 6;
@@ -324,7 +400,6 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
         for (int k = 0; k < 6; k++) An[k] = Ii[off[k]];
 #pragma unroll
         for (int k = 0; k < 6; k++) Sn[k] = Si[k];
-        Srn = Si[r];
         taun = Lw[L_TAU + i];
     };
     fetch(FR_NB - 1);
@@ -339,36 +414,32 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
             A[k] = (i >= 10) ? An[k] : An[k] + C[k];
             S[k] = Sn[k];
         }
-        const double Sr = Srn, tau = taun;
+        const double tau = taun;
         if (i > 0) fetch(i - 1);
         const double pAr = (i >= 10) ? 0.0 : pA;
         const double U = ((A[0] * S[0] + A[1] * S[1]) + (A[2] * S[2] + A[3] * S[3])) + (A[4] * S[4] + A[5] * S[5]);
-        const double D = rsum8(rmask * (Sr * U));
-        const double sp = rsum8(rmask * (Sr * pAr));
+        // D = S.U and S.pA: rows 0..5 broadcast from lanes 0..5, every lane holds S
+        const double D = bfma6(U, S, 0.0);
+        const double sp = bfma6(pAr, S, 0.0);
         const double Dinv = frcp(D);
         const double u = tau - sp;
         Lw[L_U + i * ROW + j] = U;
         Lw[L_DU + 2 * i] = Dinv;
         Lw[L_DU + 2 * i + 1] = u;
         if (i > 0) {
-            double Uall[6];
-            Uall[0] = bcast<0>(U);
-            Uall[1] = bcast<1>(U);
-            Uall[2] = bcast<2>(U);
-            Uall[3] = bcast<3>(U);
-            Uall[4] = bcast<4>(U);
-            Uall[5] = bcast<5>(U);
             const double Ud = U * Dinv;
             const double ud = u * Dinv;
+            // C = A - U U^T / D, row r: C[k] = A[k] - (U_r / D) U_k (U_k broadcast from lane k)
             if (i == 10) {
 #pragma unroll
-                for (int k = 0; k < 6; k++) C[k] += A[k] - Ud * Uall[k];
+                for (int k = 0; k < 6; k++) C[k] += A[k];
                 pA += pAr + U * ud;
             } else {
 #pragma unroll
-                for (int k = 0; k < 6; k++) C[k] = A[k] - Ud * Uall[k];
+                for (int k = 0; k < 6; k++) C[k] = A[k];
                 pA = pAr + U * ud;
             }
+            bfma6_rank1(U, -Ud, C);
         }
     }
     double acc = 0.0, a9 = 0.0;
@@ -383,7 +454,7 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
             uf = Lw[L_DU + 2 * (i + 1) + 1];
         }
         const double ap = (i == 11) ? a9 : acc;
-        const double ua = rsum8(rmask * (Ui * ap));
+        const double ua = bsum<0, 6>(Ui * ap, 1.0);
         const double dd = Dv * (ui - ua);
         acc = ap + Sr * dd;
         if (i == 9) a9 = acc;
@@ -401,9 +472,10 @@ __device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, co
     const DevBarrier lo_b{M[T_LO], M[T_LO + 1], M[T_LO + 2]}, up_b{M[T_UP], M[T_UP + 1], M[T_UP + 2]};
     const double vel_w = M[T_VW];
     const double lane_joint = jl ? left_barrier(lo_b, q) + right_barrier(up_b, q) : 0.0;
-    const double joint = rsum16(lane_joint);
     const double vq = fabs(qd);
-    const double vel = rsum16(vel_w * (vq * vq));
+    const double one = 1.0;
+    const double joint = bsum<0, FR_NB>(lane_joint, one);
+    const double vel = bsum<0, FR_NB>(vel_w * (vq * vq), one);
     const double s = bcast<2>(sq), c = bcast<2>(cq);
     double wc = 0.0;
     {
