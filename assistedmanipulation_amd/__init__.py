@@ -13,13 +13,13 @@ _load()   # fail loudly at import if the engine library is missing
 
 from .config import (Configuration, Smoothing, constant_forecast,  # noqa: E402
                      frankaridgeback_configuration, huddled_state, point_mass_configuration)
-from .trajectory import (AssistedManipulation, Cost, Dynamics, EngineError,  # noqa: E402
+from .trajectory import (AssistedManipulation, Cost, Dynamics, EngineError, TrackPoint,  # noqa: E402
                          FrankaRidgebackDynamics, PointMassDynamics, QuadraticCost, Trajectory,
                          comm_unique_id, shard_range)
 
 __all__ = [
     "abi", "Configuration", "Smoothing", "constant_forecast", "frankaridgeback_configuration",
-    "huddled_state", "point_mass_configuration", "AssistedManipulation", "Cost", "Dynamics",
+    "huddled_state", "point_mass_configuration", "AssistedManipulation", "TrackPoint", "Cost", "Dynamics",
     "EngineError", "FrankaRidgebackDynamics", "PointMassDynamics", "QuadraticCost", "Trajectory",
     "comm_unique_id", "shard_range",
 ]

@@ -23,6 +23,7 @@ PROTOTYPES = {
     "mppi_build_info": (C.c_char_p, []),
     "mppi_default_frankaridgeback": (None, [C.POINTER(abi.mppi_frankaridgeback_desc)]),
     "mppi_default_assisted_manipulation": (None, [C.POINTER(abi.mppi_assisted_manipulation_desc)]),
+    "mppi_default_track_point": (None, [C.POINTER(abi.mppi_track_point_desc)]),
     "mppi_create": (C.c_int, [C.POINTER(abi.mppi_config), C.POINTER(abi.mppi_dynamics_desc),
                               C.POINTER(abi.mppi_cost_desc), C.c_int, C.POINTER(_h)]),
     "mppi_destroy": (None, [_h]),

@@ -33,6 +33,7 @@ MPPI_JOINT_REVOLUTE = 0
 MPPI_JOINT_PRISMATIC = 1
 MPPI_COST_ASSISTED_MANIPULATION = 1
 MPPI_COST_QUADRATIC = 2
+MPPI_COST_TRACK_POINT = 3
 MPPI_NOISE_DEVICE_PHILOX = 0
 MPPI_NOISE_HOST_INJECTED = 1
 MPPI_INDEX_WIDE = 0
@@ -151,11 +152,27 @@ class mppi_quadratic_cost_desc(C.Structure):
     _fields_ = [("target", _d * 3), ("q", _d * 3), ("r", _d * 3)]
 
 
+class mppi_track_point_desc(C.Structure):
+    _fields_ = [
+        ("point", _d * 3),
+        ("enable_joint_limits", C.c_int32),
+        ("enable_self_collision_avoidance", C.c_int32),
+        ("enable_power_limit", C.c_int32),
+        ("enable_reach_limits", C.c_int32),
+        ("lower_joint_limit", mppi_barrier * MPPI_FR_JOINTS),
+        ("upper_joint_limit", mppi_barrier * MPPI_FR_JOINTS),
+        ("self_collision_limit", mppi_barrier),
+        ("self_collision_radii", _d * 8),
+        ("maximum_reach_limit", mppi_barrier),
+    ]
+
+
 class mppi_cost_desc(C.Structure):
     _fields_ = [
         ("kind", C.c_int32),
         ("assisted_manipulation", mppi_assisted_manipulation_desc),
         ("quadratic", mppi_quadratic_cost_desc),
+        ("track_point", mppi_track_point_desc),
     ]
 
 

@@ -294,6 +294,9 @@ void dfree(mppi_handle *h, double *&p)
     p = nullptr;
 }
 
+// The single-lane kernel (MPPI_FR_KERNEL=lane, A/B runs) implements AssistedManipulation only.
+bool use_coop(const mppi_handle *h) { return h->coop || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION; }
+
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
     dfree(h, h->d_noise);
@@ -331,6 +334,7 @@ const char *mppi_build_info(void)
 
 void mppi_default_frankaridgeback(mppi_frankaridgeback_desc *out) { mppi_frankaridgeback_model(out); }
 void mppi_default_assisted_manipulation(mppi_assisted_manipulation_desc *out) { mppi_assisted_manipulation_default(out); }
+void mppi_default_track_point(mppi_track_point_desc *out) { mppi_track_point_default(out); }
 
 const char *mppi_last_error(const mppi_handle *h) { return h ? h->err.c_str() : g_last_error.c_str(); }
 
@@ -355,7 +359,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     *out = nullptr;
     const int64_t Cd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 3 : (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK ? FR_C : -1);
     const int64_t Xd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 6 : FR_X;
-    const int64_t Cc = cost->kind == MPPI_COST_QUADRATIC ? 3 : (cost->kind == MPPI_COST_ASSISTED_MANIPULATION ? FR_C : -2);
+    const bool fr_cost = cost->kind == MPPI_COST_ASSISTED_MANIPULATION || cost->kind == MPPI_COST_TRACK_POINT;
+    const int64_t Cc = cost->kind == MPPI_COST_QUADRATIC ? 3 : (fr_cost ? FR_C : -2);
     const int64_t Xc = cost->kind == MPPI_COST_QUADRATIC ? 6 : FR_X;
     // Trajectory::create validation, in the reference's order (mppi.cpp:17-69)
     if (Cd < 0) return fail(nullptr, MPPI_ERR_INVALID, "unknown dynamics kind");
@@ -377,7 +382,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     if (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         mppi_status st = check_topology(dyn->frankaridgeback, why);
         if (st != MPPI_OK) return fail(nullptr, st, why);
-        if (cost->assisted_manipulation.enable_energy_limit)
+        if (cost->kind == MPPI_COST_ASSISTED_MANIPULATION && cost->assisted_manipulation.enable_energy_limit)
             return fail(nullptr, MPPI_ERR_UNSUPPORTED, "enable_energy_limit needs the NLE power term (SURVEY §8f item 3, not built yet)");
     }
 
@@ -488,6 +493,33 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(hipMemcpy(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
         const mppi_assisted_manipulation_desc &a = cost->assisted_manipulation;
         DevCost c{};
+        c.kind = cost->kind;
+        // the 20 link pairs of both objectives' self_collision_cost (Link enum: PIVOT = 3,
+        // PANDA_LINK1..7 = 4..10; radii index = link - 3), link positions the zero stub
+        static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8}, {4, 9}, {4, 10},
+                                         {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
+        if (cost->kind == MPPI_COST_TRACK_POINT) {
+            const mppi_track_point_desc &t = cost->track_point;
+            c.tp_en_joint = t.enable_joint_limits;
+            c.tp_en_self = t.enable_self_collision_avoidance;
+            c.tp_en_reach = t.enable_reach_limits;
+            for (int i = 0; i < 3; i++) c.tp_point[i] = t.point[i];
+            // joint_limit_cost's static limits (track_point.cpp:45-66)
+            static const double lo[FR_NB] = {-2.0, -2.0, -6.28, -2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973, 0.5, 0.5};
+            static const double up[FR_NB] = {2.0, 2.0, 6.28, 2.8973, 1.7628, 2.8973, 0.0698, 2.8973, 3.7525, 2.8973, 0.5, 0.5};
+            for (int i = 0; i < FR_NB; i++) {
+                c.tp_lo[i] = lo[i];
+                c.tp_up[i] = up[i];
+            }
+            double sc = 0.0;   // track_point.cpp:97-160: collision = radii - distance
+            for (auto &p : pairs) {
+                const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
+                const double radii = t.self_collision_radii[p[0] - 3] + t.self_collision_radii[p[1] - 3];
+                sc += left_barrier_h(t.self_collision_limit, radii - distance);
+            }
+            c.tp_self = sc;
+            c.tp_reach = devb(t.maximum_reach_limit);
+        } else {
         c.en_joint = a.enable_joint_limit;
         c.en_self = a.enable_self_collision_limit;
         c.en_work = a.enable_workspace_limit;
@@ -501,8 +533,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
             c.vel_q[i] = a.velocity_cost[i].quadratic_cost;
         }
         // self_collision_cost with get_link_position == 0 (assisted_manipulation.cpp:90-158)
-        static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8}, {4, 9}, {4, 10},
-                                         {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
         double sc = 0.0;
         for (auto &p : pairs) {
             const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
@@ -522,6 +552,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         c.traj_vel_c = a.trajectory_velocity_cost.constant_cost;
         c.traj_vel_l = a.trajectory_velocity_cost.linear_cost;
         c.traj_vel_q = a.trajectory_velocity_cost.quadratic_cost;
+        }
         CREATE_TRY(dalloc(h, &h->d_cost, 1));
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
     } else {
@@ -747,7 +778,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.H = (int)h->H;
         a.optimal = 0;
         a.status = h->d_status;
-        HIP_TRY(h->coop ? launch_fr_coop(a, h->stream) : launch_fr_rollout(a, h->stream));
+        a.cost_kind = h->cost_kind;
+        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream) : launch_fr_rollout(a, h->stream));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -835,7 +867,8 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         a.dt = h->dt;
         a.H = (int)h->H;
         a.optimal = 1;
-        HIP_TRY(h->coop ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
+        a.cost_kind = h->cost_kind;
+        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;

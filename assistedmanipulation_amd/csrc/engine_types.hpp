@@ -55,6 +55,12 @@ struct DevCost {
     double vel_q[FR_NB];
     double manip_c, manip_l, manip_q;
     double traj_vel_c, traj_vel_l, traj_vel_q;
+    // TrackPoint (frankaridgeback/objective/track_point.cpp) when kind == MPPI_COST_TRACK_POINT
+    int kind, tp_en_joint, tp_en_self, tp_en_reach;
+    double tp_point[3];
+    double tp_lo[FR_NB], tp_up[FR_NB];   // joint_limit_cost's hard-coded limits (joints 0..9 read)
+    double tp_self;                      // self_collision_cost with get_link_position == 0
+    DevBarrier tp_reach;                 // maximum_reach_limit (right)
 };
 
 // trajectory_cost() constants of step k (assisted_manipulation.cpp:237-290): everything that

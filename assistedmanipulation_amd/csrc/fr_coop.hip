@@ -45,6 +45,7 @@ namespace {
 
 constexpr int ROW = 16;
 constexpr int ROWS_PER_WAVE = 4;
+constexpr int CK_ASSISTED_MANIPULATION = 1, CK_TRACK_POINT = 3;   // mppi_cost_kind
 constexpr int COOP_NT = 64;   // one wave per workgroup
 constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 store into
 
@@ -315,6 +316,7 @@ struct LaneConst {
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
+template <int CK>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
                                         double *Lk, const DevCost &Cs, const StepConst &sc_next, CoopKin &kin)
 {
@@ -365,6 +367,9 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
+    kin.traj = 0.0;
+    kin.manip = 0.0;
+    if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
     // frame velocity J v over the EE chain (bodies 0..9), J_a J_a^T over the arm (bodies 3..9)
     double vl[3], jj[6];
     const double one = 1.0;
@@ -509,7 +514,44 @@ __device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, co
 
 }  // namespace
 
+// TrackPoint::get_cost (frankaridgeback/objective/track_point.cpp:10-34) at x_k with the previous
+// calculate()'s EE and arm-mount positions; row-uniform result.  The joint terms sum joints 0..9
+// in order and at most one of a joint's two terms is nonzero, so the lane sum adds exactly the
+// reference's nonzero terms in the reference's order.
+__device__ __forceinline__ double track_point_terms(const DevCost &Cs, int j, double q, double sq, double cq, const CoopKin &kin)
+{
+    const double d0 = kin.ee[0] - Cs.tp_point[0], d1 = kin.ee[1] - Cs.tp_point[1], d2 = kin.ee[2] - Cs.tp_point[2];
+    const double distance = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+    double cost = 100.0 * (distance * distance);   // point_cost: 100 pow(distance, 2)
+    const int jc = j < 10 ? j : 0;
+    const double lo = Cs.tp_lo[jc], up = Cs.tp_up[jc];
+    const double below = (q < lo) ? 1000.0 + 100000.0 * ((lo - q) * (lo - q)) : 0.0;
+    const double above = (q > up) ? 1000.0 + 100000.0 * ((q - up) * (q - up)) : 0.0;
+    const double joint = bsum<0, 10>(j < 10 ? below + above : 0.0, 1.0);
+    // reach_cost: robot = arm mount + R_z(yaw) (0.3, 0, 0.15) (track_point.cpp:162-186)
+    const double s = bcast<2>(sq), c = bcast<2>(cq);
+    const double r22 = (1.0 - c) + c;
+    const double off0 = (0.3 * c + (-s) * 0.0) + 0.0 * 0.15;
+    const double off1 = (0.3 * s + c * 0.0) + 0.0 * 0.15;
+    const double off2 = (0.0 * 0.3 + 0.0 * 0.0) + r22 * 0.15;
+    const double t0 = kin.ee[0] - (kin.am[0] + off0), t1 = kin.ee[1] - (kin.am[1] + off1), t2 = kin.ee[2] - (kin.am[2] + off2);
+    const double reach = right_barrier(Cs.tp_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
+    cost += Cs.tp_en_joint ? joint : 0.0;
+    cost += Cs.tp_en_self ? Cs.tp_self : 0.0;
+    cost += Cs.tp_en_reach ? reach : 0.0;
+    return cost;
+}
+
+template <int CK>
+__device__ __forceinline__ double objective_terms(const DevCost &Cs, bool jl, int j, const double *M, double q, double qd, double sq,
+                                                  double cq, const CoopKin &kin)
+{
+    if constexpr (CK == CK_TRACK_POINT) return track_point_terms(Cs, j, q, sq, cq, kin);
+    else return step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
+}
+
 // ---------------------------------------------------------------------------------------------
+template <int CK>
 __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
 {
     __shared__ double lds_kin[ROWS_PER_WAVE * LDS_KIN];
@@ -579,7 +621,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     double sq, cq;
     sincos(q, &sq, &cq);   // one sincos per lane and step: FK, base yaw, workspace
     CoopKin kin;
-    coop_fk(L, q, sq, cq, qd, M, Lk, Cs, a.steps[0], kin);   // set_state -> calculate() at (q0, v0)
+    coop_fk<CK>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[0], kin);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step, first used after its cost
     const bool sampled = !a.optimal && live && jl;
@@ -593,7 +635,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
-        const double step_cost = a.steps[k].gamma_k * step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[k].gamma_k * objective_terms<CK>(Cs, jl, j, M, q, qd, sq, cq, kin);
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
         {
@@ -604,7 +646,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             qd = (j == 0) ? vx : ((j == 1) ? vy : ((j == 2) ? u : qd));
         }
         Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
-        coop_fk(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin);
+        coop_fk<CK>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin);
         const double qdd = coop_aba(j, Lk, Lw);
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
@@ -617,7 +659,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         J += step_cost;
     }
     if (alive) {   // the final step's cost; its dynamics are never observed
-        const double step_cost = a.steps[H - 1].gamma_k * step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[H - 1].gamma_k * objective_terms<CK>(Cs, jl, j, M, q, qd, sq, cq, kin);
         J = (!a.optimal && isnan(step_cost)) ? NAN : J + step_cost;
     }
     if (!live || j != 0) return;
@@ -631,7 +673,8 @@ hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
 {
     const unsigned nb = (unsigned)((a.count + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(fr_coop_kernel, dim3(nb), dim3(COOP_NT), 0, s, a);
+    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL(fr_coop_kernel<CK_TRACK_POINT>, dim3(nb), dim3(COOP_NT), 0, s, a);
+    else hipLaunchKernelGGL(fr_coop_kernel<CK_ASSISTED_MANIPULATION>, dim3(nb), dim3(COOP_NT), 0, s, a);
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ struct FrRolloutArgs {
     double dt;
     int H;
     int optimal;
+    int cost_kind;            // mppi_cost_kind: AssistedManipulation or TrackPoint
 };
 
 // sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).

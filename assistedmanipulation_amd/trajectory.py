@@ -114,6 +114,29 @@ class AssistedManipulation(Cost):
         return c
 
 
+class TrackPoint(Cost):
+    """FrankaRidgeback::TrackPoint (objective/track_point.{hpp,cpp}).
+    `configuration` is a mppi_track_point_desc; by default DEFAULT_CONFIGURATION; `point`
+    overrides the tracked point."""
+    control_dof = abi.MPPI_FR_CONTROL
+    state_dof = abi.MPPI_FR_STATE
+
+    def __init__(self, configuration=None, point=None):
+        if configuration is None:
+            configuration = abi.mppi_track_point_desc()
+            load().mppi_default_track_point(C.byref(configuration))
+        if point is not None:
+            for i in range(3):
+                configuration.point[i] = float(point[i])
+        self.configuration = configuration
+
+    def descriptor(self):
+        c = abi.mppi_cost_desc()
+        c.kind = abi.MPPI_COST_TRACK_POINT
+        c.track_point = self.configuration
+        return c
+
+
 class QuadraticCost(Cost):
     control_dof = 3
     state_dof = 6

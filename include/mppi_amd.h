@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPPI_AMD_ABI_VERSION 1
+#define MPPI_AMD_ABI_VERSION 2
 
 #define MPPI_MAX_BODIES 16
 #define MPPI_MAX_CONTROL 16
@@ -129,7 +129,8 @@ typedef struct mppi_dynamics_desc {
  * ---------------------------------------------------------------------------------------- */
 typedef enum mppi_cost_kind {
     MPPI_COST_ASSISTED_MANIPULATION = 1,     /* objective/assisted_manipulation.{hpp,cpp} */
-    MPPI_COST_QUADRATIC = 2                  /* point-mass bring-up cost */
+    MPPI_COST_QUADRATIC = 2,                 /* point-mass bring-up cost */
+    MPPI_COST_TRACK_POINT = 3                /* objective/track_point.{hpp,cpp} */
 } mppi_cost_kind;
 
 typedef struct mppi_quadratic {              /* QuadraticCost (controller/cost.hpp:10-37) */
@@ -178,6 +179,23 @@ typedef struct mppi_assisted_manipulation_desc {
     int32_t has_forecast;
 } mppi_assisted_manipulation_desc;
 
+/* TrackPoint::Configuration (frankaridgeback/objective/track_point.hpp:20-61), field for field.
+ * get_cost (track_point.cpp:10-34) = 100 |p_EE - point|^2, + joint_limit_cost (hard-coded limits,
+ * track_point.cpp:45-95; the configured joint barriers are not read), + self_collision_cost,
+ * + reach_cost; enable_power_limit is never read. */
+typedef struct mppi_track_point_desc {
+    double point[3];
+    int32_t enable_joint_limits;
+    int32_t enable_self_collision_avoidance;
+    int32_t enable_power_limit;
+    int32_t enable_reach_limits;
+    mppi_barrier lower_joint_limit[MPPI_FR_JOINTS];   /* left barriers (configuration only) */
+    mppi_barrier upper_joint_limit[MPPI_FR_JOINTS];   /* right barriers (configuration only) */
+    mppi_barrier self_collision_limit;                /* left */
+    double self_collision_radii[8];
+    mppi_barrier maximum_reach_limit;                 /* right */
+} mppi_track_point_desc;
+
 typedef struct mppi_quadratic_cost_desc {    /* sum_i q_i (p_i - target_i)^2 + r_i u_i^2 */
     double target[3];
     double q[3];
@@ -188,6 +206,7 @@ typedef struct mppi_cost_desc {
     int32_t kind;                            /* mppi_cost_kind */
     mppi_assisted_manipulation_desc assisted_manipulation;
     mppi_quadratic_cost_desc quadratic;
+    mppi_track_point_desc track_point;
 } mppi_cost_desc;
 
 /* ------------------------------------------------------------------------------------------
@@ -215,6 +234,8 @@ const char *mppi_build_info(void);
  * (assisted_manipulation.hpp:133-206). */
 void mppi_default_frankaridgeback(mppi_frankaridgeback_desc *out);
 void mppi_default_assisted_manipulation(mppi_assisted_manipulation_desc *out);
+/* TrackPoint::DEFAULT_CONFIGURATION (track_point.hpp:72-107). */
+void mppi_default_track_point(mppi_track_point_desc *out);
 
 /* Trajectory::create (mppi.hpp:321-326, mppi.cpp:11-77).  Validation failures return
  * MPPI_ERR_INVALID with the reference's message available from mppi_last_error(NULL).

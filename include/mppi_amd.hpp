@@ -303,4 +303,34 @@ private:
     Configuration m_configuration;
 };
 
+// FrankaRidgeback::TrackPoint (frankaridgeback/objective/track_point.hpp:16-215): the same
+// create / copy surface; DEFAULT_CONFIGURATION is track_point.hpp:72-107.
+class TrackPoint : public mppi::Cost {
+public:
+    using Configuration = mppi_track_point_desc;
+    static Configuration default_configuration()
+    {
+        Configuration c;
+        mppi_track_point_default(&c);
+        return c;
+    }
+    static inline const Configuration DEFAULT_CONFIGURATION = default_configuration();
+    static std::unique_ptr<TrackPoint> create(const Configuration &c) { return std::make_unique<TrackPoint>(c); }
+    TrackPoint() : m_configuration(default_configuration()) {}
+    explicit TrackPoint(const Configuration &c) : m_configuration(c) {}
+    std::unique_ptr<mppi::Cost> copy() override { return std::make_unique<TrackPoint>(m_configuration); }
+    int get_control_dof() override { return MPPI_FR_CONTROL; }
+    int get_state_dof() override { return MPPI_FR_STATE; }
+    bool describe(mppi_cost_desc &out) const override
+    {
+        out = mppi_cost_desc{};
+        out.kind = MPPI_COST_TRACK_POINT;
+        out.track_point = m_configuration;
+        return true;
+    }
+
+private:
+    Configuration m_configuration;
+};
+
 }  // namespace FrankaRidgeback

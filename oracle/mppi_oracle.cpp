@@ -826,6 +826,71 @@ template <class T> struct AssistedManipulation {
 };
 
 // ------------------------------------------------------------------------------------------
+// TrackPoint (frankaridgeback/objective/track_point.cpp:10-186), SURVEY §8f item 1.
+// ------------------------------------------------------------------------------------------
+template <class T> struct TrackPoint {
+    mppi_track_point_desc cfg;
+
+    void reset(double) {}
+
+    // point_cost (:36-43): 100 pow(|p_EE - point|, 2)
+    T point(const FrankaDynamics<T> &d)
+    {
+        T distance = norm(d.ee_pos - V3<T>(T(cfg.point[0]), T(cfg.point[1]), T(cfg.point[2])));
+        return T(100.0) * (distance * distance);
+    }
+
+    // joint_limit_cost (:45-95): static limits, joints 0..9
+    T joint_limit(const T *x)
+    {
+        static const double lower[12] = {-2.0, -2.0, -6.28, -2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973, 0.5, 0.5};
+        static const double upper[12] = {2.0, 2.0, 6.28, 2.8973, 1.7628, 2.8973, 0.0698, 2.8973, 3.7525, 2.8973, 0.5, 0.5};
+        T cost = T(0);
+        for (int i = 0; i < 10; i++) {
+            if (x[i] < T(lower[i])) { T dd = T(lower[i]) - x[i]; cost += T(1000.0) + T(100000.0) * (dd * dd); }
+            if (x[i] > T(upper[i])) { T dd = x[i] - T(upper[i]); cost += T(1000.0) + T(100000.0) * (dd * dd); }
+        }
+        return cost;
+    }
+
+    // self_collision_cost (:97-160) with get_link_position == 0; collision = radii - distance
+    T self_collision()
+    {
+        static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8},
+            {4, 9}, {4, 10}, {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
+        T cost = T(0);
+        for (int k = 0; k < 20; k++) {
+            T distance = norm(V3<T>() - V3<T>());
+            T radii = T(cfg.self_collision_radii[pairs[k][0] - 3]) + T(cfg.self_collision_radii[pairs[k][1] - 3]);
+            cost += left_barrier(cfg.self_collision_limit, radii - distance);
+        }
+        return cost;
+    }
+
+    // reach_cost (:162-186)
+    T reach(const FrankaDynamics<T> &d)
+    {
+        T ang = d.state[2];
+        T s = s_sin(ang), c = s_cos(ang);
+        T r22 = (T(1) - c) + c;
+        V3<T> off(T(0.3) * c + (-s) * T(0) + T(0) * T(0.15), T(0.3) * s + c * T(0) + T(0) * T(0.15),
+                  T(0) * T(0.3) + T(0) * T(0) + r22 * T(0.15));
+        V3<T> robot = d.am_pos + off;
+        return right_barrier(cfg.maximum_reach_limit, norm(d.ee_pos - robot));
+    }
+
+    // get_cost (:10-34)
+    T get_cost(const T *x, const FrankaDynamics<T> &d, int64_t)
+    {
+        T cost = point(d);
+        if (cfg.enable_joint_limits) cost += joint_limit(x);
+        if (cfg.enable_self_collision_avoidance) cost += self_collision();
+        if (cfg.enable_reach_limits) cost += reach(d);
+        return cost;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
 // Point-mass bring-up plugin (not in the reference).  State (p, v), control
 // force; semi-implicit Euler as in a8; cost sum q (p - p*)^2 + r u^2.
 // ------------------------------------------------------------------------------------------
@@ -1162,11 +1227,24 @@ struct Trajectory {
         else m = &mf;
         if (d.M != m) d.init(m);
         d.reduced = reduced != 0;
+        if (costd.kind == MPPI_COST_TRACK_POINT) {
+            TrackPoint<T> c;
+            c.cfg = costd.track_point;
+            return rollout_franka_with(c, eps, optimal, d);
+        }
         AssistedManipulation<T> c;
         c.cfg = costd.assisted_manipulation;
         c.forecast = forecast.empty() ? nullptr : forecast.data();
         c.forecast_rows = (int64_t)forecast.size() / 6;
         c.dt = dt;
+        const double total = rollout_franka_with(c, eps, optimal, d);
+        if (terms) *terms = c.acc;
+        return total;
+    }
+
+    // rollout() (mppi.cpp:311-342) of one sample with objective c
+    template <class T, class Obj> double rollout_franka_with(Obj &c, const double *eps, bool optimal, FrankaDynamics<T> &d)
+    {
         d.set_state(rollout_state.data());
         c.reset(rollout_time);
         double total = 0.0;
@@ -1182,7 +1260,6 @@ struct Trajectory {
             const T *x = d.step(u, T(dt));
             for (int i = 0; i < MPPI_FR_STATE; i++) state[i] = x[i];
         }
-        if (terms) *terms = c.acc;
         return total;
     }
 
@@ -1346,7 +1423,7 @@ void *oracle_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, const
 {
     int64_t Cd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 3 : MPPI_FR_CONTROL;
     int64_t Xd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 6 : MPPI_FR_STATE;
-    int64_t Cc = cost->kind == MPPI_COST_QUADRATIC ? 3 : MPPI_FR_CONTROL;
+    int64_t Cc = cost->kind == MPPI_COST_QUADRATIC ? 3 : MPPI_FR_CONTROL;   // AssistedManipulation, TrackPoint
     int64_t Xc = cost->kind == MPPI_COST_QUADRATIC ? 6 : MPPI_FR_STATE;
     auto fail = [](const char *m) -> void * { orc::g_err = m; return nullptr; };
     if (Cd != Cc) return fail("controller dynamics control dof != cost control dof");

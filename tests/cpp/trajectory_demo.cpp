@@ -1,10 +1,12 @@
 // Drives the engine through the C++ drop-in (include/mppi_amd.hpp) the way the reference's
 // FrankaRidgeback::Actor drives mppi::Trajectory (actor.cpp:96-101, 166-203):
 // create -> per control period: set_forecast, update(state, t), get(control, t).
-// Prints one JSON object per update.  Usage: trajectory_demo [rollouts] [horison] [updates]
+// Prints one JSON object per update.
+// Usage: trajectory_demo [rollouts] [horison] [updates] [assisted_manipulation|track_point]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "mppi_amd.hpp"
@@ -14,6 +16,11 @@ int main(int argc, char **argv)
     const long rollouts = argc > 1 ? std::atol(argv[1]) : 128;
     const double horison = argc > 2 ? std::atof(argv[2]) : 0.32;
     const int updates = argc > 3 ? std::atoi(argv[3]) : 3;
+    const bool track_point = argc > 4 && std::strcmp(argv[4], "track_point") == 0;
+    auto objective = [&]() -> std::unique_ptr<mppi::Cost> {
+        if (track_point) return FrankaRidgeback::TrackPoint::create(FrankaRidgeback::TrackPoint::DEFAULT_CONFIGURATION);
+        return std::make_unique<FrankaRidgeback::AssistedManipulation>();
+    };
 
     mppi::Configuration c;   // BaseTest::DEFAULT_CONFIGURATION's mppi block (base.hpp:69-101)
     c.initial_state.assign(MPPI_FR_STATE, 0.0);
@@ -40,8 +47,7 @@ int main(int argc, char **argv)
                                           std::make_unique<FrankaRidgeback::AssistedManipulation>());
         if (t) { std::printf("{\"error\": \"invalid configuration accepted\"}\n"); return 1; }
     }
-    auto traj = mppi::Trajectory::create(c, std::make_unique<FrankaRidgeback::PinocchioDynamics>(),
-                                         std::make_unique<FrankaRidgeback::AssistedManipulation>());
+    auto traj = mppi::Trajectory::create(c, std::make_unique<FrankaRidgeback::PinocchioDynamics>(), objective());
     if (!traj) return 2;
     traj->set_noise_source(MPPI_NOISE_DEVICE_PHILOX, 0x5EED);
     std::vector<double> forecast(6 * traj->get_step_count(), 0.0);

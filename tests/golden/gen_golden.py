@@ -231,6 +231,32 @@ def cost(x, k_cache, force):
     return c
 
 
+# TrackPoint (frankaridgeback/objective/track_point.cpp:10-186): every term enabled in the fixture
+TP_LO = [-2.0, -2.0, -6.28, -2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973]
+TP_UP = [2.0, 2.0, 6.28, 2.8973, 1.7628, 2.8973, 0.0698, 2.8973, 3.7525, 2.8973]
+TP_POINT = np.array([0.8, 0.6, 0.9])
+
+
+TP_BREACHES = [0]
+
+
+def track_point_cost(x, k_cache, force):
+    q = x[:12]
+    ee = k_cache["ee"]
+    c = 100.0 * float(np.linalg.norm(ee - TP_POINT)) ** 2
+    for i in range(10):
+        if q[i] < TP_LO[i]:
+            c += 1000.0 + 100000.0 * (TP_LO[i] - q[i]) ** 2
+            TP_BREACHES[0] += 1
+        if q[i] > TP_UP[i]:
+            c += 1000.0 + 100000.0 * (q[i] - TP_UP[i]) ** 2
+            TP_BREACHES[0] += 1
+    c += sum(left(0.0, 1.0, RADII[a - 3] + RADII[b - 3]) for a, b in PAIRS)   # link positions == 0
+    robot = k_cache["am"] + np.array([0.3 * math.cos(x[2]), 0.3 * math.sin(x[2]), 0.15])
+    c += right(0.8, 1.0, float(np.linalg.norm(ee - robot)))
+    return c
+
+
 def step(rob, x, u, dt):
     q, v = x[:12].copy(), x[12:24].copy()
     c, s = math.cos(q[2]), math.sin(q[2])
@@ -248,13 +274,14 @@ def step(rob, x, u, dt):
     return xn, kc
 
 
-def rollout(rob, x0, U, eps, dt, forecast, optimal=False):
+def rollout(rob, x0, U, eps, dt, forecast, optimal=False, objective=None):
+    objective = objective or cost
     x = x0.copy()
     kc = kin(rob, x[:12], x[12:24])
     J = 0.0
     for k in range(U.shape[0]):
         u = U[k] + (0.0 if eps is None else eps[k])
-        sc = cost(x, kc, forecast[k])
+        sc = objective(x, kc, forecast[k])
         if not optimal and math.isnan(sc):
             return float("nan")
         J += sc
@@ -320,8 +347,9 @@ class Window:
 # mppi::Trajectory (mppi.cpp) restated in Python
 # ------------------------------------------------------------------------------------------
 class MPPI:
-    def __init__(self, rob, S, K, H, dt, var, cmin, cmax, x0, smoothing=None):
+    def __init__(self, rob, S, K, H, dt, var, cmin, cmax, x0, smoothing=None, objective=None):
         self.rob, self.S, self.K, self.H, self.dt = rob, S, K, H, dt
+        self.objective = objective or cost
         self.R = S + 2
         self.C = len(var)
         self.noise = np.zeros((self.R, H, self.C))
@@ -360,7 +388,7 @@ class MPPI:
                 self.noise[r, k] = next(it)
         self.noise[1] = -self.U
         for r in range(self.R):
-            self.cost[r] = rollout(self.rob, x0, self.Us, self.noise[r], self.dt, forecast)
+            self.cost[r] = rollout(self.rob, x0, self.Us, self.noise[r], self.dt, forecast, objective=self.objective)
         ok = ~np.isnan(self.cost)
         mn, mx = self.cost[ok].min(), self.cost[ok].max()
         if mx - mn >= 1e-6:
@@ -381,7 +409,7 @@ class MPPI:
                         self.Us[k, c] = r
                         win.uu[idx - 1] = r
             self.Us = np.maximum(np.minimum(self.Us, self.cmax), self.cmin)
-        self.opt_cost = rollout(self.rob, x0, self.Us, None, self.dt, forecast, optimal=True)
+        self.opt_cost = rollout(self.rob, x0, self.Us, None, self.dt, forecast, optimal=True, objective=self.objective)
         self.U = self.Us.copy()
 
 
@@ -417,14 +445,23 @@ def gen_kinematics(rob, n=24, seed=1):
     return np.array(qs), np.array(vs), np.array(taus), np.array(outs)
 
 
-def gen_updates(rob, S, K, H, updates, seed, smoothing=None):
+def near_limits():
+    """HUDDLED with joint 1 and joint 4 just inside TrackPoint's upper limits (2.8973, 0.0698)."""
+    x = huddled()
+    x[3], x[6] = 2.89, 0.06
+    return x
+
+
+def gen_updates(rob, S, K, H, updates, seed, smoothing=None, track_point=False):
     dt = 0.01
-    m = MPPI(rob, S, K, H, dt, VAR, CMIN, CMAX, huddled(), smoothing)
+    x0 = near_limits() if track_point else huddled()
+    m = MPPI(rob, S, K, H, dt, VAR, CMIN, CMAX, x0, smoothing,
+             objective=track_point_cost if track_point else None)
     rng = np.random.default_rng(seed)
     sd = np.sqrt(VAR)
     forecast = np.zeros((H, 6))
     forecast[:, 0] = 20.0
-    x = huddled()
+    x = x0.copy()
     rec = {k: [] for k in ("eps", "costs", "weights", "gradient", "U", "opt_cost", "time")}
     for j in range(updates):
         t = 0.05 * j
@@ -439,11 +476,13 @@ def gen_updates(rob, S, K, H, updates, seed, smoothing=None):
         rec["opt_cost"].append(m.opt_cost)
         rec["time"].append(t)
         print("  update %d: min cost %.6e argmin %d" % (j, np.nanmin(m.cost), int(np.nanargmin(m.cost))))
-    out = dict(S=S, K=K, H=H, x0=huddled(), forecast=forecast,
+    out = dict(S=S, K=K, H=H, x0=x0, forecast=forecast,
                eps=np.concatenate(rec["eps"]), eps_counts=np.array([len(e) for e in rec["eps"]]),
                costs=np.array(rec["costs"]), weights=np.array(rec["weights"]), gradient=np.array(rec["gradient"]),
                U=np.array(rec["U"]), opt_cost=np.array(rec["opt_cost"]), time=np.array(rec["time"]),
-               smoothing=np.array(smoothing if smoothing else (0, 0)))
+               smoothing=np.array(smoothing if smoothing else (0, 0)),
+               objective=np.array("track_point" if track_point else "assisted_manipulation"),
+               track_point=TP_POINT)
     return out
 
 
@@ -459,6 +498,9 @@ def main():
     np.savez_compressed(os.path.join(HERE, "update_s16_h8.npz"), **gen_updates(rob, 16, 4, 8, 4, seed=21))
     print("update fixtures: 24 x 16 with SG(4, 1)")
     np.savez_compressed(os.path.join(HERE, "update_s24_h16_sg.npz"), **gen_updates(rob, 24, 6, 16, 4, seed=22, smoothing=(4, 1)))
+    print("update fixtures: 16 x 8, TrackPoint objective (all terms)")
+    np.savez_compressed(os.path.join(HERE, "update_s16_h8_trackpoint.npz"),
+                        **gen_updates(rob, 16, 4, 8, 4, seed=23, track_point=True))
     if "--config1" in sys.argv:
         print("update fixtures: config 1 (128 x 32)")
         np.savez_compressed(os.path.join(HERE, "update_s128_h32.npz"), **gen_updates(rob, 128, 20, 32, 3, seed=12345))

@@ -14,10 +14,11 @@ WEIGHT_ATOL = 1e-11
 CONTROL_ATOL = 1e-9      # U*, gradient (controls reach O(100) for arm torques)
 
 
-def fr_pair(S, horison, K=20, smoothing=None, mode=0, threads=8, forecast=True):
+def fr_pair(S, horison, K=20, smoothing=None, mode=0, threads=8, forecast=True, cost=None):
     conf = am.frankaridgeback_configuration(rollouts=S, horison=horison, keep_best_rollouts=K,
                                             smoothing=smoothing, threads=threads)
-    dyn, cost = am.FrankaRidgebackDynamics(), am.AssistedManipulation()
+    dyn = am.FrankaRidgebackDynamics()
+    cost = cost if cost is not None else am.AssistedManipulation()
     dev = am.Trajectory.create(conf, dyn, cost)
     assert dev is not None
     dev.set_noise_source(abi.MPPI_NOISE_HOST_INJECTED)

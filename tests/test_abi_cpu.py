@@ -40,10 +40,11 @@ def test_struct_layout_matches_header(tmp_path):
     src = tmp_path / "sizes.c"
     structs = ["mppi_config", "mppi_body", "mppi_frame", "mppi_frankaridgeback_desc", "mppi_point_mass_desc",
                "mppi_dynamics_desc", "mppi_quadratic", "mppi_barrier", "mppi_assisted_manipulation_desc",
-               "mppi_quadratic_cost_desc", "mppi_cost_desc"]
+               "mppi_quadratic_cost_desc", "mppi_track_point_desc", "mppi_cost_desc"]
     body = "\n".join('printf("%s %%zu\\n", sizeof(%s));' % (s, s) for s in structs)
     body += '\nprintf("off_has_forecast %zu\\n", offsetof(mppi_assisted_manipulation_desc, has_forecast));'
     body += '\nprintf("off_threads %zu\\n", offsetof(mppi_config, threads));'
+    body += '\nprintf("off_track_point %zu\\n", offsetof(mppi_cost_desc, track_point));'
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mppi_amd.h"\nint main(void){%s return 0;}\n' % body)
     exe = tmp_path / "sizes"
     subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)])
@@ -52,11 +53,12 @@ def test_struct_layout_matches_header(tmp_path):
         assert int(got[s]) == C.sizeof(getattr(abi, s)), s
     assert int(got["off_has_forecast"]) == abi.mppi_assisted_manipulation_desc.has_forecast.offset
     assert int(got["off_threads"]) == abi.mppi_config.threads.offset
+    assert int(got["off_track_point"]) == abi.mppi_cost_desc.track_point.offset
 
 
 def test_abi_version_and_defaults():
     L = _lib.load()
-    assert L.mppi_abi_version() == 1
+    assert L.mppi_abi_version() == 2   # 2: mppi_cost_desc.track_point
     m = am.FrankaRidgebackDynamics().model
     assert m.nbodies == 12
     assert [m.bodies[i].parent for i in range(12)] == [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 9]
@@ -68,6 +70,9 @@ def test_abi_version_and_defaults():
     c = am.AssistedManipulation().configuration
     assert c.enable_energy_limit == 0 and c.has_forecast == 1
     assert c.upper_joint_limit[8].bound == 4.53785 and c.velocity_cost[0].quadratic_cost == 1000.0
+    t = am.TrackPoint().configuration   # track_point.hpp:72-107
+    assert list(t.point) == [1.0, 1.0, 1.0] and t.enable_joint_limits == 1 and t.enable_reach_limits == 0
+    assert t.lower_joint_limit[4].scale == 50.0 and t.maximum_reach_limit.bound == 0.8
 
 
 @pytest.mark.parametrize("R,world", [(4098, 1), (4098, 2), (32770, 8), (65538, 8), (130, 3), (7, 3)])

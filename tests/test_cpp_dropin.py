@@ -23,13 +23,15 @@ def test_cpp_dropin_compiles_and_validates_without_gpu():
 
 
 @pytest.mark.gpu
-def test_cpp_dropin_matches_python_api():
+@pytest.mark.parametrize("objective", ["assisted_manipulation", "track_point"])
+def test_cpp_dropin_matches_python_api(objective):
     import assistedmanipulation_amd as am
     from assistedmanipulation_amd import abi
-    out = subprocess.check_output([build(), "256", "0.32", "3"], timeout=300).decode()
+    out = subprocess.check_output([build(), "256", "0.32", "3", objective], timeout=300).decode()
     lines = [json.loads(l) for l in out.strip().split("\n")]
     conf = am.frankaridgeback_configuration(rollouts=256, horison=0.32)
-    t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    cost = am.TrackPoint() if objective == "track_point" else am.AssistedManipulation()
+    t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), cost)
     t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
     t.set_forecast(am.constant_forecast(t.H))
     x = am.huddled_state()

@@ -242,3 +242,51 @@ def test_philox_noise_statistics_and_replay():
         orc.update(x, t)
         assert_update_parity(dev, orc, "philox upd %d" % j)
         prev_costs, prev_noise = dev.costs(), noise
+
+
+def _track_point_all_terms(point=(0.8, 0.6, 0.9)):
+    tp = am.TrackPoint(point=point)
+    c = tp.configuration
+    c.enable_joint_limits = c.enable_self_collision_avoidance = c.enable_reach_limits = 1
+    return tp
+
+
+def test_track_point_objective():
+    """TrackPoint (track_point.cpp) as the device cost, every term enabled,
+    starting next to two joint limits so the hard-coded limit terms fire."""
+    conf, dev, orc, sd = fr_pair(S=128, horison=0.32, cost=_track_point_all_terms())
+    rng = np.random.default_rng(99)
+    x = am.huddled_state()
+    x[3], x[6] = 2.89, 0.06
+    for j in range(4):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert_update_parity(dev, orc, "trackpoint upd %d" % j)
+
+
+@pytest.mark.parametrize("fixture", ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s16_h8_trackpoint.npz"])
+def test_device_against_golden_fixtures(fixture):
+    """The device path against the independent numpy restatement (tests/golden/gen_golden.py)
+    directly, same injected eps: pins the kernels without going through the oracle."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", fixture), allow_pickle=False)
+    S, K, H = int(g["S"]), int(g["K"]), int(g["H"])
+    w, order = (int(v) for v in g["smoothing"])
+    conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=K,
+                                            smoothing=am.Smoothing(w, order) if w else None)
+    tp = "objective" in g and str(g["objective"]) == "track_point"
+    cost = _track_point_all_terms(g["track_point"]) if tp else am.AssistedManipulation()
+    dev = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), cost)
+    dev.set_noise_source(abi.MPPI_NOISE_HOST_INJECTED)
+    dev.set_forecast(g["forecast"])
+    offs = np.concatenate([[0], np.cumsum(g["eps_counts"])])
+    for j, t in enumerate(g["time"]):
+        assert dev.noise_draws(float(t)) == g["eps_counts"][j]
+        dev.inject_noise(g["eps"][offs[j]:offs[j + 1]])
+        dev.update(g["x0"], float(t))
+        c = dev.costs()
+        np.testing.assert_allclose(c, g["costs"][j], rtol=1e-11, atol=0)
+        assert dev.argmin() == int(np.nanargmin(g["costs"][j]))
+        np.testing.assert_allclose(dev.get_weights(), g["weights"][j], rtol=0, atol=1e-10)
+        np.testing.assert_allclose(dev.get_gradient(), g["gradient"][j], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(dev.get_optimal_rollout(), g["U"][j], rtol=0, atol=1e-8)
+        assert abs(dev.get_optimal_total_cost() - g["opt_cost"][j]) <= 1e-11 * abs(g["opt_cost"][j])

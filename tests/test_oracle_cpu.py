@@ -79,7 +79,17 @@ def test_sg_weights_against_least_squares():
     np.testing.assert_allclose(g["w10_1"], np.full(21, 1 / 21), rtol=0, atol=1e-15)
 
 
-FIXTURES = ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s128_h32.npz"]
+FIXTURES = ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s128_h32.npz", "update_s16_h8_trackpoint.npz"]
+
+
+def fixture_objective(g):
+    """The cost plugin a golden fixture was generated with (gen_golden.py)."""
+    if "objective" in g and str(g["objective"]) == "track_point":
+        tp = am.TrackPoint(point=g["track_point"])
+        c = tp.configuration
+        c.enable_joint_limits = c.enable_self_collision_avoidance = c.enable_reach_limits = 1
+        return tp
+    return am.AssistedManipulation()
 
 
 @pytest.mark.parametrize("fixture", FIXTURES)
@@ -95,7 +105,7 @@ def test_full_updates_against_numpy_restatement(model, fixture, mode):
                                             smoothing=am.Smoothing(w, order) if w else None, threads=4)
     assert conf.steps == H
     cc, keep = conf.to_c()
-    orc = O.OracleTrajectory(cc, am.FrankaRidgebackDynamics().descriptor(), am.AssistedManipulation().descriptor(),
+    orc = O.OracleTrajectory(cc, am.FrankaRidgebackDynamics().descriptor(), fixture_objective(g).descriptor(),
                              mode=mode, compat_uint8=1)
     orc.set_forecast(g["forecast"])
     offs = np.concatenate([[0], np.cumsum(g["eps_counts"])])

@@ -313,6 +313,35 @@ static inline void mppi_assisted_manipulation_default(mppi_assisted_manipulation
     a->has_forecast = 1;
 }
 
+/* TrackPoint::DEFAULT_CONFIGURATION (frankaridgeback/objective/track_point.hpp:72-107). */
+static inline void mppi_track_point_default(mppi_track_point_desc *t)
+{
+    static const double lower[12][2] = {{-2.0, 1.0}, {-2.0, 0.0}, {-6.28, 0.0}, {-2.8, 10.0},
+        {-1.745, 50.0}, {-2.8, 10.0}, {-3.0718, 10.0}, {-2.7925, 10.0}, {0.349, 10.0},
+        {-2.967, 10.0}, {0.0, 10.0}, {0.0, 10.0}};
+    static const double upper[12][2] = {{2.0, 0.0}, {2.0, 0.0}, {6.28, 0.0}, {2.8, 10.0},
+        {1.745, 50.0}, {2.8, 10.0}, {0.0, 10.0}, {2.7925, 10.0}, {4.53785, 10.0},
+        {2.967, 10.0}, {0.5, 10.0}, {0.5, 10.0}};
+    static const double radii[8] = {0.75, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1};
+    int i;
+    memset(t, 0, sizeof(*t));
+    t->point[0] = 1.0;
+    t->point[1] = 1.0;
+    t->point[2] = 1.0;
+    t->enable_joint_limits = 1;
+    t->enable_self_collision_avoidance = 0;
+    t->enable_power_limit = 0;
+    t->enable_reach_limits = 0;
+    for (i = 0; i < 12; i++) {
+        t->lower_joint_limit[i] = mppi_barrier_make(lower[i][0], lower[i][1]);
+        t->upper_joint_limit[i] = mppi_barrier_make(upper[i][0], upper[i][1]);
+    }
+    t->self_collision_limit = mppi_barrier_make(0.0, 1.0);
+    for (i = 0; i < 8; i++)
+        t->self_collision_radii[i] = radii[i];
+    t->maximum_reach_limit = mppi_barrier_make(0.8, 1.0);
+}
+
 /* make_state(Preset::HUDDLED) (frankaridgeback/state.cpp:15-18): energy 100. */
 static inline void mppi_frankaridgeback_huddled(double x[MPPI_FR_STATE])
 {
