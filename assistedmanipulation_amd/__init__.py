@@ -17,7 +17,10 @@ from .trajectory import (AssistedManipulation, Cost, Dynamics, EngineError, Trac
                          FrankaRidgebackDynamics, PointMassDynamics, QuadraticCost, Trajectory,
                          comm_unique_id, shard_range)
 
+from .csvlog import MPPILogger  # noqa: E402
+
 __all__ = [
+    "MPPILogger",
     "abi", "Configuration", "Smoothing", "constant_forecast", "frankaridgeback_configuration",
     "huddled_state", "point_mass_configuration", "AssistedManipulation", "TrackPoint", "Cost", "Dynamics",
     "EngineError", "FrankaRidgebackDynamics", "PointMassDynamics", "QuadraticCost", "Trajectory",

@@ -2,7 +2,8 @@
 // FrankaRidgeback::Actor drives mppi::Trajectory (actor.cpp:96-101, 166-203):
 // create -> per control period: set_forecast, update(state, t), get(control, t).
 // Prints one JSON object per update.
-// Usage: trajectory_demo [rollouts] [horison] [updates] [assisted_manipulation|track_point]
+// Usage: trajectory_demo [rollouts] [horison] [updates] [assisted_manipulation|track_point] [log folder]
+// With a log folder, logger::MPPI (mppi_amd_logging.hpp) writes the reference's CSV files there.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -10,6 +11,7 @@
 #include <vector>
 
 #include "mppi_amd.hpp"
+#include "mppi_amd_logging.hpp"
 
 int main(int argc, char **argv)
 {
@@ -49,6 +51,16 @@ int main(int argc, char **argv)
     }
     auto traj = mppi::Trajectory::create(c, std::make_unique<FrankaRidgeback::PinocchioDynamics>(), objective());
     if (!traj) return 2;
+    std::unique_ptr<logger::MPPI> log;
+    if (argc > 5) {   // base.cpp:49-61: the logger sized to the controller's rollout count
+        logger::MPPI::Configuration lc;
+        lc.folder = argv[5];
+        lc.state_dof = MPPI_FR_STATE;
+        lc.control_dof = MPPI_FR_CONTROL;
+        lc.rollouts = traj->get_rollout_count();
+        log = logger::MPPI::create(lc);
+        if (!log) return 3;
+    }
     traj->set_noise_source(MPPI_NOISE_DEVICE_PHILOX, 0x5EED);
     std::vector<double> forecast(6 * traj->get_step_count(), 0.0);
     for (unsigned k = 0; k < traj->get_step_count(); k++) forecast[6 * k] = 20.0;
@@ -58,6 +70,7 @@ int main(int argc, char **argv)
         const double t = 0.05 * j;
         traj->update(state, t);
         traj->get(control, t + 0.013);
+        if (log) log->log(*traj);
         std::vector<double> costs = traj->get_costs();
         long best = 0;
         for (long r = 1; r < (long)costs.size(); r++)

@@ -44,3 +44,31 @@ def test_cpp_dropin_matches_python_api(objective):
         assert rec["optimal_cost"] == t.get_optimal_total_cost()
         assert rec["u0"] == u[0] and rec["u3"] == u[3]
         assert rec["update_count"] == j + 1
+
+
+@pytest.mark.gpu
+def test_csv_logger_cpp_and_python_write_the_same_files(tmp_path):
+    """SURVEY §8f item 4: logger::MPPI (include/mppi_amd_logging.hpp) and the Python
+    MPPILogger write the reference's CSV layout byte-for-byte identically for the same run
+    (update.csv holds wall-clock durations and is only checked for shape)."""
+    import assistedmanipulation_amd as am
+    from assistedmanipulation_amd import abi
+    from assistedmanipulation_amd.csvlog import MPPILogger
+    cdir, pdir = tmp_path / "cpp", tmp_path / "py"
+    subprocess.check_output([build(), "64", "0.16", "3", "assisted_manipulation", str(cdir)], timeout=300)
+    conf = am.frankaridgeback_configuration(rollouts=64, horison=0.16)
+    t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    t.set_forecast(am.constant_forecast(t.H))
+    log = MPPILogger(str(pdir), control_dof=t.C, rollouts=t.get_rollout_count())
+    x = am.huddled_state()
+    for j in range(3):
+        t.update(x, 0.05 * j)
+        log.log(t)
+        log.log(t)   # same update time: skipped, as in the reference
+    log.close()
+    for name in ("costs.csv", "weights.csv", "gradient.csv", "optimal_rollout.csv", "optimal_cost.csv"):
+        assert (cdir / name).read_text() == (pdir / name).read_text(), name
+    cu, pu = (cdir / "update.csv").read_text().splitlines(), (pdir / "update.csv").read_text().splitlines()
+    assert cu[0] == pu[0] == "update, time, update_duration" and len(cu) == len(pu) == 4
+    assert [l.split(", ")[:2] for l in cu] == [l.split(", ")[:2] for l in pu]
