@@ -295,7 +295,11 @@ void dfree(mppi_handle *h, double *&p)
 }
 
 // The single-lane kernel (MPPI_FR_KERNEL=lane, A/B runs) implements AssistedManipulation only.
-bool use_coop(const mppi_handle *h) { return h->coop || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION; }
+// the lane kernel implements the default AssistedManipulation only (no TrackPoint, no energy tank)
+bool use_coop(const mppi_handle *h)
+{
+    return h->coop || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || h->am.enable_energy_limit;
+}
 
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
@@ -382,8 +386,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     if (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         mppi_status st = check_topology(dyn->frankaridgeback, why);
         if (st != MPPI_OK) return fail(nullptr, st, why);
-        if (cost->kind == MPPI_COST_ASSISTED_MANIPULATION && cost->assisted_manipulation.enable_energy_limit)
-            return fail(nullptr, MPPI_ERR_UNSUPPORTED, "enable_energy_limit needs the NLE power term (SURVEY §8f item 3, not built yet)");
     }
 
     h = new mppi_handle();
@@ -489,6 +491,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
                 m.f11_p[r] = (R10[r] * (p11[0] - p10[0]) + R10[3 + r] * (p11[1] - p10[1])) + R10[6 + r] * (p11[2] - p10[2]);
             }
         }
+        for (int k = 0; k < 3; k++) m.gravity[k] = d.gravity[k];
         CREATE_TRY(dalloc(h, &h->d_model, 1));
         CREATE_TRY(hipMemcpy(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
         const mppi_assisted_manipulation_desc &a = cost->assisted_manipulation;
@@ -524,6 +527,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         c.en_self = a.enable_self_collision_limit;
         c.en_work = a.enable_workspace_limit;
         c.en_energy = a.enable_energy_limit;
+        c.en_below = devb(a.energy_limit_below);
+        c.en_above = devb(a.energy_limit_above);
         c.en_vel = a.enable_velocity_cost;
         c.en_traj = a.enable_trajectory_cost;
         c.en_manip = a.enable_manipulability_cost;
@@ -779,6 +784,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.optimal = 0;
         a.status = h->d_status;
         a.cost_kind = h->cost_kind;
+        a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream) : launch_fr_rollout(a, h->stream));
     } else {
         PmRolloutArgs a{};
@@ -868,6 +874,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         a.H = (int)h->H;
         a.optimal = 1;
         a.cost_kind = h->cost_kind;
+        a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
     } else {
         PmRolloutArgs a{};

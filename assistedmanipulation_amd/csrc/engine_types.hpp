@@ -37,6 +37,7 @@ struct DevModel {
     // placement of body 11 relative to body 10's placement, (R10^T R11, R10^T (p11 - p10)): the
     // cooperative kernel's prefix scan reaches finger 11 through finger 10 (fr_coop.hip)
     double f11_R[9], f11_p[3];
+    double gravity[3];   // Pinocchio's model.gravity: the NLE of the energy tank's power
 };
 
 struct DevBarrier {
@@ -61,6 +62,8 @@ struct DevCost {
     double tp_lo[FR_NB], tp_up[FR_NB];   // joint_limit_cost's hard-coded limits (joints 0..9 read)
     double tp_self;                      // self_collision_cost with get_link_position == 0
     DevBarrier tp_reach;                 // maximum_reach_limit (right)
+    // energy_cost (assisted_manipulation.cpp:211-222): Left / Right barriers of the tank energy
+    DevBarrier en_below, en_above;
 };
 
 // trajectory_cost() constants of step k (assisted_manipulation.cpp:237-290): everything that

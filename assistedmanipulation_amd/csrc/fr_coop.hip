@@ -39,6 +39,7 @@
 #include "kernels.hpp"
 
 using namespace mppi_eng;
+using mppi_dev::smax;
 using mppi_dev::smin;
 
 namespace {
@@ -58,13 +59,16 @@ constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 stor
 constexpr int L_I = 0;
 constexpr int L_S = 274;                    // 16-byte aligned
 constexpr int LDS_KIN = 368;                // >= L_S + NSLOT * 6, = 16 (mod 32) doubles
+constexpr int L_F = 352;                    // energy tank: spatial force f of each body slot
+constexpr int LDS_KIN_EN = 432;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
 constexpr int L_U = 0;
 constexpr int L_DU = L_U + FR_NB * ROW;
 constexpr int L_QDD = L_DU + FR_NB * 2;
 constexpr int L_TAU = L_QDD + ROW;
 constexpr int LDS_SCR = 272;                // >= L_TAU + ROW, = 16 (mod 32) doubles
 static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * 6 <= LDS_KIN && L_TAU + ROW <= LDS_SCR, "LDS row layout");
-static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16, "row stride bank offset");
+static_assert(L_S + NSLOT * 6 <= L_F && L_F + NSLOT * 6 <= LDS_KIN_EN, "LDS row layout (energy)");
+static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16, "row stride bank offset");
 
 // Per-block body table (doubles per body): scan placement R p (body 11: relative to body 10),
 // mass, com, inertia, frame offset (EE on body 9, arm mount on body 2), the placement's
@@ -246,11 +250,11 @@ __host__ __device__ constexpr int pidx(int r, int c)
 }
 
 // World spatial inertia of the lane's body (packed 21), from its world pose; M = body table row.
-__device__ __forceinline__ void world_inertia_to_lds(const double *M, const double *R, const double *p, double *dst)
+__device__ __forceinline__ void world_inertia_to_lds(const double *M, const double *R, const double *p, double *dst,
+                                                     double *c, double *Iw)
 {
     const double m = M[T_M];
     const double lc0 = M[T_C], lc1 = M[T_C + 1], lc2 = M[T_C + 2];
-    double c[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) c[r] = ((R[3 * r] * lc0 + R[3 * r + 1] * lc1) + R[3 * r + 2] * lc2) + p[r];
     const double I00 = M[T_I], I01 = M[T_I + 1], I11 = M[T_I + 2], I02 = M[T_I + 3], I12 = M[T_I + 4], I22 = M[T_I + 5];
@@ -263,7 +267,6 @@ __device__ __forceinline__ void world_inertia_to_lds(const double *M, const doub
     }
     const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
     const double cc2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
-    double Iw[6];
     Iw[0] = (RI[0] * R[0] + RI[1] * R[1]) + RI[2] * R[2];
     Iw[1] = (RI[0] * R[3] + RI[1] * R[4]) + RI[2] * R[5];
     Iw[2] = (RI[0] * R[6] + RI[1] * R[7]) + RI[2] * R[8];
@@ -282,11 +285,44 @@ __device__ __forceinline__ void world_inertia_to_lds(const double *M, const doub
     dst[20] = Iw[5] + (m * cc2 - mc2 * c[2]);
 }
 
+// Inclusive prefix sum over the row's lanes of a 6-vector (Hillis-Steele, row_shr 1, 2, 4, 8).
+__device__ __forceinline__ void prefix6(double *x)
+{
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] += shr<1>(x[k]);
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] += shr<2>(x[k]);
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] += shr<4>(x[k]);
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] += shr<8>(x[k]);
+}
+__device__ __forceinline__ void cross3(const double *a, const double *b, double *o)
+{
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Spatial inertia (mass m, world com c, rotational inertia Iw about the com, packed xx xy xz yy
+// yz zz) times a motion [v; w] at the world origin: [m (v + w x c); Iw w + c x m (v + w x c)].
+__device__ __forceinline__ void inertia_mul(double m, const double *c, const double *Iw, const double *x, double *h)
+{
+    double wc[3], vc[3], ch[3];
+    cross3(x + 3, c, wc);
+#pragma unroll
+    for (int k = 0; k < 3; k++) { vc[k] = x[k] + wc[k]; h[k] = m * vc[k]; }
+    cross3(c, h, ch);
+    h[3] = ((Iw[0] * x[3] + Iw[1] * x[4]) + Iw[2] * x[5]) + ch[0];
+    h[4] = ((Iw[1] * x[3] + Iw[3] * x[4]) + Iw[4] * x[5]) + ch[1];
+    h[5] = ((Iw[2] * x[3] + Iw[4] * x[4]) + Iw[5] * x[5]) + ch[2];
+}
+
 // What the cost of the next step needs from a calculate(): EE and arm-mount positions (the
 // workspace term also reads the next yaw) and the two terms that depend on the kinematics alone
 // (trajectory: frame velocity; manipulability: J_a J_a^T), folded to scalars right away.
 struct CoopKin {
     double ee[3], am[3], traj, manip;
+    double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
 };
 
 __device__ __forceinline__ double trajectory_term(const DevCost &Cs, const StepConst &sc, const double *vl)
@@ -316,9 +352,10 @@ struct LaneConst {
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
-template <int CK>
+template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
-                                        double *Lk, const DevCost &Cs, const StepConst &sc_next, CoopKin &kin)
+                                        double *Lk, const DevCost &Cs, const StepConst &sc_next, CoopKin &kin,
+                                        const double *grav)
 {
     const double cz = L.is_rz ? cq : 1.0;
     const double sz = L.is_rz ? sq : 0.0;
@@ -356,9 +393,54 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     S[3] = w[0] * rotf;
     S[4] = w[1] * rotf;
     S[5] = w[2] * rotf;
-    world_inertia_to_lds(M, R, p, Lk + L_I + L.slot * 21);
+    double com[3], Iw[6];
+    world_inertia_to_lds(M, R, p, Lk + L_I + L.slot * 21, com, Iw);
 #pragma unroll
     for (int k = 0; k < 6; k++) Lk[L_S + L.slot * 6 + k] = S[k];
+    kin.pw = 0.0;
+    if constexpr (EN) {
+        // The energy tank's power needs tau = tau_u + nonLinearEffects(q, v) (pinocchio_dynamics.cpp:
+        // 156, 248-251).  With W_j = sum_{i <= j} S_i v_new,i, NLE . v_new = sum_j f_j . W_j where
+        // f_j = I_j A_j + V_j x* I_j V_j is body j's RNEA force (world frame, at the origin):
+        //   V_j = sum_{i <= j} S_i qd_i,   A_j = -g + sum_{i <= j} V_i x S_i qd_i   (prefix sums)
+        // and W_j = V_j + dt sum_{i <= j} S_i qdd_i: the f . V part is summed here, the qdd part in
+        // the ABA's forward pass (coop_aba).  Finger 11's prefix drops finger 10's term.
+        double xs[6], V[6], cA[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) xs[k] = S[k] * qd;
+#pragma unroll
+        for (int k = 0; k < 6; k++) V[k] = xs[k] + M[T_FIX] * shr<1>(xs[k]);
+        prefix6(V);
+        double t0[3], t1[3];
+        cross3(V + 3, xs, t0);
+        cross3(V, xs + 3, t1);
+        cross3(V + 3, xs + 3, cA + 3);
+#pragma unroll
+        for (int k = 0; k < 3; k++) cA[k] = t0[k] + t1[k];
+        double A[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) A[k] = cA[k] + M[T_FIX] * shr<1>(cA[k]);
+        prefix6(A);
+#pragma unroll
+        for (int k = 0; k < 3; k++) A[k] -= grav[k];
+        const double m = M[T_M];
+        double hA[6], hV[6], f[6];
+        inertia_mul(m, com, Iw, A, hA);
+        inertia_mul(m, com, Iw, V, hV);
+        // V x* h = [w x h_lin; w x h_ang + v x h_lin]
+        double g0[3], g1[3], g2[3];
+        cross3(V + 3, hV, g0);
+        cross3(V + 3, hV + 3, g1);
+        cross3(V, hV, g2);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            f[k] = hA[k] + g0[k];
+            f[3 + k] = hA[3 + k] + (g1[k] + g2[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) Lk[L_F + L.slot * 6 + k] = f[k];
+        kin.pw = ((f[0] * V[0] + f[1] * V[1]) + f[2] * V[2]) + ((f[3] * V[3] + f[4] * V[4]) + f[5] * V[5]);
+    }
     double fpos[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) fpos[r] = p[r] + ((R[3 * r] * M[T_F] + R[3 * r + 1] * M[T_F + 1]) + R[3 * r + 2] * M[T_F + 2]);
@@ -390,7 +472,8 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 // lanes 0..5 and 8..13 hold rows 0..5 (lanes 6, 7, 14, 15 mirror row 5 and are masked out of the
 // sums), so one 3-stage butterfly leaves the full sum in every lane.  tau_i and U of body i are
 // LDS broadcasts.
-__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
+template <bool EN>
+__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, double &pe)
 {
     const int r = j < 6 ? j : 5;   // lanes 0..5 hold rows 0..5; the others mirror row 5, unused
     int off[6];
@@ -449,20 +532,24 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
     }
     double acc = 0.0, a9 = 0.0;
     double Srf = Lk[L_S + r], Uf = Lw[L_U + j], Dvf = Lw[L_DU], uf = Lw[L_DU + 1];
+    double Ff = EN ? Lk[L_F + r] : 0.0;
+    pe = 0.0;
 #pragma unroll
     for (int i = 0; i < FR_NB; i++) {
-        const double Sr = Srf, Ui = Uf, Dv = Dvf, ui = uf;
+        const double Sr = Srf, Ui = Uf, Dv = Dvf, ui = uf, Fr = Ff;
         if (i + 1 < FR_NB) {
             Srf = Lk[L_S + (i + 1) * 6 + r];
             Uf = Lw[L_U + (i + 1) * ROW + j];
             Dvf = Lw[L_DU + 2 * (i + 1)];
             uf = Lw[L_DU + 2 * (i + 1) + 1];
+            if constexpr (EN) Ff = Lk[L_F + (i + 1) * 6 + r];
         }
         const double ap = (i == 11) ? a9 : acc;
         const double ua = bsum<0, 6>(Ui * ap, 1.0);
         const double dd = Dv * (ui - ua);
         acc = ap + Sr * dd;
         if (i == 9) a9 = acc;
+        if constexpr (EN) pe += Fr * acc;   // row r of f_i . sum_{k <= i} S_k qdd_k
         Lw[L_QDD + i] = dd;
     }
     const double qdd = Lw[L_QDD + (j < FR_NB ? j : 0)];
@@ -471,8 +558,9 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw)
 
 // AssistedManipulation::get_cost at x_k with the kinematics of the previous calculate()
 // (assisted_manipulation.cpp:58-128, term order kept); row-uniform result.
+template <bool EN>
 __device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, const double *M, double q, double qd, double sq,
-                                                  double cq, const CoopKin &kin)
+                                                  double cq, const CoopKin &kin, double E)
 {
     const DevBarrier lo_b{M[T_LO], M[T_LO + 1], M[T_LO + 2]}, up_b{M[T_UP], M[T_UP + 1], M[T_UP + 2]};
     const double vel_w = M[T_VW];
@@ -506,6 +594,7 @@ __device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, co
     cost += Cs.en_joint ? joint : 0.0;
     cost += Cs.en_self ? Cs.self_collision : 0.0;
     cost += Cs.en_work ? wc : 0.0;
+    if constexpr (EN) cost += left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);   // energy_cost (:211-222)
     cost += Cs.en_vel ? vel : 0.0;
     cost += Cs.en_traj ? kin.traj : 0.0;
     cost += Cs.en_manip ? kin.manip : 0.0;
@@ -542,26 +631,27 @@ __device__ __forceinline__ double track_point_terms(const DevCost &Cs, int j, do
     return cost;
 }
 
-template <int CK>
+template <int CK, bool EN>
 __device__ __forceinline__ double objective_terms(const DevCost &Cs, bool jl, int j, const double *M, double q, double qd, double sq,
-                                                  double cq, const CoopKin &kin)
+                                                  double cq, const CoopKin &kin, double E)
 {
     if constexpr (CK == CK_TRACK_POINT) return track_point_terms(Cs, j, q, sq, cq, kin);
-    else return step_cost_terms(Cs, jl, M, q, qd, sq, cq, kin);
+    else return step_cost_terms<EN>(Cs, jl, M, q, qd, sq, cq, kin, E);
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int CK>
+template <int CK, bool EN>
 __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
 {
-    __shared__ double lds_kin[ROWS_PER_WAVE * LDS_KIN];
+    constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
+    __shared__ double lds_kin[ROWS_PER_WAVE * KS];
     __shared__ double lds_scr[ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;
     const int lane = threadIdx.x;
     const int j = lane & (ROW - 1);
     const int rowi = lane >> 4;
-    double *Lk = lds_kin + rowi * LDS_KIN;
+    double *Lk = lds_kin + rowi * KS;
     double *Lw = lds_scr + rowi * LDS_SCR;
     {   // stage the body table
         const DevModel &dm = *a.model;
@@ -618,10 +708,12 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
     double q = live && jl ? a.x0[jb] : 0.0;
     double qd = live && jl ? a.x0[FR_NB + jb] : 0.0;
+    double E = EN && live ? a.x0[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+    const double *grav = a.model->gravity;
     double sq, cq;
     sincos(q, &sq, &cq);   // one sincos per lane and step: FK, base yaw, workspace
     CoopKin kin;
-    coop_fk<CK>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[0], kin);   // set_state -> calculate() at (q0, v0)
+    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[0], kin, grav);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step, first used after its cost
     const bool sampled = !a.optimal && live && jl;
@@ -635,7 +727,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
-        const double step_cost = a.steps[k].gamma_k * objective_terms<CK>(Cs, jl, j, M, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[k].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
         {
@@ -646,10 +738,16 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             qd = (j == 0) ? vx : ((j == 1) ? vy : ((j == 2) ? u : qd));
         }
         Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
-        coop_fk<CK>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin);
-        const double qdd = coop_aba(j, Lk, Lw);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin, grav);
+        double pe;
+        const double qdd = coop_aba<EN>(j, Lk, Lw, pe);
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
+        if constexpr (EN) {   // power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
+            const double tau_l = (j >= 3 && j < 10) ? u : 0.0;
+            const double power = bsum<0, FR_NB>(tau_l * qd + kin.pw, 1.0) + a.dt * bsum<0, 6>(pe, 1.0);
+            E = smax(0.0, E + power * a.dt);
+        }
         sincos(q, &sq, &cq);
         if (!a.optimal && isnan(step_cost)) {   // rollout cost NaN: stop (mppi.cpp:331-334)
             J = NAN;
@@ -659,7 +757,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         J += step_cost;
     }
     if (alive) {   // the final step's cost; its dynamics are never observed
-        const double step_cost = a.steps[H - 1].gamma_k * objective_terms<CK>(Cs, jl, j, M, q, qd, sq, cq, kin);
+        const double step_cost = a.steps[H - 1].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
         J = (!a.optimal && isnan(step_cost)) ? NAN : J + step_cost;
     }
     if (!live || j != 0) return;
@@ -673,8 +771,9 @@ hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
 {
     const unsigned nb = (unsigned)((a.count + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
     if (nb == 0) return hipSuccess;
-    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL(fr_coop_kernel<CK_TRACK_POINT>, dim3(nb), dim3(COOP_NT), 0, s, a);
-    else hipLaunchKernelGGL(fr_coop_kernel<CK_ASSISTED_MANIPULATION>, dim3(nb), dim3(COOP_NT), 0, s, a);
+    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_coop_kernel<CK_TRACK_POINT, false>), dim3(nb), dim3(COOP_NT), 0, s, a);
+    else if (a.energy) hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, true>), dim3(nb), dim3(COOP_NT), 0, s, a);
+    else hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, false>), dim3(nb), dim3(COOP_NT), 0, s, a);
     return hipGetLastError();
 }
 

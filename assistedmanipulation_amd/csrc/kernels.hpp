@@ -31,6 +31,7 @@ struct FrRolloutArgs {
     int H;
     int optimal;
     int cost_kind;            // mppi_cost_kind: AssistedManipulation or TrackPoint
+    int energy;               // AssistedManipulation enable_energy_limit: the tank's NLE power
 };
 
 // sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).

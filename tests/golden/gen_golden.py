@@ -128,6 +128,71 @@ class Robot:
             M += m * Jv.T @ Jv + Jw.T @ Iw @ Jw
         return M
 
+    def link_pose_any(self, q, link):
+        """link_pose for real or complex q (np.sin / np.cos): the complex-step derivatives of
+        nle() differentiate the mass matrix through it."""
+        dtype = np.complex128 if np.iscomplexobj(q) else np.float64
+        T = np.eye(4, dtype=dtype)
+        axes = {}
+        for jn in self.chain(link):
+            j = self.joints[jn]
+            T = T @ origin_T(j)
+            t = j.get("type")
+            if t in ("revolute", "prismatic"):
+                a = np.array([float(v) for v in j.find("axis").get("xyz").split()])
+                qi = q[self.dof.index(jn)]
+                axes[jn] = (T[:3, :3] @ a, T[:3, 3].copy(), t)
+                M = np.eye(4, dtype=dtype)
+                if t == "revolute":
+                    a = a / np.linalg.norm(a)
+                    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+                    M[:3, :3] = np.eye(3) + np.sin(qi) * K + (1 - np.cos(qi)) * K @ K
+                else:
+                    M[:3, 3] = a * qi
+                T = T @ M
+        return T, axes
+
+    def link_jacobians(self, q, link):
+        """World com, linear and angular Jacobians of a link's centre of mass (real or complex q)."""
+        m, c_local, I_local = self.inertial[link]
+        T, axes = self.link_pose_any(q, link)
+        R, p = T[:3, :3], T[:3, 3]
+        c = p + R @ c_local
+        n = len(self.dof)
+        Jv = np.zeros((3, n), dtype=T.dtype)
+        Jw = np.zeros((3, n), dtype=T.dtype)
+        for jn, (a, o, t) in axes.items():
+            k = self.dof.index(jn)
+            if t == "revolute":
+                Jv[:, k] = np.cross(a, c - o)
+                Jw[:, k] = a
+            else:
+                Jv[:, k] = a
+        return R, c, Jv, Jw
+
+    def mass_matrix_any(self, q):
+        n = len(self.dof)
+        M = np.zeros((n, n), dtype=np.complex128 if np.iscomplexobj(q) else np.float64)
+        for link, (m, c_local, I_local) in self.inertial.items():
+            R, c, Jv, Jw = self.link_jacobians(q, link)
+            Iw = R @ I_local @ R.T
+            M += m * Jv.T @ Jv + Jw.T @ Iw @ Jw
+        return M
+
+    def nle(self, q, v, g=9.81, h=1e-20):
+        """Coriolis/centrifugal + gravity torques from the Lagrangian, independent of RNEA:
+        g(q) = sum_l m_l Jv_l^T (0, 0, g) and C(q, v) v = Mdot v - 1/2 d(v^T M v)/dq, with Mdot and
+        dM/dq_i by complex-step differentiation of the composite-Jacobian mass matrix (exact to
+        rounding: no subtractive cancellation)."""
+        n = len(self.dof)
+        grav = np.zeros(n)
+        for link, (m, c_local, I_local) in self.inertial.items():
+            R, c, Jv, Jw = self.link_jacobians(q, link)
+            grav += m * (Jv.T @ np.array([0.0, 0.0, g]))
+        Mdot = self.mass_matrix_any(q + 1j * h * v).imag / h
+        dT = np.array([v @ (self.mass_matrix_any(q + 1j * h * np.eye(n)[i]).imag / h) @ v for i in range(n)])
+        return Mdot @ v - 0.5 * dT + grav
+
     def frame(self, q, link):
         T, axes = self.link_pose(q, link)
         return T
@@ -197,7 +262,7 @@ PAIRS = [(3, l) for l in (6, 7, 8, 9, 10)] + [(4, l) for l in (6, 7, 8, 9, 10)] 
         [(6, l) for l in (8, 9, 10)] + [(7, l) for l in (9, 10)] + [(8, 10)]
 
 
-def cost(x, k_cache, force):
+def cost(x, k_cache, force, energy=False):
     q, v = x[:12], x[12:24]
     c = 0.0
     c += sum(left(*LOWER[i], q[i]) + right(*UPPER[i], q[i]) for i in range(12))
@@ -213,6 +278,8 @@ def cost(x, k_cache, force):
         ws += 400.0 * yaw * yaw
     ws += left(0.0, 1.0, ee[2] - robot[2])
     c += ws
+    if energy:   # energy_cost: Left(0, 10) + Right(20, 10) of the tank energy (x[30])
+        c += left(0.0, 10.0, x[30]) + right(20.0, 10.0, x[30])
     c += sum(VEL[i] * v[i] ** 2 for i in range(12))
     target = np.clip(0.01 * np.asarray(force[:3]), -1.0, 1.0)
     dist = np.linalg.norm(target)
@@ -257,7 +324,37 @@ def track_point_cost(x, k_cache, force):
     return c
 
 
-def step(rob, x, u, dt):
+def energy_only_cost(x, k_cache, force):
+    """AssistedManipulation with only enable_energy_limit set: Left(0, 10) + Right(20, 10) of E."""
+    return left(0.0, 10.0, x[30]) + right(20.0, 10.0, x[30])
+
+
+def energy_rollouts(rob, seed=6, H=16):
+    """Free rollouts of the tank from HUDDLED: random controls with E0 = 15 and E0 = 0.05, and two
+    descents (arm torque -s g(q0) lets gravity pull the arm: negative power) that reach the
+    max(0, .) clamp.  Returns E0 [n], controls [n][H][12] and E after each step [n][H]."""
+    rng = np.random.default_rng(seed)
+    g0 = rob.nle(huddled()[:12], np.zeros(12))
+    cases = [(15.0, None), (15.0, None), (0.05, None), (0.05, None), (0.5, 0.1), (0.2, 0.3)]
+    us, es, e0s = [], [], []
+    for e0, s in cases:
+        x = huddled()
+        x[30] = e0
+        if s is None:
+            u = rng.standard_normal((H, 12)) * np.sqrt(VAR) * 3.0
+        else:
+            u = np.zeros((H, 12))
+            u[:, 3:10] = -s * g0[3:10]
+        E = []
+        for k in range(H):
+            x, _ = step(rob, x, u[k], 0.01, energy=True)
+            E.append(x[30])
+        us.append(u); es.append(E); e0s.append(e0)
+    assert min(min(e) for e in es) == 0.0
+    return np.array(us), np.array(es), np.array(e0s)
+
+
+def step(rob, x, u, dt, energy=False):
     q, v = x[:12].copy(), x[12:24].copy()
     c, s = math.cos(q[2]), math.sin(q[2])
     v[0] = c * u[0] - s * u[1]
@@ -267,14 +364,17 @@ def step(rob, x, u, dt):
     tau[3:10] = u[3:10]
     a = np.linalg.solve(rob.mass_matrix(q), tau)
     kc = kin(rob, q, v)     # computed before integration: the one-step lag
+    nle = rob.nle(q, v) if energy else None   # m_joint_torque += NLE at (q, v after the overwrite)
     v = v + a * dt
     q = q + v * dt
     xn = x.copy()
     xn[:12], xn[12:24] = q, v
+    if energy:   # power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
+        xn[30] = max(0.0, x[30] + float((tau + nle) @ v) * dt)
     return xn, kc
 
 
-def rollout(rob, x0, U, eps, dt, forecast, optimal=False, objective=None):
+def rollout(rob, x0, U, eps, dt, forecast, optimal=False, objective=None, energy=False):
     objective = objective or cost
     x = x0.copy()
     kc = kin(rob, x[:12], x[12:24])
@@ -286,7 +386,7 @@ def rollout(rob, x0, U, eps, dt, forecast, optimal=False, objective=None):
             return float("nan")
         J += sc
         if k < U.shape[0] - 1:
-            x, kc = step(rob, x, u, dt)
+            x, kc = step(rob, x, u, dt, energy)
     return J
 
 
@@ -347,8 +447,9 @@ class Window:
 # mppi::Trajectory (mppi.cpp) restated in Python
 # ------------------------------------------------------------------------------------------
 class MPPI:
-    def __init__(self, rob, S, K, H, dt, var, cmin, cmax, x0, smoothing=None, objective=None):
+    def __init__(self, rob, S, K, H, dt, var, cmin, cmax, x0, smoothing=None, objective=None, energy=False):
         self.rob, self.S, self.K, self.H, self.dt = rob, S, K, H, dt
+        self.energy = energy
         self.objective = objective or cost
         self.R = S + 2
         self.C = len(var)
@@ -388,7 +489,8 @@ class MPPI:
                 self.noise[r, k] = next(it)
         self.noise[1] = -self.U
         for r in range(self.R):
-            self.cost[r] = rollout(self.rob, x0, self.Us, self.noise[r], self.dt, forecast, objective=self.objective)
+            self.cost[r] = rollout(self.rob, x0, self.Us, self.noise[r], self.dt, forecast, objective=self.objective,
+                                   energy=self.energy)
         ok = ~np.isnan(self.cost)
         mn, mx = self.cost[ok].min(), self.cost[ok].max()
         if mx - mn >= 1e-6:
@@ -409,7 +511,8 @@ class MPPI:
                         self.Us[k, c] = r
                         win.uu[idx - 1] = r
             self.Us = np.maximum(np.minimum(self.Us, self.cmax), self.cmin)
-        self.opt_cost = rollout(self.rob, x0, self.Us, None, self.dt, forecast, optimal=True, objective=self.objective)
+        self.opt_cost = rollout(self.rob, x0, self.Us, None, self.dt, forecast, optimal=True, objective=self.objective,
+                                energy=self.energy)
         self.U = self.Us.copy()
 
 
@@ -452,11 +555,14 @@ def near_limits():
     return x
 
 
-def gen_updates(rob, S, K, H, updates, seed, smoothing=None, track_point=False):
+def gen_updates(rob, S, K, H, updates, seed, smoothing=None, track_point=False, energy0=None):
     dt = 0.01
     x0 = near_limits() if track_point else huddled()
-    m = MPPI(rob, S, K, H, dt, VAR, CMIN, CMAX, x0, smoothing,
-             objective=track_point_cost if track_point else None)
+    objective = track_point_cost if track_point else None
+    if energy0 is not None:   # energy_cost alone (every other term disabled), tank started at energy0
+        x0[30] = energy0
+        objective = energy_only_cost
+    m = MPPI(rob, S, K, H, dt, VAR, CMIN, CMAX, x0, smoothing, objective=objective, energy=energy0 is not None)
     rng = np.random.default_rng(seed)
     sd = np.sqrt(VAR)
     forecast = np.zeros((H, 6))
@@ -481,13 +587,31 @@ def gen_updates(rob, S, K, H, updates, seed, smoothing=None, track_point=False):
                costs=np.array(rec["costs"]), weights=np.array(rec["weights"]), gradient=np.array(rec["gradient"]),
                U=np.array(rec["U"]), opt_cost=np.array(rec["opt_cost"]), time=np.array(rec["time"]),
                smoothing=np.array(smoothing if smoothing else (0, 0)),
-               objective=np.array("track_point" if track_point else "assisted_manipulation"),
+               objective=np.array("track_point" if track_point else ("energy_only" if energy0 is not None else "assisted_manipulation")),
+               energy=np.array(1 if energy0 is not None else 0),
                track_point=TP_POINT)
     return out
 
 
 def main():
     rob = Robot()
+    if "--energy" in sys.argv or not os.path.exists(os.path.join(HERE, "nle.npz")):
+        print("NLE fixtures (complex-step Lagrangian)")
+        rng = np.random.default_rng(5)
+        nq, nv, nn = [], [], []
+        for i in range(12):
+            qq = huddled()[:12] + rng.normal(0, 0.6, 12) * (1 if i else 0)
+            qq[10:] = np.abs(qq[10:]) * 0.05 + 0.01
+            vv = rng.normal(0, 1.5, 12)
+            nq.append(qq); nv.append(vv); nn.append(rob.nle(qq, vv))
+        ru, rE, re0 = energy_rollouts(rob)
+        np.savez_compressed(os.path.join(HERE, "nle.npz"), q=np.array(nq), v=np.array(nv), nle=np.array(nn),
+                            roll_u=ru, roll_E=rE, roll_E0=re0)
+        print("update fixtures: 16 x 8, energy tank enabled (E0 = 15)")
+        np.savez_compressed(os.path.join(HERE, "update_s16_h8_energy.npz"),
+                            **gen_updates(rob, 16, 4, 8, 4, seed=24, energy0=15.0))
+        if "--energy" in sys.argv:
+            return
     print("kinematics fixtures")
     q, v, tau, out = gen_kinematics(rob)
     np.savez_compressed(os.path.join(HERE, "kinematics.npz"), q=q, v=v, tau=tau, out=out)

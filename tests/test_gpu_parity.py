@@ -10,7 +10,7 @@ import assistedmanipulation_amd as am
 from assistedmanipulation_amd import abi
 from oracle import oracle as O
 
-from helpers import assert_update_parity, fr_pair, pm_pair, step_both
+from helpers import assert_update_parity, energy_only_cost, fr_pair, pm_pair, step_both
 
 pytestmark = pytest.mark.gpu
 
@@ -263,7 +263,44 @@ def test_track_point_objective():
         assert_update_parity(dev, orc, "trackpoint upd %d" % j)
 
 
-@pytest.mark.parametrize("fixture", ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s16_h8_trackpoint.npz"])
+def test_energy_tank_with_every_term():
+    """a10.7: enable_energy_limit on top of the default cost stack (the tank's power needs the NLE,
+    SURVEY §8f item 3); tank started inside its barriers."""
+    cost = am.AssistedManipulation()
+    cost.configuration.enable_energy_limit = 1
+    conf, dev, orc, sd = fr_pair(S=128, horison=0.32, cost=cost)
+    rng = np.random.default_rng(31)
+    x = am.huddled_state()
+    x[30] = 15.0
+    for j in range(4):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert_update_parity(dev, orc, "energy+all upd %d" % j)
+
+
+# The barriers amplify the tank's rounding: dJ/J = sum_k |c'(E_k)| E_k / J * (dE/E), and with
+# c = 10/E + 10/(20 - E) a rollout that passes E = 19.995 has sum |c'(E_k)| E_k / J ~ 3.4e3
+# (measured on the oracle: rollout 75 of update 1 below), so 1e-14 relative in E is 3.4e-11 in J.
+ENERGY_COST_RTOL = 1e-9
+ENERGY_WEIGHT_ATOL = 1e-9
+
+
+@pytest.mark.parametrize("e0", [15.0, 0.3])
+def test_energy_only_cost(e0):
+    """The tank's barrier alone decides the weights: every rollout's energy trajectory is checked
+    through its cost; E0 = 0.3 sits next to the Left(0, 10) bound and the max(0, .) clamp, and the
+    state carries a velocity so NLE . v is nonzero from the first step."""
+    conf, dev, orc, sd = fr_pair(S=256, horison=0.32, cost=energy_only_cost())
+    rng = np.random.default_rng(32)
+    x = am.huddled_state()
+    x[30] = e0
+    x[12 + 3:12 + 10] = rng.normal(0, 0.5, 7)
+    for j in range(4):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert_update_parity(dev, orc, "energy-only E0=%g upd %d" % (e0, j), ENERGY_COST_RTOL, ENERGY_WEIGHT_ATOL)
+
+
+@pytest.mark.parametrize("fixture", ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s16_h8_trackpoint.npz",
+                                     "update_s16_h8_energy.npz"])
 def test_device_against_golden_fixtures(fixture):
     """The device path against the independent numpy restatement (tests/golden/gen_golden.py)
     directly, same injected eps: pins the kernels without going through the oracle."""
@@ -273,8 +310,9 @@ def test_device_against_golden_fixtures(fixture):
     w, order = (int(v) for v in g["smoothing"])
     conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=K,
                                             smoothing=am.Smoothing(w, order) if w else None)
-    tp = "objective" in g and str(g["objective"]) == "track_point"
-    cost = _track_point_all_terms(g["track_point"]) if tp else am.AssistedManipulation()
+    objective = str(g["objective"]) if "objective" in g else "assisted_manipulation"
+    cost = {"track_point": lambda: _track_point_all_terms(g["track_point"]),
+            "energy_only": energy_only_cost}.get(objective, am.AssistedManipulation)()
     dev = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), cost)
     dev.set_noise_source(abi.MPPI_NOISE_HOST_INJECTED)
     dev.set_forecast(g["forecast"])
@@ -284,7 +322,7 @@ def test_device_against_golden_fixtures(fixture):
         dev.inject_noise(g["eps"][offs[j]:offs[j + 1]])
         dev.update(g["x0"], float(t))
         c = dev.costs()
-        np.testing.assert_allclose(c, g["costs"][j], rtol=1e-11, atol=0)
+        np.testing.assert_allclose(c, g["costs"][j], rtol=ENERGY_COST_RTOL if objective == "energy_only" else 1e-11, atol=0)
         assert dev.argmin() == int(np.nanargmin(g["costs"][j]))
         np.testing.assert_allclose(dev.get_weights(), g["weights"][j], rtol=0, atol=1e-10)
         np.testing.assert_allclose(dev.get_gradient(), g["gradient"][j], rtol=0, atol=1e-8)

@@ -15,6 +15,8 @@ import pytest
 import assistedmanipulation_amd as am
 from oracle import oracle as O
 
+from helpers import energy_only_cost
+
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
@@ -70,6 +72,31 @@ def test_gravity_torque_matches_potential_gradient(model):
     np.testing.assert_allclose(k["nle"], grad, rtol=0, atol=1e-6)
 
 
+def test_nle_against_complex_step_lagrangian(model):
+    """nonLinearEffects (RNEA, Pinocchio order) = C(q, v) v + g(q) of the numpy model, where C v
+    comes from complex-step derivatives of the composite-Jacobian mass matrix (gen_golden.nle)."""
+    g = load("nle.npz")
+    for q, v, n in zip(g["q"], g["v"], g["nle"]):
+        k = O.kinematics(model, q, v, np.zeros(12), 0)
+        assert np.max(np.abs(k["nle"] - n)) <= 1e-10 * max(1.0, np.max(np.abs(n))), (k["nle"], n)
+
+
+def test_energy_tank_against_numpy(model):
+    """EnergyTank::step with power (tau_u + NLE) . v_new (pinocchio_dynamics.cpp:248-251): the
+    oracle's tank after every step of six free rollouts, two of which reach the max(0, .) clamp."""
+    g = load("nle.npz")
+    cost = energy_only_cost().configuration
+    hit_zero = 0
+    for e0, u, E in zip(g["roll_E0"], g["roll_u"], g["roll_E"]):
+        x0 = am.huddled_state()
+        x0[30] = e0
+        for k in range(1, u.shape[0] + 1):
+            _, sc, xf = O.rollout(model, cost, x0, u[:k], 0.01)
+            assert abs(xf[30] - E[k - 1]) <= 1e-11 * max(1.0, abs(E[k - 1])), (k, xf[30], E[k - 1])
+            hit_zero += xf[30] == 0.0
+    assert hit_zero > 0
+
+
 def test_sg_weights_against_least_squares():
     g = load("sg_weights.npz")
     np.testing.assert_allclose(O.sg_weights(10, 0, 1, 0), g["w10_1"], rtol=0, atol=1e-14)
@@ -79,11 +106,14 @@ def test_sg_weights_against_least_squares():
     np.testing.assert_allclose(g["w10_1"], np.full(21, 1 / 21), rtol=0, atol=1e-15)
 
 
-FIXTURES = ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s128_h32.npz", "update_s16_h8_trackpoint.npz"]
+FIXTURES = ["update_s16_h8.npz", "update_s24_h16_sg.npz", "update_s128_h32.npz", "update_s16_h8_trackpoint.npz",
+            "update_s16_h8_energy.npz"]
 
 
 def fixture_objective(g):
     """The cost plugin a golden fixture was generated with (gen_golden.py)."""
+    if "objective" in g and str(g["objective"]) == "energy_only":
+        return energy_only_cost()
     if "objective" in g and str(g["objective"]) == "track_point":
         tp = am.TrackPoint(point=g["track_point"])
         c = tp.configuration
@@ -99,6 +129,8 @@ def test_full_updates_against_numpy_restatement(model, fixture, mode):
     if not os.path.exists(path):
         pytest.skip("fixture not generated")
     g = np.load(path, allow_pickle=False)
+    if mode == 1 and "energy" in g and int(g["energy"]):
+        pytest.skip("the tank's power needs NLE: reference arithmetic (mode 0) only")
     S, K, H = int(g["S"]), int(g["K"]), int(g["H"])
     w, order = (int(x) for x in g["smoothing"])
     conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=K,
