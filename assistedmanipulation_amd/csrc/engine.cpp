@@ -44,6 +44,11 @@ struct mppi_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
+    // sample()'s stable order of this update's costs, ranked as soon as the costs are final
+    // (after the cost all-reduce) so it runs beside optimise() instead of on the next update's
+    // critical path
+    hipStream_t stream_rank = nullptr;
+    hipEvent_t ev_costs = nullptr, ev_rank = nullptr;
     hipEvent_t ev[6] = {};
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
     bool opt_pending = false;
@@ -88,6 +93,7 @@ struct mppi_handle {
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
     size_t inj_capacity = 0;   // doubles
     int *d_rank = nullptr;
+    uint64_t *d_rank_keys = nullptr;   // rank scratch: chunk-sorted cost keys
     Status *d_status = nullptr;
     double *d_sg_w = nullptr, *d_sg_uu = nullptr, *d_sg_tt = nullptr, *d_sg_last = nullptr;
     int64_t *d_sg_start = nullptr;
@@ -437,6 +443,9 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipSetDevice(device));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
+    CREATE_TRY(hipStreamCreateWithFlags(&h->stream_rank, hipStreamNonBlocking));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_costs, hipEventDisableTiming));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_rank, hipEventDisableTiming));
     for (auto &e : h->ev) CREATE_TRY(hipEventCreate(&e));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_pub, hipEventDisableTiming));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
@@ -457,6 +466,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_rank_keys, (size_t)rank_scratch(h->S)));
     CREATE_TRY(dalloc(h, &h->d_status, 1));
     CREATE_TRY(dalloc(h, &h->d_steps, (size_t)h->H));
     CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocDefault));
@@ -594,6 +604,11 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         st = upload_steps(h);
         if (st != MPPI_OK) return cleanup_fail(st);
     }
+    // the first update's order: every previous cost is 0 (mppi.cpp:222-231: identity).  The
+    // zero-fills above run on the null stream, which the non-blocking streams do not wait for.
+    CREATE_TRY(hipDeviceSynchronize());
+    CREATE_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream_rank));
+    CREATE_TRY(hipEventRecord(h->ev_rank, h->stream_rank));
 #undef CREATE_TRY
     *out = h;
     return MPPI_OK;
@@ -605,6 +620,7 @@ void mppi_destroy(mppi_handle *h)
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
+    if (h->stream_rank) (void)hipStreamSynchronize(h->stream_rank);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
@@ -614,6 +630,9 @@ void mppi_destroy(mppi_handle *h)
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
+    if (h->ev_costs) (void)hipEventDestroy(h->ev_costs);
+    if (h->ev_rank) (void)hipEventDestroy(h->ev_rank);
+    if (h->stream_rank) (void)hipStreamDestroy(h->stream_rank);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -745,8 +764,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         if (need) HIP_TRY(hipMemcpy(h->d_inj, h->inj_pending.data(), need * sizeof(double), hipMemcpyHostToDevice));
         h->inj_pending.erase(h->inj_pending.begin(), h->inj_pending.begin() + (long)need);
     }
-    HIP_TRY(hipMemsetAsync(h->d_rank, 0, (size_t)h->R * sizeof(int), h->stream));
-    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->stream));
+    // the stable order of the previous costs, ranked beside the previous optimise() (phase 2)
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_rank, 0));
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
@@ -812,6 +831,11 @@ mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
+    // the costs are final here (all-reduced when sharded): rank them for the next sample()
+    HIP_TRY(hipEventRecord(h->ev_costs, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream_rank, h->ev_costs, 0));
+    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream_rank));
+    HIP_TRY(hipEventRecord(h->ev_rank, h->stream_rank));
     HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,

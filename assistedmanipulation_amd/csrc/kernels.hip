@@ -510,9 +510,13 @@ constexpr int FR_NT = 64;   // one wave per workgroup; the LDS stack takes 120 K
 // Rank of each sampled rollout (indices 2..R-1) in the stable order of the previous costs.
 // NaN sorts last (the reference's comparator is not a strict weak order with NaN: UB).
 // Costs become order-preserving 64-bit keys (-0 == +0, NaN above +inf); rank_i counts keys below
-// key_i plus equal keys at lower indices.  Grid (ceil(S/256), ceil(S/256)): block (x, y) ranks
-// its 256 rollouts against the 256 of tile y staged in LDS; off the diagonal tile the index
-// tie-break is block-uniform, so one compare per pair.  rank[] zeroed beforehand.
+// key_i plus equal keys at lower indices.  O(S log S) in two kernels over chunks of 256:
+//   rank_chunk_kernel   chunk-local stable rank by all-pairs compares in LDS; writes rank_i
+//                       (local) and the chunk's keys in sorted order;
+//   rank_merge_kernel   block (a, g) counts, for each key of chunk a, the keys of a group of
+//                       RANK_G other chunks below it (chunks after a: lower_bound) or not above
+//                       it (chunks before a: upper_bound, equal keys at lower indices), by
+//                       binary searches of the sorted chunks staged in LDS; one atomic per key.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t cost_key(double c)
 {
@@ -522,25 +526,71 @@ __device__ __forceinline__ uint64_t cost_key(double c)
     return isnan(c) ? ~0ull : k;
 }
 
-__global__ __launch_bounds__(256) void rank_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
+constexpr int RANK_T = 256;   // chunk size (one block)
+constexpr int RANK_G = 16;    // chunks searched per merge block
+
+__global__ __launch_bounds__(RANK_T) void rank_chunk_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank,
+                                                            uint64_t *__restrict__ sorted)
 {
-    __shared__ uint64_t kj[256];
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t j0 = (int64_t)blockIdx.y * 256;
-    const int64_t jl = j0 + threadIdx.x;
-    kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
+    __shared__ uint64_t kj[RANK_T];
+    const int t = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * RANK_T + t;
+    const uint64_t ki = (i < S) ? cost_key(cost[2 + i]) : ~0ull;
+    kj[t] = ki;
     __syncthreads();
+    // pads (key ~0 at the chunk's end) sort after every real key, NaN included
+    int lr = 0;
+#pragma unroll 8
+    for (int u = 0; u < RANK_T; u++) {
+        const uint64_t k = kj[u];
+        lr += (k < ki || (k == ki && u < t)) ? 1 : 0;
+    }
+    sorted[(int64_t)blockIdx.x * RANK_T + lr] = ki;
+    if (i < S) rank[2 + i] = lr;
+}
+
+__global__ __launch_bounds__(RANK_T) void rank_merge_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank,
+                                                            const uint64_t *__restrict__ sorted)
+{
+    __shared__ uint64_t sk[RANK_G * RANK_T];
+    const int t = threadIdx.x;
+    const int a = blockIdx.x;
+    const int nch = (int)((S + RANK_T - 1) / RANK_T);
+    const int b0 = blockIdx.y * RANK_G;
+    const int nb = (nch - b0) < RANK_G ? (nch - b0) : RANK_G;
+    {   // all RANK_G loads in flight before the LDS stores
+        uint64_t v[RANK_G];
+#pragma unroll
+        for (int g = 0; g < RANK_G; g++) v[g] = (g < nb) ? sorted[(int64_t)(b0 + g) * RANK_T + t] : ~0ull;
+#pragma unroll
+        for (int g = 0; g < RANK_G; g++) sk[g * RANK_T + t] = v[g];
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)a * RANK_T + t;
     if (i >= S) return;
     const uint64_t ki = cost_key(cost[2 + i]);
-    const int jn = (int)((S - j0) < 256 ? (S - j0) : 256);
+    int pos[RANK_G];
+#pragma unroll
+    for (int g = 0; g < RANK_G; g++) pos[g] = 0;
+    // branch-free binary searches, RANK_G independent chains per thread
+#pragma unroll
+    for (int step = RANK_T / 2; step > 0; step >>= 1) {
+#pragma unroll
+        for (int g = 0; g < RANK_G; g++) {
+            const bool before = b0 + g < a;   // chunk b precedes a: equal keys count
+            const uint64_t k = sk[g * RANK_T + pos[g] + step - 1];
+            pos[g] += (k < ki || (before && k == ki)) ? step : 0;
+        }
+    }
     int cnt = 0;
-    if (blockIdx.y < blockIdx.x) {          // every j < i: equal keys count
-        for (int t = 0; t < jn; t++) cnt += (kj[t] <= ki) ? 1 : 0;
-    } else if (blockIdx.y > blockIdx.x) {   // every j > i
-        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki) ? 1 : 0;
-    } else {
-        const int il = threadIdx.x;
-        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki || (kj[t] == ki && t < il)) ? 1 : 0;
+#pragma unroll
+    for (int g = 0; g < RANK_G; g++) {
+        const int b = b0 + g;
+        // the last position (RANK_T - 1) is never probed: add it when every probe passed
+        const uint64_t kl = sk[g * RANK_T + RANK_T - 1];
+        const int p = pos[g] + ((pos[g] == RANK_T - 1 && (kl < ki || (b < a && kl == ki))) ? 1 : 0);
+        const int64_t nb_b = (S - (int64_t)b * RANK_T) < RANK_T ? (S - (int64_t)b * RANK_T) : RANK_T;   // real keys
+        cnt += (g < nb && b != a) ? (p < nb_b ? p : (int)nb_b) : 0;
     }
     if (cnt) atomicAdd(&rank[2 + i], cnt);
 }
@@ -749,18 +799,28 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
-__global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict__ cost, int64_t R, double cost_scale,
-                                                       double *__restrict__ weights, Status *__restrict__ status)
+constexpr int WT = 1024;   // weights_kernel: one workgroup
+constexpr int WU = 8;      // costs in flight per thread and pass
+__global__ __launch_bounds__(WT) void weights_kernel(const double *__restrict__ cost, int64_t R, double cost_scale,
+                                                     double *__restrict__ weights, Status *__restrict__ status)
 {
-    __shared__ double smn[16], smx[16], ssum[16];
+    __shared__ double smn[WT / 64], smx[WT / 64], ssum[WT / 64];
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     double mn = INFINITY, mx = -INFINITY, cnt = 0.0;
-    for (int64_t i = t; i < R; i += 1024) {
-        const double c = cost[i];
-        if (isnan(c)) continue;
-        cnt += 1.0;
-        mn = (c < mn) ? c : mn;
-        mx = (c > mx) ? c : mx;
+    for (int64_t base = 0; base < R; base += WT * WU) {
+        double c[WU];
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const int64_t i = base + (int64_t)u * WT + t;
+            c[u] = (i < R) ? cost[i] : NAN;
+        }
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const bool ok = !isnan(c[u]);
+            cnt += ok ? 1.0 : 0.0;
+            mn = (ok && c[u] < mn) ? c[u] : mn;
+            mx = (ok && c[u] > mx) ? c[u] : mx;
+        }
     }
     mn = wave_min(mn);
     mx = wave_max(mx);
@@ -769,7 +829,7 @@ __global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict_
     __syncthreads();
     double minimum = smn[0], maximum = smx[0], valid = ssum[0];
 #pragma unroll
-    for (int i = 1; i < 16; i++) {
+    for (int i = 1; i < WT / 64; i++) {
         minimum = smin(minimum, smn[i]);
         maximum = smax(maximum, smx[i]);
         valid += ssum[i];
@@ -785,22 +845,40 @@ __global__ __launch_bounds__(1024) void weights_kernel(const double *__restrict_
         return;
     }
     double tot = 0.0;
-    for (int64_t i = t; i < R; i += 1024) {
-        const double c = cost[i];
-        double e = 0.0;
-        if (!isnan(c)) {
-            e = exp(-cost_scale * (c - minimum) / difference);
-            tot += e;
+    for (int64_t base = 0; base < R; base += WT * WU) {
+        double c[WU];
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const int64_t i = base + (int64_t)u * WT + t;
+            c[u] = (i < R) ? cost[i] : NAN;
         }
-        weights[i] = e;
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const int64_t i = base + (int64_t)u * WT + t;
+            const double e = isnan(c[u]) ? 0.0 : exp(-cost_scale * (c[u] - minimum) / difference);
+            tot += e;
+            if (i < R) weights[i] = e;
+        }
     }
     tot = wave_sum(tot);
     if (l == 0) ssum[w] = tot;
     __syncthreads();
     double total = ssum[0];
 #pragma unroll
-    for (int i = 1; i < 16; i++) total += ssum[i];
-    for (int64_t i = t; i < R; i += 1024) weights[i] = weights[i] / total;
+    for (int i = 1; i < WT / 64; i++) total += ssum[i];
+    for (int64_t base = 0; base < R; base += WT * WU) {
+        double e[WU];
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const int64_t i = base + (int64_t)u * WT + t;
+            e[u] = (i < R) ? weights[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < WU; u++) {
+            const int64_t i = base + (int64_t)u * WT + t;
+            if (i < R) weights[i] = e[u] / total;
+        }
+    }
     if (t == 0) { status->all_nan = 0; status->early = 0; status->minimum = minimum; status->maximum = maximum; status->total = total; }
 }
 
@@ -968,11 +1046,14 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 // ---------------------------------------------------------------------------------------------
 namespace mppi_eng {
 
-hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s)
+hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s)
 {
     if (S <= 0) return hipSuccess;
-    const unsigned nb = (unsigned)((S + 255) / 256);
-    hipLaunchKernelGGL(rank_kernel, dim3(nb, nb), dim3(256), 0, s, cost, S, rank);
+    const unsigned nch = (unsigned)((S + RANK_T - 1) / RANK_T);
+    hipLaunchKernelGGL(rank_chunk_kernel, dim3(nch), dim3(RANK_T), 0, s, cost, S, rank, sorted);
+    if (nch > 1)
+        hipLaunchKernelGGL(rank_merge_kernel, dim3(nch, (nch + RANK_G - 1) / RANK_G), dim3(RANK_T), 0, s, cost, S, rank,
+                           (const uint64_t *)sorted);
     return hipGetLastError();
 }
 
@@ -1012,7 +1093,7 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 
 hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s)
 {
-    hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(1024), 0, s, cost, R, cost_scale, weights, status);
+    hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(WT), 0, s, cost, R, cost_scale, weights, status);
     return hipGetLastError();
 }
 

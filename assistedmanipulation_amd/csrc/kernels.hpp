@@ -87,7 +87,9 @@ struct FinishArgs {
     double *out;
 };
 
-hipError_t launch_rank(const double *cost, int64_t S, int *rank, hipStream_t s);
+// stable rank of rollouts 2..S+1 by cost; `sorted` is scratch of rank_scratch(S) keys
+hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s);
+inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);

@@ -99,6 +99,31 @@ def test_nan_rollouts_get_zero_weight():
         assert_update_parity(dev, orc, "after nan %d" % j)
 
 
+@pytest.mark.parametrize("S", [4500, 20000])
+def test_stable_order_at_scale(S):
+    """The chunked rank (chunk sort + binary-search merge, kernels.hip) beyond one merge group
+    (16 chunks of 256): the previous costs hold exact ties (the first update's kept rollouts
+    duplicate rollout 0) and NaNs, so the keep-best set and every resampled rollout's draws
+    (noise tensor, bit-exact) depend on the full stable order including both tie rules."""
+    conf, dev, orc, sd = fr_pair(S=S, horison=0.04, K=20, threads=16)
+    rng = np.random.default_rng(S)
+    x = am.huddled_state()
+    step_both(dev, orc, x, 0.0, rng, sd)
+    n = orc.noise_draws(0.05)
+    eps = rng.standard_normal((n, 12)) * sd
+    for r in (7, 300, S // 2, S - 30):
+        eps[r * 4, 4] = 1e300   # NaN costs at scattered resampled rollouts
+    dev.inject_noise(eps)
+    orc.inject_noise(eps)
+    orc.update(x, 0.05)
+    dev.update(x, 0.05)
+    assert np.isnan(orc.costs()).sum() == 4
+    for j in (2, 3):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert_update_parity(dev, orc, "S=%d upd %d" % (S, j))
+        np.testing.assert_array_equal(dev.noise()[2:], orc.noise()[2:])
+
+
 def test_nan_noise_poisons_gradient_like_the_reference():
     """NaN eps: 0 * NaN = NaN in the gradient sum, so U* becomes NaN on both sides."""
     conf, dev, orc, sd = fr_pair(S=32, horison=0.08, K=4)

@@ -52,6 +52,24 @@ __global__ void bench(double *out, long long *cyc, double seed)
             REP8(asm volatile("v_mov_b64 %0, %2\n v_mov_b64 %1, %3\n" : "=v"(a0), "=v"(a1) : "v"(a2), "v"(a3));)
         } else if (MODE == 10) {   // dependent LDS write -> read round trip
             REP8(asm volatile("ds_write_b64 %1, %0\n s_waitcnt lgkmcnt(0)\n ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)\n" : "+v"(a0) : "v"(addr));)
+        } else if (MODE == 12) {   // independent v_fmac_f64_dpp row_newbcast (8 accumulators)
+            REP8(asm volatile("v_fmac_f64_dpp %0, %4, %5 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+                              "v_fmac_f64_dpp %1, %4, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(b), "v"(c));)
+        } else if (MODE == 13) {   // dependent v_fmac_f64_dpp chain
+            REP8(asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+                              "s_nop 1\n"
+                              "v_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+                              "s_nop 1\n"
+                              : "+v"(a0) : "v"(b), "v"(c));)
+        } else if (MODE == 14) {   // independent v_fmac_f64_dpp, 4 accumulators interleaved
+            REP8(asm volatile("v_fmac_f64_dpp %0, %4, %5 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+                              "v_fmac_f64_dpp %1, %4, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+                              "v_fmac_f64_dpp %2, %4, %5 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+                              "v_fmac_f64_dpp %3, %4, %5 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(b), "v"(c));)
+        } else if (MODE == 15) {   // dependent v_add_f64 chain
+            REP8(asm volatile("v_add_f64 %0, %0, %1\n v_add_f64 %0, %0, %1\n" : "+v"(a0) : "v"(c));)
         } else if (MODE == 11) {   // independent f32 FMA (reference point)
             float f0 = a0, f1 = a1;
             REP8(asm volatile("v_fma_f32 %0, %2, %2, %0\n v_fma_f32 %1, %2, %2, %1\n" : "+v"(f0), "+v"(f1) : "v"((float)c));)
@@ -73,7 +91,7 @@ void run(const char *name, int blocks, double *d_out, long long *d_cyc)
     double m = 0;
     for (int i = 0; i < blocks; i++) m += h[i];
     m /= blocks;
-    printf("%-34s blocks=%5d  cyc/instr = %.2f\n", name, blocks, m / (ITERS * 16.0 * (MODE == 0 ? 2 : 1)));
+    printf("%-34s blocks=%5d  cyc/instr = %.2f\n", name, blocks, m / (ITERS * 16.0 * (MODE == 0 || MODE == 14 ? 2 : 1)));
 }
 
 int main()
@@ -94,6 +112,10 @@ int main()
         run<9>("mov_b64 indep", blocks, d_out, d_cyc);
         run<10>("lds write->read roundtrip", blocks, d_out, d_cyc);
         run<11>("fma_f32 indep", blocks, d_out, d_cyc);
+        run<12>("fmac_f64_dpp indep (2 acc)", blocks, d_out, d_cyc);
+        run<13>("fmac_f64_dpp dependent (+nop1)", blocks, d_out, d_cyc);
+        run<14>("fmac_f64_dpp indep (4 acc)", blocks, d_out, d_cyc);
+        run<15>("add_f64 dependent", blocks, d_out, d_cyc);
     }
     return 0;
 }
