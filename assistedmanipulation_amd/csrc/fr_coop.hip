@@ -193,6 +193,73 @@ __device__ __forceinline__ double bsum<0, 12>(double x, double one)
         : "v"(x), "v"(one));
     return acc;
 }
+// Interleaved chains.  A v_fmac_f64_dpp that accumulates into the result of the previous one waits
+// ~14 cycles (no forwarding through a DPP instruction), while independent ones issue every ~5
+// (tools/ubench.hip), so every block below round-robins several independent accumulators.
+#define DPPF(acc, x, y, lane) "v_fmac_f64_dpp " acc ", " x ", " y " row_newbcast:" #lane " row_mask:0xf bank_mask:0xf\n\t"
+
+// D = sum_{r<6} U[lane r] S[r] and sp = sum_{r<6} P[lane r] S[r]: two chains, interleaved (a
+// four-chain split measured no faster: the extra zero-inits and adds cost what the shorter chains
+// save).
+__device__ __forceinline__ void bfma6_pair(double U, double P, const double *S, double &D, double &sp)
+{
+    double d0 = 0.0, p0 = 0.0;
+    asm("s_nop 1\n\t"
+        DPPF("%0", "%2", "%4", 0) DPPF("%1", "%3", "%4", 0) DPPF("%0", "%2", "%5", 1) DPPF("%1", "%3", "%5", 1)
+        DPPF("%0", "%2", "%6", 2) DPPF("%1", "%3", "%6", 2) DPPF("%0", "%2", "%7", 3) DPPF("%1", "%3", "%7", 3)
+        DPPF("%0", "%2", "%8", 4) DPPF("%1", "%3", "%8", 4) DPPF("%0", "%2", "%9", 5) DPPF("%1", "%3", "%9", 5)
+        : "+&v"(d0), "+&v"(p0)
+        : "v"(U), "v"(P), "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]));
+    D = d0;
+    sp = p0;
+}
+// sum over lanes 0..5 of x: two chains (lanes 0..2, 3..5)
+__device__ __forceinline__ double bsum6_split(double x, double one)
+{
+    double a0 = 0.0, a1 = 0.0;
+    asm("s_nop 1\n\t"
+        DPPF("%0", "%2", "%3", 0) DPPF("%1", "%2", "%3", 3)
+        DPPF("%0", "%2", "%3", 1) DPPF("%1", "%2", "%3", 4)
+        DPPF("%0", "%2", "%3", 2) DPPF("%1", "%2", "%3", 5)
+        : "+&v"(a0), "+&v"(a1)
+        : "v"(x), "v"(one));
+    return a0 + a1;
+}
+// two sums over lanes 0..11, each split in two chains (lanes 0..5, 6..11): four chains
+__device__ __forceinline__ void bsum12_pair(double x, double y, double one, double &sx, double &sy)
+{
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    asm("s_nop 1\n\t"
+        DPPF("%0", "%4", "%6", 0) DPPF("%2", "%5", "%6", 0) DPPF("%1", "%4", "%6", 6) DPPF("%3", "%5", "%6", 6)
+        DPPF("%0", "%4", "%6", 1) DPPF("%2", "%5", "%6", 1) DPPF("%1", "%4", "%6", 7) DPPF("%3", "%5", "%6", 7)
+        DPPF("%0", "%4", "%6", 2) DPPF("%2", "%5", "%6", 2) DPPF("%1", "%4", "%6", 8) DPPF("%3", "%5", "%6", 8)
+        DPPF("%0", "%4", "%6", 3) DPPF("%2", "%5", "%6", 3) DPPF("%1", "%4", "%6", 9) DPPF("%3", "%5", "%6", 9)
+        DPPF("%0", "%4", "%6", 4) DPPF("%2", "%5", "%6", 4) DPPF("%1", "%4", "%6", 10) DPPF("%3", "%5", "%6", 10)
+        DPPF("%0", "%4", "%6", 5) DPPF("%2", "%5", "%6", 5) DPPF("%1", "%4", "%6", 11) DPPF("%3", "%5", "%6", 11)
+        : "+&v"(a0), "+&v"(a1), "+&v"(b0), "+&v"(b1)
+        : "v"(x), "v"(y), "v"(one));
+    sx = a0 + a1;
+    sy = b0 + b1;
+}
+// The EE frame velocity J v (three sums over lanes 0..9) and J_a J_a^T (six sums over lanes 3..9):
+// nine chains round-robin.
+__device__ __forceinline__ void kin_sums(const double *v, const double *m, double one, double *vl, double *jj)
+{
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0, b4 = 0.0, b5 = 0.0;
+#define KV(l) DPPF("%0", "%9", "%18", l) DPPF("%1", "%10", "%18", l) DPPF("%2", "%11", "%18", l)
+#define KJ(l) DPPF("%3", "%12", "%18", l) DPPF("%4", "%13", "%18", l) DPPF("%5", "%14", "%18", l) \
+              DPPF("%6", "%15", "%18", l) DPPF("%7", "%16", "%18", l) DPPF("%8", "%17", "%18", l)
+    asm("s_nop 1\n\t"
+        KV(0) KV(1) KV(2) KV(3) KJ(3) KV(4) KJ(4) KV(5) KJ(5) KV(6) KJ(6) KV(7) KJ(7) KV(8) KJ(8) KV(9) KJ(9)
+        : "+&v"(a0), "+&v"(a1), "+&v"(a2), "+&v"(b0), "+&v"(b1), "+&v"(b2), "+&v"(b3), "+&v"(b4), "+&v"(b5)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(m[5]), "v"(one));
+#undef KV
+#undef KJ
+    vl[0] = a0; vl[1] = a1; vl[2] = a2;
+    jj[0] = b0; jj[1] = b1; jj[2] = b2; jj[3] = b3; jj[4] = b4; jj[5] = b5;
+}
+static_assert(FR_EE_PARENT == 9 && FR_ARM0 == 3 && FR_ARM1 == 10, "kin_sums lane ranges");
+
 // 1/d by v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; d finite, normal)
 __device__ __forceinline__ double frcp(double d)
 {
@@ -454,15 +521,11 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
     // frame velocity J v over the EE chain (bodies 0..9), J_a J_a^T over the arm (bodies 3..9)
     double vl[3], jj[6];
-    const double one = 1.0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) vl[k] = bsum<0, FR_EE_PARENT + 1>(S[k] * qd, one);
-    jj[0] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[0], one);
-    jj[1] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[1], one);
-    jj[2] = bsum<FR_ARM0, FR_ARM1>(S[0] * S[2], one);
-    jj[3] = bsum<FR_ARM0, FR_ARM1>(S[1] * S[1], one);
-    jj[4] = bsum<FR_ARM0, FR_ARM1>(S[1] * S[2], one);
-    jj[5] = bsum<FR_ARM0, FR_ARM1>(S[2] * S[2], one);
+    {
+        const double v3[3] = {S[0] * qd, S[1] * qd, S[2] * qd};
+        const double m6[6] = {S[0] * S[0], S[0] * S[1], S[0] * S[2], S[1] * S[1], S[1] * S[2], S[2] * S[2]};
+        kin_sums(v3, m6, 1.0, vl, jj);
+    }
     kin.traj = trajectory_term(Cs, sc_next, vl);
     kin.manip = manipulability_term(Cs, jj);
 }
@@ -507,8 +570,8 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         const double pAr = (i >= 10) ? 0.0 : pA;
         const double U = ((A[0] * S[0] + A[1] * S[1]) + (A[2] * S[2] + A[3] * S[3])) + (A[4] * S[4] + A[5] * S[5]);
         // D = S.U and S.pA: rows 0..5 broadcast from lanes 0..5, every lane holds S
-        const double D = bfma6(U, S, 0.0);
-        const double sp = bfma6(pAr, S, 0.0);
+        double D, sp;
+        bfma6_pair(U, pAr, S, D, sp);
         const double Dinv = frcp(D);
         const double u = tau - sp;
         Lw[L_U + i * ROW + j] = U;
@@ -545,7 +608,7 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
             if constexpr (EN) Ff = Lk[L_F + (i + 1) * 6 + r];
         }
         const double ap = (i == 11) ? a9 : acc;
-        const double ua = bsum<0, 6>(Ui * ap, 1.0);
+        const double ua = bsum6_split(Ui * ap, 1.0);
         const double dd = Dv * (ui - ua);
         acc = ap + Sr * dd;
         if (i == 9) a9 = acc;
@@ -567,8 +630,8 @@ __device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, co
     const double lane_joint = jl ? left_barrier(lo_b, q) + right_barrier(up_b, q) : 0.0;
     const double vq = fabs(qd);
     const double one = 1.0;
-    const double joint = bsum<0, FR_NB>(lane_joint, one);
-    const double vel = bsum<0, FR_NB>(vel_w * (vq * vq), one);
+    double joint, vel;
+    bsum12_pair(lane_joint, vel_w * (vq * vq), one, joint, vel);
     const double s = bcast<2>(sq), c = bcast<2>(cq);
     double wc = 0.0;
     {
@@ -727,7 +790,11 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
+#ifdef ABL_NOCOST
+        const double step_cost = 0.0;
+#else
         const double step_cost = a.steps[k].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
+#endif
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
         {
@@ -738,9 +805,15 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             qd = (j == 0) ? vx : ((j == 1) ? vy : ((j == 2) ? u : qd));
         }
         Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
+#ifndef ABL_NOFK
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin, grav);
-        double pe;
+#endif
+        double pe = 0.0;
+#ifdef ABL_NOABA
+        const double qdd = Lw[L_TAU + j] * 1e-3;
+#else
         const double qdd = coop_aba<EN>(j, Lk, Lw, pe);
+#endif
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
         if constexpr (EN) {   // power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
