@@ -11,8 +11,9 @@ from ._lib import load as _load
 
 _load()   # fail loudly at import if the engine library is missing
 
-from .config import (Configuration, Smoothing, constant_forecast,  # noqa: E402
-                     frankaridgeback_configuration, huddled_state, point_mass_configuration)
+from .config import (Configuration, Smoothing, average_forecast_configuration, constant_forecast,  # noqa: E402
+                     frankaridgeback_configuration, huddled_state, kalman_forecast_configuration,
+                     locf_forecast_configuration, point_mass_configuration)
 from .trajectory import (AssistedManipulation, Cost, Dynamics, EngineError, TrackPoint,  # noqa: E402
                          FrankaRidgebackDynamics, PointMassDynamics, QuadraticCost, Trajectory,
                          comm_unique_id, shard_range)
@@ -22,7 +23,8 @@ from .csvlog import MPPILogger  # noqa: E402
 __all__ = [
     "MPPILogger",
     "abi", "Configuration", "Smoothing", "constant_forecast", "frankaridgeback_configuration",
-    "huddled_state", "point_mass_configuration", "AssistedManipulation", "TrackPoint", "Cost", "Dynamics",
+    "huddled_state", "point_mass_configuration", "locf_forecast_configuration", "average_forecast_configuration",
+    "kalman_forecast_configuration", "AssistedManipulation", "TrackPoint", "Cost", "Dynamics",
     "EngineError", "FrankaRidgebackDynamics", "PointMassDynamics", "QuadraticCost", "Trajectory",
     "comm_unique_id", "shard_range",
 ]

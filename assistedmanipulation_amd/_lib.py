@@ -37,6 +37,11 @@ PROTOTYPES = {
     "mppi_noise_draws": (C.c_int, [_h, C.c_double, _i64p]),
     "mppi_set_index_semantics": (C.c_int, [_h, C.c_int]),
     "mppi_set_forecast": (C.c_int, [_h, _dp]),
+    "mppi_forecast_attach": (C.c_int, [_h, C.POINTER(abi.mppi_forecast_config)]),
+    "mppi_forecast_observe": (C.c_int, [_h, _dp, C.c_double]),
+    "mppi_forecast_observe_time": (C.c_int, [_h, C.c_double]),
+    "mppi_forecast_get": (C.c_int, [_h, C.c_double, _dp]),
+    "mppi_step_constants": (C.c_int, [_h, _dp]),
     "mppi_update": (C.c_int, [_h, _dp, C.c_double]),
     "mppi_update_phase1": (C.c_int, [_h, _dp, C.c_double]),
     "mppi_update_phase2": (C.c_int, [_h]),

@@ -179,3 +179,25 @@ class mppi_cost_desc(C.Structure):
 def dptr(arr):
     """ctypes double* into a contiguous float64 numpy array (keeps no reference!)."""
     return arr.ctypes.data_as(_dp)
+
+
+MPPI_FORECAST_LOCF = 0
+MPPI_FORECAST_AVERAGE = 1
+MPPI_FORECAST_KALMAN = 2
+MPPI_FORECAST_MAX_ORDER = 3
+
+
+class mppi_forecast_config(C.Structure):
+    """Forecast::Configuration (controller/forecast.hpp:377-416) -> include/mppi_amd.h."""
+    _fields_ = [
+        ("type", C.c_int32),
+        ("locf_observation", C.c_double * 6),
+        ("locf_horison", C.c_double),
+        ("average_states", C.c_int32),
+        ("average_window", C.c_double),
+        ("kalman_observed_states", C.c_int32),
+        ("kalman_time_step", C.c_double),
+        ("kalman_horison", C.c_double),
+        ("kalman_order", C.c_int32),
+        ("kalman_initial_state", C.c_double * 6),
+    ]

@@ -153,3 +153,33 @@ def constant_forecast(H, force=(20.0, 0.0, 0.0)):
     t = np.zeros((H, 6))
     t[:, :3] = force
     return t
+
+
+def locf_forecast_configuration(observation=(0.0,) * 6, horison=0.0):
+    """LOCFForecast::Configuration (forecast.hpp:66-76)."""
+    c = abi.mppi_forecast_config()
+    c.type = abi.MPPI_FORECAST_LOCF
+    c.locf_observation[:] = list(observation)
+    c.locf_horison = horison
+    return c
+
+
+def average_forecast_configuration(window, states=6):
+    """AverageForecast::Configuration (forecast.hpp:151-161)."""
+    c = abi.mppi_forecast_config()
+    c.type = abi.MPPI_FORECAST_AVERAGE
+    c.average_states = states
+    c.average_window = window
+    return c
+
+
+def kalman_forecast_configuration(time_step, horison, order, initial_state=(0.0,) * 6, observed_states=6):
+    """KalmanForecast::Configuration (forecast.hpp:227-249)."""
+    c = abi.mppi_forecast_config()
+    c.type = abi.MPPI_FORECAST_KALMAN
+    c.kalman_observed_states = observed_states
+    c.kalman_time_step = time_step
+    c.kalman_horison = horison
+    c.kalman_order = order
+    c.kalman_initial_state[:] = list(initial_state)
+    return c

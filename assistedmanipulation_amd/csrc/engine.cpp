@@ -13,6 +13,7 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -78,7 +79,21 @@ struct mppi_handle {
     std::vector<double> U_host;
     double opt_cost = 0;
     // forecast / per-step constants
-    std::vector<double> forecast;   // H x 6
+    std::vector<double> forecast;   // H x 6 caller table (mppi_set_forecast)
+    struct DeviceForecast {         // mppi_forecast_attach (forecast.hip)
+        int type = FC_NONE;
+        double horison = 0, valid_until = 0, value[6] = {0, 0, 0, 0, 0, 0};   // LOCF / Average mean
+        double window = 0, last = 0;                                          // Average
+        std::vector<std::pair<double, std::array<double, 6>>> buffer;
+        int order = 0, n = 0, steps = 0;                                      // Kalman
+        double time_step = 0, last_update = 0;
+        int64_t pending = 0;
+        DevKalman *d_kf = nullptr;
+        double *d_pred = nullptr;
+    } fc;
+    double *d_gamma = nullptr;      // [H] pow(gamma, k) (host std::pow)
+    double *d_fc_out = nullptr;     // [6] forecast_eval result
+    StepConst *d_steps_buf[2] = {nullptr, nullptr};   // per-update constants, alternate updates
     mppi_assisted_manipulation_desc am{};
     mppi_quadratic_cost_desc quad{};
     double pm_mass = 1.0;
@@ -264,7 +279,8 @@ mppi_status upload_steps(mppi_handle *h)
 {
     std::vector<StepConst> steps;
     build_steps(h, steps);
-    HIP_TRY(hipMemcpyAsync(h->d_steps, steps.data(), steps.size() * sizeof(StepConst), hipMemcpyHostToDevice, h->stream));
+    for (StepConst *d : h->d_steps_buf)
+        HIP_TRY(hipMemcpyAsync(d, steps.data(), steps.size() * sizeof(StepConst), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return MPPI_OK;
 }
@@ -292,7 +308,8 @@ mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
     return MPPI_OK;
 }
 
-void dfree(mppi_handle *h, double *&p)
+template <class T>
+void dfree(mppi_handle *h, T *&p)
 {
     if (!p) return;
     (void)hipFree(p);
@@ -468,7 +485,16 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_rank_keys, (size_t)rank_scratch(h->S)));
     CREATE_TRY(dalloc(h, &h->d_status, 1));
-    CREATE_TRY(dalloc(h, &h->d_steps, (size_t)h->H));
+    CREATE_TRY(dalloc(h, &h->d_steps_buf[0], (size_t)h->H));
+    CREATE_TRY(dalloc(h, &h->d_steps_buf[1], (size_t)h->H));
+    h->d_steps = h->d_steps_buf[0];
+    CREATE_TRY(dalloc(h, &h->d_gamma, (size_t)h->H));
+    CREATE_TRY(dalloc(h, &h->d_fc_out, 6));
+    {
+        std::vector<double> g((size_t)h->H);
+        for (int64_t k = 0; k < h->H; k++) g[(size_t)k] = std::pow(h->gamma, (double)k);
+        CREATE_TRY(hipMemcpy(h->d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocDefault));
     CREATE_TRY(hipHostMalloc((void **)&h->h_stage, 64 * sizeof(double), hipHostMallocDefault));
     CREATE_TRY(hipHostMalloc((void **)&h->h_opt, 8 * sizeof(double), hipHostMallocDefault));
@@ -716,9 +742,191 @@ mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6)
     if (!h) return MPPI_ERR_INVALID;
     if (wrench_Hx6) h->forecast.assign(wrench_Hx6, wrench_Hx6 + 6 * h->H);
     else h->forecast.clear();
+    h->fc.type = FC_NONE;   // a table replaces an attached forecast
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipStreamSynchronize(h->stream_opt));   // the pending optimal rollout reads d_steps
     return upload_steps(h);
+}
+
+namespace {
+
+ForecastArgs forecast_args(const mppi_handle *h)
+{
+    ForecastArgs f{};
+    f.type = h->fc.type;
+    f.steps = h->fc.steps;
+    for (int k = 0; k < 6; k++) f.value[k] = h->fc.value[k];
+    f.valid_until = h->fc.valid_until;
+    f.last_update = h->fc.last_update;
+    f.horison = h->fc.horison;
+    f.time_step = h->fc.time_step;
+    f.pred = h->fc.d_pred;
+    return f;
+}
+
+StepParams step_params(const mppi_handle *h)
+{
+    const mppi_assisted_manipulation_desc &a = h->am;
+    StepParams p{};
+    p.assisted_manipulation = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION;
+    p.has_forecast = a.has_forecast;
+    p.target_scale = a.trajectory_target_scale;
+    p.target_maximum = a.trajectory_target_maximum;
+    p.position_threshold = a.trajectory_position_threshold;
+    p.pos_c = a.trajectory_position_cost.constant_cost;
+    p.pos_l = a.trajectory_position_cost.linear_cost;
+    p.pos_q = a.trajectory_position_cost.quadratic_cost;
+    p.vel_dropoff = a.trajectory_velocity_dropoff;
+    p.vel_minimum = a.trajectory_velocity_minimum;
+    p.vel_maximum = a.trajectory_velocity_maximum;
+    return p;
+}
+
+unsigned fc_factorial(unsigned k) { return k <= 1 ? 1 : k * fc_factorial(k - 1); }
+
+// AverageForecast::clear_old_measurements + update_average (forecast.cpp:67-101)
+void average_refresh(mppi_handle::DeviceForecast &f, double time)
+{
+    size_t it = 0;
+    while (it < f.buffer.size() && !(time - f.window < f.buffer[it].first)) it++;
+    f.buffer.erase(f.buffer.begin(), f.buffer.begin() + (long)it);
+    if (f.buffer.empty()) {
+        for (double &v : f.value) v = 0.0;
+        return;
+    }
+    std::array<double, 6> total = f.buffer[0].second;
+    for (size_t i = 1; i < f.buffer.size(); i++)
+        for (int k = 0; k < 6; k++) total[(size_t)k] += f.buffer[i].second[(size_t)k];
+    for (int k = 0; k < 6; k++) f.value[k] = total[(size_t)k] / (double)f.buffer.size();
+}
+
+}  // namespace
+
+mppi_status mppi_forecast_attach(mppi_handle *h, const mppi_forecast_config *c)
+{
+    if (!h) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    mppi_handle::DeviceForecast &f = h->fc;
+    if (!c) {   // detach: back to the caller's table
+        f.type = FC_NONE;
+        return upload_steps(h);
+    }
+    // Forecast::create (forecast.cpp:6-39) and the kind's create()
+    if (c->type != MPPI_FORECAST_LOCF && c->type != MPPI_FORECAST_AVERAGE && c->type != MPPI_FORECAST_KALMAN)
+        return fail(h, MPPI_ERR_INVALID, "unknown forecast type " + std::to_string(c->type) + "selected");
+    dfree(h, f.d_kf);
+    dfree(h, f.d_pred);
+    if (c->type == MPPI_FORECAST_LOCF) {
+        f = mppi_handle::DeviceForecast{};
+        for (int k = 0; k < 6; k++) f.value[k] = c->locf_observation[k];
+        f.horison = c->locf_horison;
+        f.valid_until = 0.0;
+    } else if (c->type == MPPI_FORECAST_AVERAGE) {
+        if (c->average_window < 0.0) return fail(h, MPPI_ERR_INVALID, "prediction window time is negative");
+        if (c->average_states != 6) return fail(h, MPPI_ERR_UNSUPPORTED, "the end-effector wrench forecast has 6 states");
+        f = mppi_handle::DeviceForecast{};
+        f.window = c->average_window;
+    } else if (c->type == MPPI_FORECAST_KALMAN) {
+        if (c->kalman_observed_states != 6)
+            return fail(h, MPPI_ERR_UNSUPPORTED, "KalmanForecast::update works on the 6-state wrench (forecast.cpp:303)");
+        if (c->kalman_order < 0 || c->kalman_order > MPPI_FORECAST_MAX_ORDER)
+            return fail(h, MPPI_ERR_UNSUPPORTED, "kalman order must be in [0, " + std::to_string(MPPI_FORECAST_MAX_ORDER) + "]");
+        if (!(c->kalman_time_step > 0) || !(c->kalman_horison >= 0))
+            return fail(h, MPPI_ERR_INVALID, "kalman time_step must be positive and horison non-negative");
+        f = mppi_handle::DeviceForecast{};
+        f.order = c->kalman_order;
+        f.n = 6 * (f.order + 1);
+        f.time_step = c->kalman_time_step;
+        f.horison = c->kalman_horison;
+        f.steps = (int)std::ceil(c->kalman_horison / c->kalman_time_step);
+        f.last_update = -c->kalman_time_step;
+        DevKalman k{};
+        const int n = f.n;
+        for (int d = 0; d <= f.order; d++)   // create_euler_state_transition_matrix (forecast.cpp:238-285)
+            for (int st = 0; st < 6; st++)
+                for (int i = 0; i <= f.order - d; i++)
+                    k.F[(d * 6 + st) * KMAX + d * 6 + i * 6 + st] = 1.0 / (double)fc_factorial((unsigned)i) * std::pow(f.time_step, (double)i);
+        for (int i = 0; i < n; i++) k.P[i * KMAX + i] = 1e-8;   // initial_covariance
+        for (int i = 0; i < 6; i++) k.x[i] = c->kalman_initial_state[i];
+        for (int i = 0; i < n; i++) {   // m_next_state = F x0
+            double acc = 0.0;
+            for (int j = 0; j < n; j++) acc += k.F[i * KMAX + j] * k.x[j];
+            k.xn[i] = acc;
+        }
+        HIP_TRY(dalloc(h, &f.d_kf, 1));
+        HIP_TRY(dalloc(h, &f.d_pred, (size_t)(f.steps + 1) * 6));   // zeros: uninitialised in the reference
+        HIP_TRY(hipMemcpy(f.d_kf, &k, sizeof(k), hipMemcpyHostToDevice));
+    }
+    f.type = c->type;
+    return MPPI_OK;
+}
+
+mppi_status mppi_forecast_observe(mppi_handle *h, const double *m, double time)
+{
+    if (!h || !m || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
+    mppi_handle::DeviceForecast &f = h->fc;
+    if (f.type == FC_LOCF) {   // forecast.hpp:96-100
+        f.valid_until = time + f.horison;
+        for (int k = 0; k < 6; k++) f.value[k] = m[k];
+    } else if (f.type == FC_AVERAGE) {   // forecast.cpp:109-122
+        if (time < f.last) return MPPI_OK;
+        f.last = time;
+        f.buffer.emplace_back(time, std::array<double, 6>{m[0], m[1], m[2], m[3], m[4], m[5]});
+        average_refresh(f, time);
+    } else {   // KalmanForecast::update (forecast.cpp:298-331) on the engine stream
+        HIP_TRY(hipSetDevice(h->device));
+        KalmanObserve a{};
+        a.n = f.n;
+        a.order = f.order;
+        a.steps = f.steps;
+        a.pending = f.pending;
+        a.dt = time - f.last_update;
+        for (int k = 0; k < 6; k++) a.m[k] = m[k];
+        HIP_TRY(launch_kalman_observe(f.d_kf, f.d_pred, a, h->stream));
+        f.pending = 0;
+        f.last_update = time;
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_forecast_observe_time(mppi_handle *h, double time)
+{
+    if (!h || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
+    mppi_handle::DeviceForecast &f = h->fc;
+    if (f.type == FC_AVERAGE) {
+        average_refresh(f, time);   // forecast.cpp:102-107
+    } else if (f.type == FC_KALMAN) {
+        // forecast.cpp:333-340: filter predict(); it changes only the filter state, which the next
+        // observation reads, so the predictions are applied at the start of that observation
+        if (time > f.last_update) f.pending++;
+    }
+    return MPPI_OK;
+}
+
+mppi_status mppi_forecast_get(mppi_handle *h, double time, double *out)
+{
+    if (!h || !out || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(launch_forecast_eval(forecast_args(h), time, h->d_fc_out, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, h->d_fc_out, 6 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_step_constants(mppi_handle *h, double *out)
+{
+    if (!h || !out) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    std::vector<StepConst> st((size_t)h->H);
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(st.data(), h->d_steps, st.size() * sizeof(StepConst), hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < st.size(); k++) {
+        double *o = out + 8 * k;
+        o[0] = st[k].target[0]; o[1] = st[k].target[1]; o[2] = st[k].target[2];
+        o[3] = st[k].tt; o[4] = st[k].pos_cost; o[5] = st[k].vtarget; o[6] = st[k].gamma_k; o[7] = st[k].active;
+    }
+    return MPPI_OK;
 }
 
 void *mppi_device_costs(mppi_handle *h) { return h ? (void *)h->d_costs : nullptr; }
@@ -736,6 +944,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     std::memcpy(h->h_stage, state, (size_t)h->X * sizeof(double));
     HIP_TRY(hipEventRecord(h->ev[0], h->stream));
     HIP_TRY(hipMemcpyAsync(h->d_x0, h->h_stage, (size_t)h->X * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (h->fc.type != FC_NONE) {   // this update's forecast samples, t0 + k dt (mppi.cpp:326)
+        h->d_steps = h->d_steps_buf[(h->update_count + 1) & 1];   // the previous filter() reads the other
+        HIP_TRY(launch_forecast_steps(forecast_args(h), step_params(h), h->d_gamma, (int)h->H, time, h->dt, h->d_steps, h->stream));
+    }
 
     // sample(): shift count by truncation (mppi.cpp:194-201)
     h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);

@@ -88,6 +88,48 @@ struct FinishArgs {
 };
 
 // stable rank of rollouts 2..S+1 by cost; `sorted` is scratch of rank_scratch(S) keys
+// ---- wrench forecast on the device (forecast.hip) --------------------------------------------
+constexpr int FC_NONE = -1, FC_LOCF = 0, FC_AVERAGE = 1, FC_KALMAN = 2;   // mppi_forecast_type
+constexpr int KMAX = 24;   // Kalman states 6 (order + 1), order <= 3
+
+// Forecast::forecast(t) inputs: LOCF observation / Average mean (value), LOCF validity, Kalman
+// interpolation grid and its prediction table [steps + 1][6] in device memory.
+struct ForecastArgs {
+    int type;
+    int steps;
+    double value[6];
+    double valid_until;
+    double last_update, horison, time_step;
+    const double *pred;
+};
+
+// trajectory_cost's configuration (assisted_manipulation.hpp) for the per-step constants
+struct StepParams {
+    int assisted_manipulation;
+    int has_forecast;
+    double target_scale, target_maximum, position_threshold;
+    double pos_c, pos_l, pos_q;
+    double vel_dropoff, vel_minimum, vel_maximum;
+};
+
+// KalmanFilter state (kalman.hpp) of the forecast's filter, row-major KMAX x KMAX
+struct DevKalman {
+    double F[KMAX * KMAX], P[KMAX * KMAX];
+    double x[KMAX], xn[KMAX], meas[KMAX];
+};
+
+struct KalmanObserve {
+    int n, order, steps;
+    int64_t pending;   // update(time) calls since the last observation
+    double dt;         // time - m_last_update
+    double m[6];
+};
+
+hipError_t launch_forecast_steps(const ForecastArgs &f, const StepParams &p, const double *gamma, int H, double t0, double dt,
+                                 StepConst *out, hipStream_t s);
+hipError_t launch_kalman_observe(DevKalman *kf, double *pred, const KalmanObserve &a, hipStream_t s);
+hipError_t launch_forecast_eval(const ForecastArgs &f, double time, double *out, hipStream_t s);
+
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s);
 inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);

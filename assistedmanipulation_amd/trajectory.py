@@ -248,6 +248,34 @@ class Trajectory:
         assert t.shape == (self.H, 6), t.shape
         self._check(self._L.mppi_set_forecast(self._h, _p(t)))
 
+    # -- device wrench forecast -------------------------------------------
+    def attach_forecast(self, configuration):
+        """Forecast::create bound to the engine (forecast.cpp:6-39): every update then samples
+        forecast(t0 + k dt) on the device.  None detaches (back to set_forecast tables)."""
+        self._check(self._L.mppi_forecast_attach(self._h, None if configuration is None else C.byref(configuration)))
+
+    def observe_wrench(self, wrench, time):
+        """DynamicsForecast::observe_wrench (dynamics.hpp:221-224)."""
+        w = np.ascontiguousarray(wrench, dtype=np.float64)
+        assert w.size == 6
+        self._check(self._L.mppi_forecast_observe(self._h, _p(w), float(time)))
+
+    def observe_time(self, time):
+        """DynamicsForecast::observe_time (dynamics.hpp:231-234)."""
+        self._check(self._L.mppi_forecast_observe_time(self._h, float(time)))
+
+    def forecast(self, time):
+        """Forecast::forecast(time): the wrench the rollout's cost sees at `time`."""
+        out = np.zeros(6)
+        self._check(self._L.mppi_forecast_get(self._h, float(time), _p(out)))
+        return out
+
+    def step_constants(self):
+        """Parity hook: [H x 8] per-step trajectory-cost constants of the last update."""
+        out = np.zeros((self.H, 8))
+        self._check(self._L.mppi_step_constants(self._h, _p(out)))
+        return out
+
     # -- the hot path ------------------------------------------------------------------------
     def update(self, state, time):
         """Trajectory::update (mppi.cpp:154-187)."""

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPPI_AMD_ABI_VERSION 2
+#define MPPI_AMD_ABI_VERSION 3
 
 #define MPPI_MAX_BODIES 16
 #define MPPI_MAX_CONTROL 16
@@ -269,6 +269,55 @@ mppi_status mppi_set_index_semantics(mppi_handle *h, int semantics);
 /* Per-update forecast table: row k = predicted end-effector wrench (fx fy fz tx ty tz) at
  * t0 + k*dt, k < H (KalmanForecast::forecast, forecast.cpp:342-367, sampled on the step grid). */
 mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6);
+
+/* Device-resident wrench forecast.  Replaces the caller's table: every
+ * update samples Forecast::forecast(t0 + k*dt) for k < H on the device (the rollout queries it
+ * through DynamicsForecast::get_end_effector_wrench, dynamics.hpp:275-278, in
+ * AssistedManipulation::trajectory_cost, assisted_manipulation.cpp:237-290).  The three kinds of
+ * Forecast::Configuration (forecast.hpp:377-416):
+ *   LOCFForecast     (forecast.hpp:64-140)   the last observation, zero past its horison;
+ *   AverageForecast  (forecast.cpp:41-129)   mean of the observations inside the window;
+ *   KalmanForecast   (forecast.cpp:131-367, kalman.cpp:103-152)  Euler state-transition Kalman
+ *                    filter over the wrench and its derivatives; each observation runs the filter
+ *                    update and the horison of predictions in one device kernel. */
+typedef enum mppi_forecast_type {
+    MPPI_FORECAST_LOCF = 0,
+    MPPI_FORECAST_AVERAGE = 1,
+    MPPI_FORECAST_KALMAN = 2
+} mppi_forecast_type;
+
+#define MPPI_FORECAST_MAX_ORDER 3   /* Kalman states 6 (order + 1) <= 24 */
+
+typedef struct mppi_forecast_config {
+    int32_t type;                         /* mppi_forecast_type */
+    /* LOCFForecast::Configuration */
+    double locf_observation[6];
+    double locf_horison;
+    /* AverageForecast::Configuration */
+    int32_t average_states;               /* 6: the end-effector wrench */
+    double average_window;
+    /* KalmanForecast::Configuration */
+    int32_t kalman_observed_states;       /* 6: KalmanForecast::update works on Vector6d */
+    double kalman_time_step;
+    double kalman_horison;
+    int32_t kalman_order;                 /* <= MPPI_FORECAST_MAX_ORDER */
+    double kalman_initial_state[6];
+    /* `variance` is read by create_euler_state_transition_covariance_matrix, which ignores
+     * it (forecast.cpp:287-296: 1e-8 I), so it is not carried. */
+} mppi_forecast_config;
+
+/* Forecast::create (forecast.cpp:6-39) bound to the handle; failures return MPPI_ERR_INVALID
+ * with the reference's message.  NULL detaches (back to mppi_set_forecast tables). */
+mppi_status mppi_forecast_attach(mppi_handle *h, const mppi_forecast_config *config);
+/* DynamicsForecast::observe_wrench -> Forecast::update(measurement, time). */
+mppi_status mppi_forecast_observe(mppi_handle *h, const double *wrench6, double time);
+/* DynamicsForecast::observe_time -> Forecast::update(time). */
+mppi_status mppi_forecast_observe_time(mppi_handle *h, double time);
+/* Forecast::forecast(time) (host copy of the device evaluation). */
+mppi_status mppi_forecast_get(mppi_handle *h, double time, double *wrench6);
+/* Parity hook: the per-step trajectory-cost constants the last update's rollouts read, H rows of
+ * (target x y z, target.target, position cost, velocity target, gamma^k, active). */
+mppi_status mppi_step_constants(mppi_handle *h, double *out_Hx8);
 
 /* Trajectory::update (mppi.hpp:339, mppi.cpp:154-187): sample, rollout, optimise, filter,
  * publish.  Blocks until the update is complete on the device. */

@@ -211,6 +211,12 @@ public:
     template <class Vec>
     void set_forecast(const Vec &wrench_Hx6) { check(mppi_set_forecast(m_h, wrench_Hx6.data())); }
     void set_noise_source(int source, uint64_t seed = 0x5EED) { check(mppi_set_noise_source(m_h, source, seed)); }
+    // The wrench forecast on the device (DynamicsForecast::observe_wrench / observe_time and
+    // Forecast::forecast, dynamics.hpp:221-278): every update samples it at t0 + k dt.
+    void attach_forecast(const mppi_forecast_config *configuration) { check(mppi_forecast_attach(m_h, configuration)); }
+    void observe_wrench(const double *wrench6, double time) { check(mppi_forecast_observe(m_h, wrench6, time)); }
+    void observe_time(double time) { check(mppi_forecast_observe_time(m_h, time)); }
+    void forecast(double time, double *wrench6) { check(mppi_forecast_get(m_h, time, wrench6)); }
     mppi_handle *handle() const { return m_h; }
 
 private:

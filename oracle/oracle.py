@@ -73,6 +73,12 @@ def lib(path=None):
     L.oracle_sg_weights.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp]
     L.oracle_default_frankaridgeback.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc)]
     L.oracle_default_assisted_manipulation.argtypes = [C.POINTER(abi.mppi_assisted_manipulation_desc)]
+    L.oracle_forecast_create.restype = vp
+    L.oracle_forecast_create.argtypes = [C.POINTER(abi.mppi_forecast_config), C.c_char_p, C.c_int]
+    L.oracle_forecast_destroy.argtypes = [vp]
+    L.oracle_forecast_observe.argtypes = [vp, dp, C.c_double]
+    L.oracle_forecast_observe_time.argtypes = [vp, C.c_double]
+    L.oracle_forecast_get.argtypes = [vp, C.c_double, dp]
     if path is None:
         _lib = L
     return L
@@ -228,3 +234,36 @@ class OracleTrajectory:
 
     def update_duration(self):
         return self._L.oracle_update_duration(self._h)
+
+
+class OracleForecast:
+    """controller/forecast.{hpp,cpp} + kalman.cpp restated (oracle/forecast_oracle.cpp)."""
+
+    def __init__(self, config):
+        self._L = lib()
+        err = C.create_string_buffer(256)
+        self._h = self._L.oracle_forecast_create(C.byref(config), err, 256)
+        self.error = err.value.decode()
+        if not self._h:
+            raise ValueError(self.error)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.oracle_forecast_destroy(self._h)
+            self._h = None
+
+    def observe(self, wrench, time):
+        w = np.ascontiguousarray(wrench, dtype=np.float64)
+        self._L.oracle_forecast_observe(self._h, _p(w), float(time))
+
+    def observe_time(self, time):
+        self._L.oracle_forecast_observe_time(self._h, float(time))
+
+    def get(self, time):
+        out = np.zeros(6)
+        self._L.oracle_forecast_get(self._h, float(time), _p(out))
+        return out
+
+    def table(self, t0, dt, H):
+        """[H x 6]: forecast(t0 + k dt), what the rollout's cost queries at step k."""
+        return np.array([self.get(t0 + k * dt) for k in range(H)])

@@ -521,6 +521,86 @@ CMIN = np.array([-0.5, -0.5, -1.0] + [-100.0] * 7 + [-0.05, -0.05])
 CMAX = -CMIN
 
 
+class KalmanForecastNp:
+    """KalmanForecast + KalmanFilter (forecast.cpp:131-367, kalman.cpp:103-152) restated with
+    numpy matrices: np.linalg.inv for the gain and the horison as matrix powers F^i x (the
+    reference iterates predict(false)), so it is built differently from the C++ oracle."""
+
+    def __init__(self, order, time_step, horison, initial_state):
+        self.n = n = 6 * (order + 1)
+        self.order, self.dt, self.horison = order, time_step, horison
+        self.steps = int(math.ceil(horison / time_step))
+        F = np.zeros((n, n))
+        for d in range(order + 1):
+            for s in range(6):
+                for i in range(order - d + 1):
+                    F[d * 6 + s, d * 6 + i * 6 + s] = time_step ** i / math.factorial(i)
+        self.F = F
+        self.Q = self.R = np.eye(n) * 1e-8
+        self.P = np.eye(n) * 1e-8
+        self.x = np.zeros(n)
+        self.x[:6] = initial_state
+        self.xn = F @ self.x
+        self.meas = np.zeros(n)
+        self.last = -time_step
+        self.pred = np.zeros((self.steps + 1, n))
+
+    def observe(self, m, t):
+        dt = t - self.last
+        delta = (np.asarray(m) - self.meas[:6]) / dt
+        for i in range(1, self.order + 1):
+            nxt = (delta - self.meas[6 * i:6 * i + 6]) / dt
+            self.meas[6 * i:6 * i + 6] = delta
+            delta = nxt
+        self.meas[:6] = m
+        self.last = t
+        K = self.P @ np.linalg.inv(self.P + self.R)
+        self.x = self.xn + K @ (self.meas - self.xn)
+        self.P = (np.eye(self.n) - K) @ self.P
+        self.xn = self.F @ self.x
+        self.P = self.F @ self.P @ self.F.T + self.Q
+        for i in range(self.steps + 1):
+            self.pred[i] = np.linalg.matrix_power(self.F, i) @ self.x
+
+    def observe_time(self, t):
+        if t <= self.last:
+            return
+        self.x = self.xn
+        self.xn = self.F @ self.x
+        self.P = self.F @ self.P @ self.F.T + self.Q
+
+    def get(self, t):
+        if t > self.last + self.horison:
+            return np.zeros(6)
+        u = (t - self.last) / self.dt
+        lo = int(u)
+        u -= lo
+        lo = min(max(lo, 0), self.steps)
+        hi = min(lo + 1, self.steps)
+        return (1.0 - u) * self.pred[lo, :6] + u * self.pred[hi, :6]
+
+
+def gen_kalman(order, seed, H=64):
+    """An actor-like event stream (actor.cpp:155-197): a wrench observed every 5 ms, time ticks
+    in between, and the H-step table an update at the same instant would sample."""
+    rng = np.random.default_rng(seed)
+    kf = KalmanForecastNp(order, 0.005, 0.3, np.zeros(6))
+    events, tables = [], []
+    for j in range(40):
+        t = 0.005 * j
+        w = np.array([20 + 5 * math.sin(4 * t), 3 * math.cos(2 * t), -1 + t, 0.1, -0.2, 0.05 * j]) + rng.normal(0, 0.2, 6)
+        kf.observe(w, t)
+        events.append(np.concatenate([[0.0, t], w]))
+        for q in (0.001, 0.002, 0.003):
+            kf.observe_time(t + q)
+            events.append(np.concatenate([[1.0, t + q], np.zeros(6)]))
+        if j % 8 == 7:
+            tables.append(np.array([kf.get(t + 0.004 + 0.01 * k) for k in range(H)]))
+            events.append(np.concatenate([[2.0, t + 0.004], np.zeros(6)]))
+    return dict(order=np.array(order), time_step=np.array(0.005), horison=np.array(0.3),
+                events=np.array(events), tables=np.array(tables), H=np.array(H), dt=np.array(0.01))
+
+
 def huddled():
     x = np.zeros(31)
     x[:12] = [0.2, 0.2, math.pi / 4, 0.0, math.pi / 5, 0.0, -math.pi / 2, 0.0, 2, math.pi / 4, 0.025, 0.025]
@@ -595,6 +675,13 @@ def gen_updates(rob, S, K, H, updates, seed, smoothing=None, track_point=False, 
 
 def main():
     rob = Robot()
+    if "--kalman" in sys.argv or not os.path.exists(os.path.join(HERE, "kalman.npz")):
+        print("Kalman forecast fixtures (orders 1, 2)")
+        k1, k2 = gen_kalman(1, 41), gen_kalman(2, 42)
+        np.savez_compressed(os.path.join(HERE, "kalman.npz"), **{"o1_" + k: v for k, v in k1.items()},
+                            **{"o2_" + k: v for k, v in k2.items()})
+        if "--kalman" in sys.argv:
+            return
     if "--energy" in sys.argv or not os.path.exists(os.path.join(HERE, "nle.npz")):
         print("NLE fixtures (complex-step Lagrangian)")
         rng = np.random.default_rng(5)
