@@ -50,9 +50,13 @@ struct mppi_handle {
     // critical path
     hipStream_t stream_rank = nullptr;
     hipEvent_t ev_costs = nullptr, ev_rank = nullptr;
+
     hipEvent_t ev[6] = {};
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
-    bool opt_pending = false;
+    // filter() (the optimal rollout) of the last update: pending (not launched yet: it rides in the
+    // next update's remainder launch, or runs alone when something needs it first), launched
+    enum { OPT_NONE, OPT_PENDING, OPT_LAUNCHED, OPT_FOLDED } opt_state = OPT_NONE;
+    const StepConst *opt_steps = nullptr;   // the step constants its update used
     float kernel_ms[5] = {0, 0, 0, 0, 0};
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
@@ -106,6 +110,8 @@ struct mppi_handle {
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
+    uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
+    std::string trace_path;
     size_t inj_capacity = 0;   // doubles
     int *d_rank = nullptr;
     uint64_t *d_rank_keys = nullptr;   // rank scratch: chunk-sorted cost keys
@@ -122,6 +128,8 @@ struct mppi_handle {
     std::chrono::steady_clock::time_point t_start;
     double phase_time = 0;
 };
+
+static mppi_status launch_filter_standalone(mppi_handle *h);
 
 namespace {
 
@@ -439,6 +447,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     h->begin = 0;
     h->count = h->R;
     h->U_host.assign((size_t)(h->H * h->C), 0.0);
+    if (const char *tp = std::getenv("MPPI_WAVE_TRACE")) h->trace_path = tp;
     {
         const char *kv = std::getenv("MPPI_FR_KERNEL");
         h->coop = !(kv && std::string(kv) == "lane");
@@ -458,6 +467,11 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     } while (0)
 
     CREATE_TRY(hipSetDevice(device));
+    {
+        int ncu = 0;
+        CREATE_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        fr_coop_set_cu_count((unsigned)ncu);
+    }
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_rank, hipStreamNonBlocking));
@@ -635,6 +649,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipDeviceSynchronize());
     CREATE_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream_rank));
     CREATE_TRY(hipEventRecord(h->ev_rank, h->stream_rank));
+    if (!h->trace_path.empty()) CREATE_TRY(dalloc(h, &h->d_trace, (size_t)(4 * (h->R / 4 + 2))));
 #undef CREATE_TRY
     *out = h;
     return MPPI_OK;
@@ -744,6 +759,10 @@ mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6)
     else h->forecast.clear();
     h->fc.type = FC_NONE;   // a table replaces an attached forecast
     HIP_TRY(hipSetDevice(h->device));
+    if (h->opt_state == mppi_handle::OPT_PENDING) {   // the pending filter() reads the old constants
+        mppi_status st = launch_filter_standalone(h);
+        if (st != MPPI_OK) return st;
+    }
     HIP_TRY(hipStreamSynchronize(h->stream_opt));   // the pending optimal rollout reads d_steps
     return upload_steps(h);
 }
@@ -807,6 +826,11 @@ mppi_status mppi_forecast_attach(mppi_handle *h, const mppi_forecast_config *c)
     if (!h) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->opt_state == mppi_handle::OPT_PENDING) {   // the pending filter() reads the current constants
+        mppi_status st = launch_filter_standalone(h);
+        if (st != MPPI_OK) return st;
+        HIP_TRY(hipStreamSynchronize(h->stream_opt));
+    }
     mppi_handle::DeviceForecast &f = h->fc;
     if (!c) {   // detach: back to the caller's table
         f.type = FC_NONE;
@@ -935,6 +959,50 @@ void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 
 // ---- update ---------------------------------------------------------------------------------
 
+// filter() of the last update on the side stream, by itself (mppi.cpp:450-479)
+static mppi_status launch_filter_standalone(mppi_handle *h)
+{
+    HIP_TRY(hipStreamWaitEvent(h->stream_opt, h->ev_pub, 0));
+    HIP_TRY(hipEventRecord(h->ev[4], h->stream_opt));
+    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        FrRolloutArgs a{};
+        a.model = h->d_model;
+        a.cost = h->d_cost;
+        a.steps = h->opt_steps;
+        a.x0 = h->d_x0_opt;
+        a.Ushift = h->d_U;
+        a.cost_out = h->d_opt;
+        a.status = h->d_status;
+        a.count = 1;
+        a.Rpad = 64;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 1;
+        a.cost_kind = h->cost_kind;
+        a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
+        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
+    } else {
+        PmRolloutArgs a{};
+        a.pm = h->d_pm;
+        a.steps = h->opt_steps;
+        a.x0 = h->d_x0_opt;
+        a.Ushift = h->d_U;
+        a.cost_out = h->d_opt;
+        a.status = h->d_status;
+        a.count = 1;
+        a.Rpad = 64;
+        a.dt = h->dt;
+        a.H = (int)h->H;
+        a.optimal = 1;
+        HIP_TRY(launch_pm_rollout(a, h->stream_opt));
+    }
+    HIP_TRY(hipEventRecord(h->ev_opt_end, h->stream_opt));
+    HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream_opt));
+    HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream_opt));
+    h->opt_state = mppi_handle::OPT_LAUNCHED;
+    return MPPI_OK;
+}
+
 mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
 {
     if (!h || !state) return MPPI_ERR_INVALID;
@@ -1016,7 +1084,24 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.status = h->d_status;
         a.cost_kind = h->cost_kind;
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
-        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream) : launch_fr_rollout(a, h->stream));
+        a.trace = h->d_trace;
+        // a pending filter() not folded here stays pending: this update's phase 3 supersedes it,
+        // and only the latest one is observable (mppi_optimal_cost / logger)
+        const bool fold = use_coop(h) && h->opt_state == mppi_handle::OPT_PENDING;
+        if (fold) {   // the previous update's filter() as one more row of the remainder launch
+            a.fx0 = h->d_x0_opt;
+            a.fU = h->d_U;
+            a.fsteps = h->opt_steps;
+            a.fcost = h->d_opt;
+        }
+        bool folded = false;
+        HIP_TRY(use_coop(h) ? launch_fr_coop_update(a, h->stream, &folded) : launch_fr_rollout(a, h->stream));
+        if (folded) {   // the optimal cost is ready with this update's rollouts
+            HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream));
+            h->kernel_ms[3] = 0.0f;   // timed inside the rollout launch
+            h->opt_state = mppi_handle::OPT_FOLDED;
+        }
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -1092,45 +1177,15 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     HIP_TRY(hipMemcpyAsync(h->d_x0_opt, h->d_x0, (size_t)h->X * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
-    // filter(): cost of the published U* (mppi.cpp:450-479) on the side stream
-    HIP_TRY(hipStreamWaitEvent(h->stream_opt, h->ev_pub, 0));
-    HIP_TRY(hipEventRecord(h->ev[4], h->stream_opt));
-    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
-        FrRolloutArgs a{};
-        a.model = h->d_model;
-        a.cost = h->d_cost;
-        a.steps = h->d_steps;
-        a.x0 = h->d_x0_opt;
-        a.Ushift = h->d_U;
-        a.cost_out = h->d_opt;
-        a.status = h->d_status;
-        a.count = 1;
-        a.Rpad = 64;
-        a.dt = h->dt;
-        a.H = (int)h->H;
-        a.optimal = 1;
-        a.cost_kind = h->cost_kind;
-        a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
-        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
-    } else {
-        PmRolloutArgs a{};
-        a.pm = h->d_pm;
-        a.steps = h->d_steps;
-        a.x0 = h->d_x0_opt;
-        a.Ushift = h->d_U;
-        a.cost_out = h->d_opt;
-        a.status = h->d_status;
-        a.count = 1;
-        a.Rpad = 64;
-        a.dt = h->dt;
-        a.H = (int)h->H;
-        a.optimal = 1;
-        HIP_TRY(launch_pm_rollout(a, h->stream_opt));
+    // filter(): cost of the published U* (mppi.cpp:450-479).  With the cooperative kernel it rides
+    // in the next update's remainder launch (it then shares a SIMD with rollouts 0 and 1 instead of
+    // doubling up a SIMD of the next update's main launch); otherwise it runs now on the side stream.
+    h->opt_steps = h->d_steps;
+    h->opt_state = mppi_handle::OPT_PENDING;
+    if (!(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h))) {
+        mppi_status st = launch_filter_standalone(h);
+        if (st != MPPI_OK) return st;
     }
-    HIP_TRY(hipEventRecord(h->ev_opt_end, h->stream_opt));
-    HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream_opt));
-    HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream_opt));
-    h->opt_pending = true;
     HIP_TRY(hipEventRecord(h->ev[5], h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->phase_open = false;
@@ -1144,6 +1199,14 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         std::lock_guard<std::mutex> lock(h->mtx);   // publish under lock (mppi.cpp:178-182)
         h->last_rollout_time = h->rollout_time;
         std::memcpy(h->U_host.data(), h->h_out, (size_t)HC * sizeof(double));
+    }
+    if (h->d_trace) {   // diagnostics: append this update's per-block records
+        std::vector<uint32_t> tr((size_t)(4 * (h->R / 4 + 2)));
+        HIP_TRY(hipMemcpy(tr.data(), h->d_trace, tr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (FILE *fp = std::fopen(h->trace_path.c_str(), "ab")) {
+            std::fwrite(tr.data(), sizeof(uint32_t), tr.size(), fp);
+            std::fclose(fp);
+        }
     }
     h->update_duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - h->t_start).count();
     h->update_last = h->rollout_time;
@@ -1221,11 +1284,15 @@ mppi_status mppi_optimal_control(mppi_handle *h, double *out)
 
 static mppi_status wait_optimal(mppi_handle *h)
 {
-    if (!h->opt_pending) return MPPI_OK;
+    if (h->opt_state == mppi_handle::OPT_PENDING) {
+        mppi_status st = launch_filter_standalone(h);
+        if (st != MPPI_OK) return st;
+    }
+    if (h->opt_state != mppi_handle::OPT_LAUNCHED && h->opt_state != mppi_handle::OPT_FOLDED) return MPPI_OK;
     HIP_TRY(hipEventSynchronize(h->ev_opt_done));
-    (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
+    if (h->opt_state == mppi_handle::OPT_LAUNCHED) (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
     h->opt_cost = h->h_opt[0];
-    h->opt_pending = false;
+    h->opt_state = mppi_handle::OPT_NONE;
     return MPPI_OK;
 }
 
@@ -1319,7 +1386,7 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
 {
     if (!h || !ms5) return MPPI_ERR_INVALID;
-    if (h->opt_pending && hipEventQuery(h->ev_opt_end) == hipSuccess)
+    if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
     std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
     return MPPI_OK;

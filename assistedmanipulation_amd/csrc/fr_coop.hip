@@ -47,7 +47,6 @@ namespace {
 constexpr int ROW = 16;
 constexpr int ROWS_PER_WAVE = 4;
 constexpr int CK_ASSISTED_MANIPULATION = 1, CK_TRACK_POINT = 3;   // mppi_cost_kind
-constexpr int COOP_NT = 64;   // one wave per workgroup
 constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 store into
 
 // LDS per row (doubles).  Kinematic array (written by FK): packed world inertias (21) and motion
@@ -703,62 +702,73 @@ __device__ __forceinline__ double objective_terms(const DevCost &Cs, bool jl, in
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int CK, bool EN>
-__global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
+// Stage the per-body table (geometry, inertia, axes, cost weights, lane masks) in LDS.
+__device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double *Lmodel, int nt)
 {
-    constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
-    __shared__ double lds_kin[ROWS_PER_WAVE * KS];
-    __shared__ double lds_scr[ROWS_PER_WAVE * LDS_SCR];
-    __shared__ double Lmodel[LDS_MODEL];
-    if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;
-    const int lane = threadIdx.x;
-    const int j = lane & (ROW - 1);
-    const int rowi = lane >> 4;
-    double *Lk = lds_kin + rowi * KS;
-    double *Lw = lds_scr + rowi * LDS_SCR;
-    {   // stage the body table
-        const DevModel &dm = *a.model;
-        const DevCost &dc = *a.cost;
-        for (int t = lane; t < LDS_MODEL; t += COOP_NT) {
-            const int row = t / MB, f = t % MB;
-            const bool dummy = row == FR_NB;
-            const int b = dummy ? 0 : row;
-            const DevBody &db = dm.b[b];
-            const int kind = FR_KIND[b];
-            const double *Rs = (b == 11) ? dm.f11_R : db.R;
-            const double *ps = (b == 11) ? dm.f11_p : db.p;
-            // translation axis a_t (prismatic; 0 for revolute) and joint axis a, body frame
-            const double ax0 = (kind == KIND_PX) ? 1.0 : 0.0;
-            const double ax1 = (kind == KIND_PY) ? 1.0 : ((kind == KIND_PNY) ? -1.0 : 0.0);
-            const double ax2 = (kind == KIND_RZ) ? 1.0 : 0.0;
-            const double live = dummy ? 0.0 : 1.0;
-            double v;
-            if (f < T_P) v = Rs[f];
-            else if (f < T_M) v = ps[f - T_P];
-            else if (f == T_M) v = db.mass;
-            else if (f < T_I) v = db.c[f - T_C];
-            else if (f < T_F) v = db.Ic[f - T_I];
-            else if (f < T_MA) v = (b == FR_EE_PARENT) ? dm.ee_p[f - T_F] : ((b == FR_AM_PARENT) ? dm.am_p[f - T_F] : 0.0);
-            else if (f < T_AX) {
-                const int r = f - T_MA;
-                v = Rs[3 * r] * ax0 + Rs[3 * r + 1] * ax1;   // a_t = a for prismatic joints (PX, PY, PNY)
-            } else if (f == T_AX) v = ax0;
-            else if (f == T_AX + 1) v = ax1;
-            else if (f == T_AX + 2) v = ax2;
-            else if (f == T_ROT) v = (kind == KIND_RZ) ? live : 0.0;
-            else if (f == T_NROT) v = (kind == KIND_RZ) ? 0.0 : live;
-            else if (f < T_UP) v = live * ((f == T_LO) ? dc.lower[b].bound : (f == T_LO + 1) ? dc.lower[b].scale : dc.lower[b].max);
-            else if (f < T_VW) v = live * ((f == T_UP) ? dc.upper[b].bound : (f == T_UP + 1) ? dc.upper[b].scale : dc.upper[b].max);
-            else if (f == T_VW) v = live * dc.vel_q[b];
-            else if (f == T_WV) v = (!dummy && b <= FR_EE_PARENT) ? 1.0 : 0.0;
-            else if (f == T_WA) v = (!dummy && b >= FR_ARM0 && b < FR_ARM1) ? 1.0 : 0.0;
-            else v = (!dummy && b == 11) ? -1.0 : 0.0;   // T_FIX
-            Lmodel[t] = v;
-        }
-        __syncthreads();
+    const DevModel &dm = *a.model;
+    const DevCost &dc = *a.cost;
+    for (int t = threadIdx.x; t < LDS_MODEL; t += nt) {
+        const int row = t / MB, f = t % MB;
+        const bool dummy = row == FR_NB;
+        const int b = dummy ? 0 : row;
+        const DevBody &db = dm.b[b];
+        const int kind = FR_KIND[b];
+        const double *Rs = (b == 11) ? dm.f11_R : db.R;
+        const double *ps = (b == 11) ? dm.f11_p : db.p;
+        // translation axis a_t (prismatic; 0 for revolute) and joint axis a, body frame
+        const double ax0 = (kind == KIND_PX) ? 1.0 : 0.0;
+        const double ax1 = (kind == KIND_PY) ? 1.0 : ((kind == KIND_PNY) ? -1.0 : 0.0);
+        const double ax2 = (kind == KIND_RZ) ? 1.0 : 0.0;
+        const double live = dummy ? 0.0 : 1.0;
+        double v;
+        if (f < T_P) v = Rs[f];
+        else if (f < T_M) v = ps[f - T_P];
+        else if (f == T_M) v = db.mass;
+        else if (f < T_I) v = db.c[f - T_C];
+        else if (f < T_F) v = db.Ic[f - T_I];
+        else if (f < T_MA) v = (b == FR_EE_PARENT) ? dm.ee_p[f - T_F] : ((b == FR_AM_PARENT) ? dm.am_p[f - T_F] : 0.0);
+        else if (f < T_AX) {
+            const int r = f - T_MA;
+            v = Rs[3 * r] * ax0 + Rs[3 * r + 1] * ax1;   // a_t = a for prismatic joints (PX, PY, PNY)
+        } else if (f == T_AX) v = ax0;
+        else if (f == T_AX + 1) v = ax1;
+        else if (f == T_AX + 2) v = ax2;
+        else if (f == T_ROT) v = (kind == KIND_RZ) ? live : 0.0;
+        else if (f == T_NROT) v = (kind == KIND_RZ) ? 0.0 : live;
+        else if (f < T_UP) v = live * ((f == T_LO) ? dc.lower[b].bound : (f == T_LO + 1) ? dc.lower[b].scale : dc.lower[b].max);
+        else if (f < T_VW) v = live * ((f == T_UP) ? dc.upper[b].bound : (f == T_UP + 1) ? dc.upper[b].scale : dc.upper[b].max);
+        else if (f == T_VW) v = live * dc.vel_q[b];
+        else if (f == T_WV) v = (!dummy && b <= FR_EE_PARENT) ? 1.0 : 0.0;
+        else if (f == T_WA) v = (!dummy && b >= FR_ARM0 && b < FR_ARM1) ? 1.0 : 0.0;
+        else v = (!dummy && b == 11) ? -1.0 : 0.0;   // T_FIX
+        Lmodel[t] = v;
     }
-    const int64_t lr = (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // local rollout of this row
-    const bool live = lr < a.count;
+}
+
+// One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
+// row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / fcost).
+template <int CK, bool EN, bool FROW>
+__device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
+                                          const double *Lmodel)
+{
+    const int j = lane & (ROW - 1);
+#ifdef COOP_TRACE
+    if (a.trace && lane == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.trace[4 * wblk + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        a.trace[4 * wblk + 2] = hw;
+        a.trace[4 * wblk + 3] = xcc;
+    }
+#endif
+    // FROW: the row after the last rollout is the previous update's filter() (optimal rollout)
+    const bool frow = FROW && a.fcost != nullptr && lr == a.count;
+    const bool live = lr < a.count || frow;
+    const bool opt_row = a.optimal || frow;   // no noise, no NaN stop (mppi.cpp:450-479)
+    const double *x0p = FROW && frow ? a.fx0 : a.x0;
+    const double *Up = FROW && frow ? a.fU : a.Ushift;
+    const StepConst *stp = FROW && frow ? a.fsteps : a.steps;
     const int64_t g = a.optimal ? -1 : a.begin + lr;
     const int H = a.H;
     const bool jl = j < FR_NB;   // lane owns a body / control component
@@ -769,31 +779,31 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
     L.is_rz = jl && FR_KIND[jb] == KIND_RZ;
     L.slot = jl ? j : FR_NB;
 
-    double q = live && jl ? a.x0[jb] : 0.0;
-    double qd = live && jl ? a.x0[FR_NB + jb] : 0.0;
-    double E = EN && live ? a.x0[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+    double q = live && jl ? x0p[jb] : 0.0;
+    double qd = live && jl ? x0p[FR_NB + jb] : 0.0;
+    double E = EN && live ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
     const double *grav = a.model->gravity;
     double sq, cq;
     sincos(q, &sq, &cq);   // one sincos per lane and step: FK, base yaw, workspace
     CoopKin kin;
-    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[0], kin, grav);   // set_state -> calculate() at (q0, v0)
+    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, Cs, stp[0], kin, grav);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step, first used after its cost
-    const bool sampled = !a.optimal && live && jl;
+    const bool sampled = !opt_row && live && jl;
     const int64_t nstride = a.Rpad * FR_C;
-    const double *np = sampled ? a.noise + lr * FR_C + jb : a.Ushift;   // any valid address when unused
+    const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
     double J = 0.0;
     bool alive = true;
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[sampled ? (int64_t)k * nstride : 0];
-        const double ub_l = a.Ushift[k * FR_C + jb];
+        const double ub_l = Up[k * FR_C + jb];
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
 #ifdef ABL_NOCOST
         const double step_cost = 0.0;
 #else
-        const double step_cost = a.steps[k].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
+        const double step_cost = stp[k].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
 #endif
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
@@ -806,7 +816,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
 #ifndef ABL_NOFK
-        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, Cs, a.steps[k + 1], kin, grav);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, Cs, stp[k + 1], kin, grav);
 #endif
         double pe = 0.0;
 #ifdef ABL_NOABA
@@ -822,7 +832,7 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
             E = smax(0.0, E + power * a.dt);
         }
         sincos(q, &sq, &cq);
-        if (!a.optimal && isnan(step_cost)) {   // rollout cost NaN: stop (mppi.cpp:331-334)
+        if (!opt_row && isnan(step_cost)) {   // rollout cost NaN: stop (mppi.cpp:331-334)
             J = NAN;
             alive = false;
             break;
@@ -830,23 +840,125 @@ __global__ __launch_bounds__(COOP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
         J += step_cost;
     }
     if (alive) {   // the final step's cost; its dynamics are never observed
-        const double step_cost = a.steps[H - 1].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
-        J = (!a.optimal && isnan(step_cost)) ? NAN : J + step_cost;
+        const double step_cost = stp[H - 1].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
+        J = (!opt_row && isnan(step_cost)) ? NAN : J + step_cost;
     }
+#ifdef COOP_TRACE
+    if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
     if (!live || j != 0) return;
-    if (a.optimal) *a.cost_out = J;
-    else a.cost_out[g] = J;
+    if (FROW && frow) {   // skipped when the update threw (no filter(), mppi.cpp:170-176)
+        if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;
+    } else if (a.optimal) {
+        *a.cost_out = J;
+    } else {
+        a.cost_out[g] = J;
+    }
+}
+
+// WPB waves per workgroup.  The update's launch uses WPB = 5 with > 80 KB of LDS per workgroup, so a
+// CU holds one workgroup: waves 0..3 take one SIMD each, and wave 4 runs the rows left over when
+// the rollouts do not fill four-wave groups (rollouts 0 and 1 of the reference's R = S + 2, plus the
+// previous update's filter()) or exits at once.  With one-wave workgroups the dispatcher balances
+// waves per CU but not per SIMD: the ~9 % of SIMDs it gave two waves ran 1.23x longer and set the
+// kernel's time, and a separate launch for the leftover rows was placed by XCD round-robin, not
+// on the free CU (per-block traces, tools/wave_trace.py).
+template <int CK, bool EN, int WPB, bool FROW>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
+{
+    constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
+    __shared__ double lds_kin[WPB * ROWS_PER_WAVE * KS];
+    __shared__ double lds_scr[WPB * ROWS_PER_WAVE * LDS_SCR];
+    __shared__ double Lmodel[LDS_MODEL];
+    if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;
+    const int wv = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int rowi = lane >> 4;
+    const int wrow = wv * ROWS_PER_WAVE + rowi;   // row within the workgroup
+    const int wblk = blockIdx.x * WPB + wv;        // wave index in the launch
+    stage_body_table(a, Lmodel, 64 * WPB);
+    __syncthreads();
+    coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
+                            Lmodel);
+}
+
+// The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and a fifth wave
+// for the extra rows [xbase, count) plus the folded filter() row (xrows of them in all).
+template <int CK, bool EN>
+__global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
+{
+    constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
+    __shared__ double lds_kin[5 * ROWS_PER_WAVE * KS];
+    __shared__ double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
+    __shared__ double Lmodel[LDS_MODEL];
+    const int wv = (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int rowi = lane >> 4;
+    const int wrow = wv * ROWS_PER_WAVE + rowi;
+    stage_body_table(a, Lmodel, 320);
+    __syncthreads();
+    double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
+    if (wv < 4) {
+        const int wblk = blockIdx.x * 4 + wv;
+        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel);
+    } else if ((int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows) {
+        const int wblk = gridDim.x * 4 + blockIdx.x;
+        coop_rows<CK, EN, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel);
+    }
 }
 
 namespace mppi_eng {
+
+static unsigned g_cu_count = 256;   // set by fr_coop_set_cu_count (hipDeviceProp multiProcessorCount)
+
+void fr_coop_set_cu_count(unsigned n) { g_cu_count = n ? n : 256; }
+
+template <int WPB, bool FROW>
+static void launch_one(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
+{
+    const dim3 grid(nb), block(64 * WPB);
+    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_coop_kernel<CK_TRACK_POINT, false, WPB, FROW>), grid, block, 0, s, a);
+    else if (a.energy) hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, true, WPB, FROW>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, false, WPB, FROW>), grid, block, 0, s, a);
+}
 
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
 {
     const unsigned nb = (unsigned)((a.count + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
     if (nb == 0) return hipSuccess;
-    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_coop_kernel<CK_TRACK_POINT, false>), dim3(nb), dim3(COOP_NT), 0, s, a);
-    else if (a.energy) hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, true>), dim3(nb), dim3(COOP_NT), 0, s, a);
-    else hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, false>), dim3(nb), dim3(COOP_NT), 0, s, a);
+    launch_one<1, false>(a, nb, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, bool *folded)
+{
+    constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
+    const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
+    *folded = false;
+    // the previous update's filter() rides along when there are extra rows anyway (the fifth wave
+    // of the first workgroup has room); alone it would add a wave, so then it stays pending
+    const bool frow = a0.fcost != nullptr && extra > 0;
+    const int64_t xrows = extra + (frow ? 1 : 0);
+    if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
+        FrRolloutArgs a = a0;   // more than one round of workgroups: one-wave workgroups throughout
+        a.fcost = nullptr;
+        return launch_fr_coop(a, s);
+    }
+    FrRolloutArgs a = a0;
+    if (!frow) a.fcost = nullptr;
+    a.xbase = groups * WG_ROWS;
+    a.xrows = xrows;
+    const dim3 grid((unsigned)groups);
+    if (xrows == 0) {
+        launch_one<4, false>(a, (unsigned)groups, s);
+    } else if (a.cost_kind == CK_TRACK_POINT) {
+        hipLaunchKernelGGL((fr_coop_x_kernel<CK_TRACK_POINT, false>), grid, dim3(320), 0, s, a);
+    } else if (a.energy) {
+        hipLaunchKernelGGL((fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, true>), grid, dim3(320), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, false>), grid, dim3(320), 0, s, a);
+    }
+    *folded = frow;
     return hipGetLastError();
 }
 

@@ -32,6 +32,13 @@ struct FrRolloutArgs {
     int optimal;
     int cost_kind;            // mppi_cost_kind: AssistedManipulation or TrackPoint
     int energy;               // AssistedManipulation enable_energy_limit: the tank's NLE power
+    uint32_t *trace;          // diagnostics (COOP_TRACE builds, MPPI_WAVE_TRACE): per block start, end, hw id, xcc
+    // filter() of the previous update folded into this launch as one extra row (fr_coop.hip):
+    // its state, published U*, step constants and cost output
+    const double *fx0, *fU;
+    const StepConst *fsteps;
+    double *fcost;
+    int64_t xbase, xrows;     // fr_coop_x_kernel: the fifth waves' rows [xbase, xbase + xrows)
 };
 
 // sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
@@ -140,6 +147,11 @@ constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's fir
 hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
                            int H, int C, const Status *status, double *gsplit, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
+void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split leaves one CU to the remainder)
+// The update's rollouts (fr_coop_x_kernel): one workgroup per CU of four one-SIMD waves of rollouts
+// plus a fifth wave for the rows left over (and, when there are some, the previous update's
+// filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, bool *folded);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
 
 
