@@ -794,9 +794,19 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
     double J = 0.0;
     bool alive = true;
+#ifdef NO_EPS_PREFETCH
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[sampled ? (int64_t)k * nstride : 0];
         const double ub_l = Up[k * FR_C + jb];
+#else
+    // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
+    // whose latency a single wave per SIMD cannot hide within one step
+    double eps_n = np[0], ub_n = Up[jb];
+    for (int k = 0; k < H - 1; k++) {
+        const double eps_l = eps_n, ub_l = ub_n;
+        eps_n = np[sampled ? (int64_t)(k + 1) * nstride : 0];
+        ub_n = Up[(k + 1) * FR_C + jb];
+#endif
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
         // cost at x_k with the kinematics cached by the previous calculate()
