@@ -63,6 +63,7 @@ PROTOTYPES = {
     "mppi_smoothing_windows": (C.c_int, [_h, _dp, _dp, _i64p]),
     "mppi_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float)]),
     "mppi_kernel_times_nowait": (C.c_int, [_h, C.POINTER(C.c_float)]),
+    "mppi_kernel_times_detail": (C.c_int, [_h, C.POINTER(C.c_float), C.c_int]),
 }
 
 _lib = None

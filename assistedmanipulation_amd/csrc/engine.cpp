@@ -53,11 +53,13 @@ struct mppi_handle {
 
     hipEvent_t ev[6] = {};
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
+    hipEvent_t ev_dyn = nullptr;   // after the rollout (dynamics) kernel, before the cost kernel
     // filter() (the optimal rollout) of the last update: pending (not launched yet: it rides in the
     // next update's remainder launch, or runs alone when something needs it first), launched
     enum { OPT_NONE, OPT_PENDING, OPT_LAUNCHED, OPT_FOLDED } opt_state = OPT_NONE;
     const StepConst *opt_steps = nullptr;   // the step constants its update used
-    float kernel_ms[5] = {0, 0, 0, 0, 0};
+    // sample, rollout (dynamics + cost kernels), reduce, optimal rollout, update, dynamics kernel
+    float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
     double dt = 0, gradient_step = 0, cost_scale = 0, gamma = 1;
@@ -109,6 +111,8 @@ struct mppi_handle {
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
+    // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
+    double *d_rec = nullptr, *d_rec_opt = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
@@ -339,6 +343,10 @@ mppi_status alloc_shard_buffers(mppi_handle *h)
     h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
     HIP_TRY(dalloc(h, &h->d_noise, (size_t)(h->H * h->C * h->Rpad)));
     HIP_TRY(dalloc(h, &h->d_noise_prev, (size_t)(h->H * h->C * h->Rpad)));
+    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
+        dfree(h, h->d_rec);
+        HIP_TRY(dalloc(h, &h->d_rec, (size_t)(h->H * h->Rpad * FR_NREC)));
+    }
     return MPPI_OK;
 }
 
@@ -481,6 +489,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_pub, hipEventDisableTiming));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
     CREATE_TRY(hipEventCreate(&h->ev_opt_end));
+    CREATE_TRY(hipEventCreate(&h->ev_dyn));
     const size_t HC = (size_t)(h->H * h->C);
     CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
@@ -493,6 +502,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
+    CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_NREC)));
     CREATE_TRY(dalloc(h, &h->d_out, HC + 8));
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
@@ -670,6 +680,7 @@ void mppi_destroy(mppi_handle *h)
     if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
+    if (h->ev_dyn) (void)hipEventDestroy(h->ev_dyn);
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
     if (h->ev_costs) (void)hipEventDestroy(h->ev_costs);
     if (h->ev_rank) (void)hipEventDestroy(h->ev_rank);
@@ -959,6 +970,28 @@ void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 
 // ---- update ---------------------------------------------------------------------------------
 
+// The cost kernel's view of a cooperative rollout launch (same rows, records and outputs).
+static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
+{
+    FrCostArgs c{};
+    c.cost = a.cost;
+    c.steps = a.steps;
+    c.rec = a.rec;
+    c.begin = a.begin;
+    c.count = a.count;
+    c.cost_out = a.cost_out;
+    c.status = a.status;
+    c.H = a.H;
+    c.optimal = a.optimal;
+    c.cost_kind = a.cost_kind;
+    c.energy = a.energy;
+    c.frec = a.frec;
+    c.fsteps = a.fsteps;
+    c.fcost = a.fcost;
+    (void)h;
+    return c;
+}
+
 // filter() of the last update on the side stream, by itself (mppi.cpp:450-479)
 static mppi_status launch_filter_standalone(mppi_handle *h)
 {
@@ -980,7 +1013,13 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         a.optimal = 1;
         a.cost_kind = h->cost_kind;
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
-        HIP_TRY(use_coop(h) ? launch_fr_coop(a, h->stream_opt) : launch_fr_rollout(a, h->stream_opt));
+        a.rec = h->d_rec_opt;
+        if (use_coop(h)) {
+            HIP_TRY(launch_fr_coop(a, h->stream_opt));
+            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
+        } else {
+            HIP_TRY(launch_fr_rollout(a, h->stream_opt));
+        }
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -1085,6 +1124,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.cost_kind = h->cost_kind;
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
+        a.rec = h->d_rec;
         // a pending filter() not folded here stays pending: this update's phase 3 supersedes it,
         // and only the latest one is observable (mppi_optimal_cost / logger)
         const bool fold = use_coop(h) && h->opt_state == mppi_handle::OPT_PENDING;
@@ -1093,9 +1133,18 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.fU = h->d_U;
             a.fsteps = h->opt_steps;
             a.fcost = h->d_opt;
+            a.frec = h->d_rec_opt;
         }
         bool folded = false;
-        HIP_TRY(use_coop(h) ? launch_fr_coop_update(a, h->stream, &folded) : launch_fr_rollout(a, h->stream));
+        if (use_coop(h)) {
+            HIP_TRY(launch_fr_coop_update(a, h->stream, &folded));
+            HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+            if (!folded) a.fcost = nullptr;
+            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+        } else {
+            HIP_TRY(launch_fr_rollout(a, h->stream));
+            HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+        }
         if (folded) {   // the optimal cost is ready with this update's rollouts
             HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream));
             HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream));
@@ -1117,6 +1166,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.H = (int)h->H;
         a.optimal = 0;
         HIP_TRY(launch_pm_rollout(a, h->stream));
+        HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
     }
     HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     h->updated_once = true;
@@ -1191,6 +1241,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     h->phase_open = false;
     for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
     (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
+    (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
     if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
@@ -1379,16 +1430,21 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
     if (!h || !ms5) return MPPI_ERR_INVALID;
     mppi_status st = wait_optimal(h);
     if (st != MPPI_OK) return st;
-    std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
+    std::memcpy(ms5, h->kernel_ms, 5 * sizeof(float));
     return MPPI_OK;
 }
 
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
 {
-    if (!h || !ms5) return MPPI_ERR_INVALID;
+    return mppi_kernel_times_detail(h, ms5, 5);
+}
+
+mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
+{
+    if (!h || !ms || n < 0 || n > 6) return MPPI_ERR_INVALID;
     if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
-    std::memcpy(ms5, h->kernel_ms, sizeof(h->kernel_ms));
+    std::memcpy(ms, h->kernel_ms, (size_t)n * sizeof(float));
     return MPPI_OK;
 }
 

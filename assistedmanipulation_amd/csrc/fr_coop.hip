@@ -16,19 +16,22 @@
 //                 local transform carries -q10, so its prefix world_10 * local_10^-1 * local_11
 //                 is world_9 * local_11 without a second pass.
 //   kinematics    EE / arm-mount positions (row_newbcast 9 / 2); frame velocity J v and J_a J_a^T
-//                 as chains of v_fmac_f64_dpp row_newbcast (lane sums), folded straight into the
-//                 trajectory and manipulability terms of the next step's cost.
+//                 as chains of v_fmac_f64_dpp row_newbcast (lane sums).
 //   ABA           articulated inertia distributed by rows (lane r < 6 holds row r); world
 //                 inertias / S / tau staged in LDS and read one level ahead; S.U, S.pA, the
 //                 rank-1 update A - U U^T / D and the forward U.a are v_fmac_f64_dpp broadcasts.
-//   cost          joint-limit / velocity terms per lane + lane sums; workspace row-uniform.
+//   records       every step's state and kinematics go to a per-rollout record array (kernels.hpp
+//                 FR_NREC); fr_step_cost_kernel (fr_cost.hip) evaluates the objective on all of
+//                 them, a lane per (rollout, step), and sums each rollout's costs in step order.
+//                 The objective's terms are row-uniform, so inside this kernel all 16 lanes of a
+//                 row would repeat them: moving them out cut the executed VALU work by 40 %.
 //
-// The step is written branch-free (selects, not branches) so the cost of step k, the FK of
-// step k and the cost terms of step k + 1 share basic blocks with the ABA chain and the
-// scheduler can fill the chain's latency with them; the NaN stop is tested at the loop latch.
+// The step is written branch-free (selects, not branches) so the FK of step k and its record
+// stores share basic blocks with the ABA chain and the scheduler can fill the chain's latency.
 //
 // Semantics are those of fr_rollout_kernel (PinocchioDynamics::step + AssistedManipulation,
 // one-step kinematic lag, NaN stop); only the association order of sums and products differs.
+// The rollout runs all H - 1 steps: a NaN step cost makes the rollout's sum NaN whatever follows.
 
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -269,22 +272,6 @@ __device__ __forceinline__ double frcp(double d)
     return __builtin_fma(r, e, r);
 }
 
-// AssistedManipulation barriers (assisted_manipulation.cpp), written as selects
-__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v)
-{
-    const double d = v - b.bound;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (b.bound - v), b.max);
-    return (v >= b.bound) ? over : under;
-}
-__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v)
-{
-    const double d = b.bound - v;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (v - b.bound), b.max);
-    return (v <= b.bound) ? over : under;
-}
-
 // One level of the delta-form prefix scan: (I + Da)(I + D) = I + Da + D + Da D,
 // pa + (I + Da) p = pa + p + Da p.
 template <int S>
@@ -383,33 +370,12 @@ __device__ __forceinline__ void inertia_mul(double m, const double *c, const dou
     h[5] = ((Iw[2] * x[3] + Iw[4] * x[4]) + Iw[5] * x[5]) + ch[2];
 }
 
-// What the cost of the next step needs from a calculate(): EE and arm-mount positions (the
-// workspace term also reads the next yaw) and the two terms that depend on the kinematics alone
-// (trajectory: frame velocity; manipulability: J_a J_a^T), folded to scalars right away.
+// What the cost of the next step needs from a calculate() (row-uniform): EE and arm-mount
+// positions, the EE frame velocity J v and J_a J_a^T.  Written to the step record.
 struct CoopKin {
-    double ee[3], am[3], traj, manip;
+    double ee[3], am[3], vl[3], jj[6];
     double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
 };
-
-__device__ __forceinline__ double trajectory_term(const DevCost &Cs, const StepConst &sc, const double *vl)
-{
-    double proj = ((vl[0] * sc.target[0] + vl[1] * sc.target[1]) + vl[2] * sc.target[2]) / sc.tt;
-    const double p0 = proj * sc.target[0], p1 = proj * sc.target[1], p2 = proj * sc.target[2];
-    proj = copysign(1.0, proj) * sqrt((p0 * p0 + p1 * p1) + p2 * p2);
-    const double err = fabs(sc.vtarget - proj);
-    const double tc = sc.pos_cost + ((Cs.traj_vel_c + Cs.traj_vel_l * fabs(err)) + Cs.traj_vel_q * err * err);
-    return sc.active ? tc : 0.0;
-}
-
-__device__ __forceinline__ double manipulability_term(const DevCost &Cs, const double *jj)
-{
-    const double m00 = jj[0], m01 = jj[1], m02 = jj[2], m11 = jj[3], m12 = jj[4], m22 = jj[5];
-    const double det = (m00 * (m11 * m22 - m12 * m12) - m01 * (m01 * m22 - m12 * m02)) + m02 * (m01 * m12 - m11 * m02);
-    double vol = sqrt(det);
-    vol = isnan(vol) ? 1e-5 : ((vol < 1e-5) ? 1e-5 : ((1e5 < vol) ? 1e5 : vol));
-    const double iv = 1.0 / vol;
-    return (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
-}
 
 // Lane-constant data of the row's body j (the doubles live in the body table).
 struct LaneConst {
@@ -420,8 +386,7 @@ struct LaneConst {
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
 template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
-                                        double *Lk, const DevCost &Cs, const StepConst &sc_next, CoopKin &kin,
-                                        const double *grav)
+                                        double *Lk, CoopKin &kin, const double *grav)
 {
     const double cz = L.is_rz ? cq : 1.0;
     const double sz = L.is_rz ? sq : 0.0;
@@ -515,18 +480,15 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
-    kin.traj = 0.0;
-    kin.manip = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) kin.vl[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) kin.jj[k] = 0.0;
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
     // frame velocity J v over the EE chain (bodies 0..9), J_a J_a^T over the arm (bodies 3..9)
-    double vl[3], jj[6];
-    {
-        const double v3[3] = {S[0] * qd, S[1] * qd, S[2] * qd};
-        const double m6[6] = {S[0] * S[0], S[0] * S[1], S[0] * S[2], S[1] * S[1], S[1] * S[2], S[2] * S[2]};
-        kin_sums(v3, m6, 1.0, vl, jj);
-    }
-    kin.traj = trajectory_term(Cs, sc_next, vl);
-    kin.manip = manipulability_term(Cs, jj);
+    const double v3[3] = {S[0] * qd, S[1] * qd, S[2] * qd};
+    const double m6[6] = {S[0] * S[0], S[0] * S[1], S[0] * S[2], S[1] * S[1], S[1] * S[2], S[2] * S[2]};
+    kin_sums(v3, m6, 1.0, kin.vl, kin.jj);
 }
 
 // Articulated-body passes over the world inertias / S staged in LDS; returns qdd of the lane's
@@ -618,88 +580,7 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
     return j < FR_NB ? qdd : 0.0;   // lanes 12..15 keep q = qd = 0
 }
 
-// AssistedManipulation::get_cost at x_k with the kinematics of the previous calculate()
-// (assisted_manipulation.cpp:58-128, term order kept); row-uniform result.
-template <bool EN>
-__device__ __forceinline__ double step_cost_terms(const DevCost &Cs, bool jl, const double *M, double q, double qd, double sq,
-                                                  double cq, const CoopKin &kin, double E)
-{
-    const DevBarrier lo_b{M[T_LO], M[T_LO + 1], M[T_LO + 2]}, up_b{M[T_UP], M[T_UP + 1], M[T_UP + 2]};
-    const double vel_w = M[T_VW];
-    const double lane_joint = jl ? left_barrier(lo_b, q) + right_barrier(up_b, q) : 0.0;
-    const double vq = fabs(qd);
-    const double one = 1.0;
-    double joint, vel;
-    bsum12_pair(lane_joint, vel_w * (vq * vq), one, joint, vel);
-    const double s = bcast<2>(sq), c = bcast<2>(cq);
-    double wc = 0.0;
-    {
-        const double r22 = (1.0 - c) + c;
-        const double fw0 = c, fw1 = s, fw2 = 0.0;
-        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
-        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
-        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
-        const double rb2 = kin.am[2] + off2;
-        const double t0 = kin.ee[0] - (kin.am[0] + off0), t1 = kin.ee[1] - (kin.am[1] + off1), t2 = kin.ee[2] - rb2;
-        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
-        wc += left_barrier(Cs.ws_infront, proj);
-        wc += right_barrier(Cs.ws_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
-        const double n1 = sqrt(t0 * t0 + t1 * t1);
-        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
-        const double yaw = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
-        const double ay = fabs(yaw);
-        const double yc = (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
-        wc += isnan(yaw) ? 0.0 : yc;
-        wc += left_barrier(Cs.ws_above, kin.ee[2] - rb2);
-    }
-    double cost = 0.0;
-    cost += Cs.en_joint ? joint : 0.0;
-    cost += Cs.en_self ? Cs.self_collision : 0.0;
-    cost += Cs.en_work ? wc : 0.0;
-    if constexpr (EN) cost += left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);   // energy_cost (:211-222)
-    cost += Cs.en_vel ? vel : 0.0;
-    cost += Cs.en_traj ? kin.traj : 0.0;
-    cost += Cs.en_manip ? kin.manip : 0.0;
-    return cost;
-}
-
 }  // namespace
-
-// TrackPoint::get_cost (frankaridgeback/objective/track_point.cpp:10-34) at x_k with the previous
-// calculate()'s EE and arm-mount positions; row-uniform result.  The joint terms sum joints 0..9
-// in order and at most one of a joint's two terms is nonzero, so the lane sum adds exactly the
-// reference's nonzero terms in the reference's order.
-__device__ __forceinline__ double track_point_terms(const DevCost &Cs, int j, double q, double sq, double cq, const CoopKin &kin)
-{
-    const double d0 = kin.ee[0] - Cs.tp_point[0], d1 = kin.ee[1] - Cs.tp_point[1], d2 = kin.ee[2] - Cs.tp_point[2];
-    const double distance = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
-    double cost = 100.0 * (distance * distance);   // point_cost: 100 pow(distance, 2)
-    const int jc = j < 10 ? j : 0;
-    const double lo = Cs.tp_lo[jc], up = Cs.tp_up[jc];
-    const double below = (q < lo) ? 1000.0 + 100000.0 * ((lo - q) * (lo - q)) : 0.0;
-    const double above = (q > up) ? 1000.0 + 100000.0 * ((q - up) * (q - up)) : 0.0;
-    const double joint = bsum<0, 10>(j < 10 ? below + above : 0.0, 1.0);
-    // reach_cost: robot = arm mount + R_z(yaw) (0.3, 0, 0.15) (track_point.cpp:162-186)
-    const double s = bcast<2>(sq), c = bcast<2>(cq);
-    const double r22 = (1.0 - c) + c;
-    const double off0 = (0.3 * c + (-s) * 0.0) + 0.0 * 0.15;
-    const double off1 = (0.3 * s + c * 0.0) + 0.0 * 0.15;
-    const double off2 = (0.0 * 0.3 + 0.0 * 0.0) + r22 * 0.15;
-    const double t0 = kin.ee[0] - (kin.am[0] + off0), t1 = kin.ee[1] - (kin.am[1] + off1), t2 = kin.ee[2] - (kin.am[2] + off2);
-    const double reach = right_barrier(Cs.tp_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
-    cost += Cs.tp_en_joint ? joint : 0.0;
-    cost += Cs.tp_en_self ? Cs.tp_self : 0.0;
-    cost += Cs.tp_en_reach ? reach : 0.0;
-    return cost;
-}
-
-template <int CK, bool EN>
-__device__ __forceinline__ double objective_terms(const DevCost &Cs, bool jl, int j, const double *M, double q, double qd, double sq,
-                                                  double cq, const CoopKin &kin, double E)
-{
-    if constexpr (CK == CK_TRACK_POINT) return track_point_terms(Cs, j, q, sq, cq, kin);
-    else return step_cost_terms<EN>(Cs, jl, M, q, qd, sq, cq, kin, E);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Stage the per-body table (geometry, inertia, axes, cost weights, lane masks) in LDS.
@@ -747,6 +628,46 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / fcost).
+// Step record stores (layout: kernels.hpp FR_NREC).  After a calculate(), the dummy lanes 12..15
+// write its row-uniform kinematics (two 16-byte stores: EE, arm mount, J v, J_a J_a^T but the last
+// entry); at the end of the step, lanes 0..11 write (q_j, qd_j) of the new state and lane 12 the
+// last J_a J_a^T entry with the tank energy.
+// register value the optimiser cannot trace back to a memory location (keeps the record selects
+// as v_cndmask instead of a dynamically indexed private copy of CoopKin)
+__device__ __forceinline__ double vreg(double x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ void store_kin(double *rp, int j, const CoopKin &kin)
+{
+    if (j < 12) return;
+    const int s = j - 12;
+    const double e0 = vreg(kin.ee[0]), e1 = vreg(kin.ee[1]), e2 = vreg(kin.ee[2]);
+    const double m0 = vreg(kin.am[0]), m1 = vreg(kin.am[1]), m2 = vreg(kin.am[2]);
+    const double l0 = vreg(kin.vl[0]), l1 = vreg(kin.vl[1]), l2 = vreg(kin.vl[2]);
+    const double k0 = vreg(kin.jj[0]), k1 = vreg(kin.jj[1]), k2 = vreg(kin.jj[2]), k3 = vreg(kin.jj[3]), k4 = vreg(kin.jj[4]);
+    const double a0 = (s == 0) ? e0 : (s == 1) ? e2 : (s == 2) ? m1 : l0;
+    const double a1 = (s == 0) ? e1 : (s == 1) ? m0 : (s == 2) ? m2 : l1;
+    *reinterpret_cast<double2 *>(rp + REC_EE + 2 * s) = double2{a0, a1};
+    if (s == 3) return;
+    const double b0 = (s == 0) ? l2 : (s == 1) ? k1 : k3;
+    const double b1 = (s == 0) ? k0 : (s == 1) ? k2 : k4;
+    *reinterpret_cast<double2 *>(rp + REC_VL + 2 + 2 * s) = double2{b0, b1};
+}
+__device__ __forceinline__ void store_state(double *rp, int j, double q, double qd, double jj5, double E)
+{
+    if (j > 12) return;
+    const bool st = j < 12;
+    *reinterpret_cast<double2 *>(rp + 2 * j + (st ? 0 : REC_JJ + 5 - 24)) = double2{st ? q : jj5, st ? qd : E};
+}
+static_assert(REC_EE == 24 && REC_AM == 27 && REC_VL == 30 && REC_JJ == 33 && REC_E == 39 && FR_NREC == 40, "record layout");
+
+// One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
+// row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / frec).  The
+// costs are not summed here: every step's record goes to HBM and fr_step_cost_kernel evaluates
+// the objective for all (rollout, step) pairs at once, a lane each, instead of 16 lanes of a row
+// repeating its row-uniform terms.
 template <int CK, bool EN, bool FROW>
 __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                           const double *Lmodel)
@@ -765,35 +686,34 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // FROW: the row after the last rollout is the previous update's filter() (optimal rollout)
     const bool frow = FROW && a.fcost != nullptr && lr == a.count;
     const bool live = lr < a.count || frow;
-    const bool opt_row = a.optimal || frow;   // no noise, no NaN stop (mppi.cpp:450-479)
+    if (!live) return;   // row-uniform: the row's lanes leave together (no DPP partner is lost)
+    const int H = a.H;
+    const bool opt_row = a.optimal || frow;   // no noise (mppi.cpp:450-479)
     const double *x0p = FROW && frow ? a.fx0 : a.x0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
-    const StepConst *stp = FROW && frow ? a.fsteps : a.steps;
-    const int64_t g = a.optimal ? -1 : a.begin + lr;
-    const int H = a.H;
+    double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_NREC;   // [rollout][step][FR_NREC]
     const bool jl = j < FR_NB;   // lane owns a body / control component
     const int jb = jl ? j : 0;
     const double *M = Lmodel + (jl ? j : FR_NB) * MB;
-    const DevCost &Cs = *a.cost;
     LaneConst L;
     L.is_rz = jl && FR_KIND[jb] == KIND_RZ;
     L.slot = jl ? j : FR_NB;
 
-    double q = live && jl ? x0p[jb] : 0.0;
-    double qd = live && jl ? x0p[FR_NB + jb] : 0.0;
-    double E = EN && live ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+    double q = jl ? x0p[jb] : 0.0;
+    double qd = jl ? x0p[FR_NB + jb] : 0.0;
+    double E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
     const double *grav = a.model->gravity;
     double sq, cq;
-    sincos(q, &sq, &cq);   // one sincos per lane and step: FK, base yaw, workspace
+    sincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
-    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, Cs, stp[0], kin, grav);   // set_state -> calculate() at (q0, v0)
+    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, grav);   // set_state -> calculate() at (q0, v0)
+    store_kin(rp, j, kin);
+    store_state(rp, j, q, qd, kin.jj[5], E);
 
-    // eps and U*_shifted of step k: loaded at the top of the step, first used after its cost
-    const bool sampled = !opt_row && live && jl;
+    // eps and U*_shifted of step k: loaded at the top of the step
+    const bool sampled = !opt_row && jl;
     const int64_t nstride = a.Rpad * FR_C;
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
-    double J = 0.0;
-    bool alive = true;
 #ifdef NO_EPS_PREFETCH
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[sampled ? (int64_t)k * nstride : 0];
@@ -809,12 +729,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #endif
         const double eps = sampled ? eps_l : 0.0;
         const double ub = jl ? ub_l : 0.0;
-        // cost at x_k with the kinematics cached by the previous calculate()
-#ifdef ABL_NOCOST
-        const double step_cost = 0.0;
-#else
-        const double step_cost = stp[k].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
-#endif
+        double *rn = rp + (k + 1) * FR_NREC;   // record of step k + 1
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
         {
@@ -826,8 +741,9 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         }
         Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
 #ifndef ABL_NOFK
-        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, Cs, stp[k + 1], kin, grav);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, grav);
 #endif
+        store_kin(rn, j, kin);
         double pe = 0.0;
 #ifdef ABL_NOABA
         const double qdd = Lw[L_TAU + j] * 1e-3;
@@ -841,29 +757,13 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             const double power = bsum<0, FR_NB>(tau_l * qd + kin.pw, 1.0) + a.dt * bsum<0, 6>(pe, 1.0);
             E = smax(0.0, E + power * a.dt);
         }
+        store_state(rn, j, q, qd, kin.jj[5], E);
         sincos(q, &sq, &cq);
-        if (!opt_row && isnan(step_cost)) {   // rollout cost NaN: stop (mppi.cpp:331-334)
-            J = NAN;
-            alive = false;
-            break;
-        }
-        J += step_cost;
     }
-    if (alive) {   // the final step's cost; its dynamics are never observed
-        const double step_cost = stp[H - 1].gamma_k * objective_terms<CK, EN>(Cs, jl, j, M, q, qd, sq, cq, kin, E);
-        J = (!opt_row && isnan(step_cost)) ? NAN : J + step_cost;
-    }
+    // the final step's dynamics are never observed (deviation 5)
 #ifdef COOP_TRACE
     if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    if (!live || j != 0) return;
-    if (FROW && frow) {   // skipped when the update threw (no filter(), mppi.cpp:170-176)
-        if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;
-    } else if (a.optimal) {
-        *a.cost_out = J;
-    } else {
-        a.cost_out[g] = J;
-    }
 }
 
 // WPB waves per workgroup.  The update's launch uses WPB = 5 with > 80 KB of LDS per workgroup, so a
@@ -880,7 +780,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     __shared__ double lds_kin[WPB * ROWS_PER_WAVE * KS];
     __shared__ double lds_scr[WPB * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
-    if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;
+    if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;   // no filter() (mppi.cpp:170-176)
     const int wv = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;

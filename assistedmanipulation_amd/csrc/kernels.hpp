@@ -39,6 +39,38 @@ struct FrRolloutArgs {
     const StepConst *fsteps;
     double *fcost;
     int64_t xbase, xrows;     // fr_coop_x_kernel: the fifth waves' rows [xbase, xbase + xrows)
+    // cooperative kernel: per-step records for the cost kernel, [count][H][FR_NREC] (rollout-major:
+    // one rollout's records are contiguous), and the folded / standalone filter() row's [H][FR_NREC]
+    double *rec, *frec;
+};
+
+// Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
+// the state x_k the cost is evaluated at and the kinematics of the calculate() before it.
+constexpr int FR_NREC = 40;
+constexpr int REC_QQD = 0;    // [2j], [2j + 1]: q_j, qd_j (j < 12)
+constexpr int REC_EE = 24;    // EE position (world)
+constexpr int REC_AM = 27;    // arm-mount position (world)
+constexpr int REC_VL = 30;    // EE linear frame velocity J v (bodies 0..9)
+constexpr int REC_JJ = 33;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11 12 22
+constexpr int REC_E = 39;     // energy tank level (enable_energy_limit)
+
+// The rollout costs from the records (fr_cost.hip): one wave per rollout, one lane per step, the
+// step costs summed in step order (the reference's J += cost, mppi.cpp:322-337).
+struct FrCostArgs {
+    const DevCost *cost;
+    const StepConst *steps;   // [H]
+    const double *rec;        // [count][H][FR_NREC]
+    int64_t begin, count;
+    double *cost_out;         // [R] (global index begin + row) or the optimal-cost scalar
+    const Status *status;
+    int H;
+    int optimal;
+    int cost_kind;
+    int energy;
+    // filter() row of the previous update (row == count): its records, constants and output
+    const double *frec;
+    const StepConst *fsteps;
+    double *fcost;
 };
 
 // sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
@@ -153,6 +185,7 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, bool *folded);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
+hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
 
 
 }  // namespace mppi_eng

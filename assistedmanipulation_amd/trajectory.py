@@ -395,9 +395,15 @@ class Trajectory:
                                                    st.ctypes.data_as(C.POINTER(C.c_int64))))
         return uu, tt, st
 
-    def kernel_times(self, wait=True):
+    def kernel_times(self, wait=True, detail=False):
         """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
-        wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's)."""
+        wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's).
+        detail=True appends [5], the rollout (dynamics) kernel alone ([1] also spans the cost kernel);
+        it implies wait=False."""
+        if detail:
+            out = (C.c_float * 6)()
+            self._check(self._L.mppi_kernel_times_detail(self._h, out, 6))
+            return list(out)
         out = (C.c_float * 5)()
         fn = self._L.mppi_kernel_times if wait else self._L.mppi_kernel_times_nowait
         self._check(fn(self._h, out))

@@ -29,13 +29,18 @@ HORISON = 0.64            # 64 steps at dt = 0.01
 KEEP_BEST = 20
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; the rollout is fp64 VALU
-# Algorithmic FLOPs of one rollout-step of the minimal arithmetic the kernel executes
+# Algorithmic FLOPs of one rollout-step of the minimal arithmetic the device executes
 # (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
-# FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins this value).
+# FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins these values):
+# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel.
 FLOPS_PER_ROLLOUT_STEP = 6518.0
-# Algorithmic HBM bytes of the rollout kernel per rollout-step: its eps column (C = 12 fp64) read
-# once (the sampler writes it, the gradient reduction reads it again: separate kernels).
-BYTES_PER_ROLLOUT_STEP = 96.0
+FLOPS_COST_PER_ROLLOUT_STEP = 690.0
+FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STEP
+# Algorithmic HBM bytes per rollout-step: the rollout kernel reads its eps column (C = 12 fp64)
+# once and writes one step record (FR_NREC = 40 fp64); the cost kernel reads the record back.
+BYTES_EPS_PER_ROLLOUT_STEP = 96.0
+BYTES_REC_PER_ROLLOUT_STEP = 320.0
+BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
 # HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
 # tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
 PMC_JSON = os.path.join(HERE, "profiles", "r01_pmc_rollout.json")
@@ -112,11 +117,11 @@ def main():
         j += 1
     if dist:
         dist.barrier()
-    kt = np.zeros(5)
+    kt = np.zeros(6)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         traj.update(x, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
-        kt += np.array(traj.kernel_times(wait=False))   # HIP-event times of this update
+        kt += np.array(traj.kernel_times(detail=True))   # HIP-event times of this update
         j += 1
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
@@ -130,14 +135,17 @@ def main():
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
     value = S_total * traj.H / (elapsed / args.steps)
-    rollout_ms = float(kt[1])
+    lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
+    dyn_ms = float(kt[1] if lane else kt[5])             # the rollout (dynamics) kernel alone
+    cost_ms = 0.0 if lane else float(kt[1] - kt[5])      # fr_step_cost_kernel
     traffic = None
     if os.path.exists(PMC_JSON) and world == 1 and args.samples_per_gpu == SAMPLES_PER_GPU:
         with open(PMC_JSON) as f:
             traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
-    flops = FLOPS_PER_ROLLOUT_STEP * count_local * traj.H
-    achieved_tflops = flops / (rollout_ms * 1e-3) / 1e12
+    units = count_local * traj.H
+    flops = (FLOPS_PER_ROLLOUT_STEP if lane else FLOPS_DYN_PER_ROLLOUT_STEP) * units
+    achieved_tflops = flops / (dyn_ms * 1e-3) / 1e12
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -159,13 +167,17 @@ def main():
                                "full AssistedManipulation cost stack%s" % (2 if world == 1 else 3, S_total, traj.H,
                                                                           ", sample-sharded over RCCL" if world > 1 else ""),
                    "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
-        "kernel_ms": {"sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
+        "kernel_ms": {"sample": kt[0], "rollout": kt[1], "rollout_dynamics": dyn_ms, "rollout_cost": cost_ms,
+                      "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
         "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
-                     "kernel": "fr_rollout_kernel" if os.environ.get("MPPI_FR_KERNEL") == "lane" else "fr_coop_kernel", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "traffic_unit": "bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
-                     "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP},
-        "hbm": {"rollout_algorithmic_GBs": BYTES_PER_ROLLOUT_STEP * count_local * traj.H / (rollout_ms * 1e-3) / 1e9,
+                     "kernel": "fr_rollout_kernel" if lane else "fr_coop_x_kernel", "achieved": achieved_tflops,
+                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
+                     "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
+                     "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP if lane else FLOPS_DYN_PER_ROLLOUT_STEP},
+        "hbm": {"rollout_algorithmic_GBs": (BYTES_EPS_PER_ROLLOUT_STEP if lane else BYTES_PER_ROLLOUT_STEP) * units
+                / (dyn_ms * 1e-3) / 1e9,
+                "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else None,
                 "peak_GBs": HBM_PEAK_GBS},
     }
     if not args.no_cpu_baseline:

@@ -365,6 +365,10 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
 /* As mppi_kernel_times without waiting for the side stream: [3] is the latest optimal rollout
  * already finished (possibly an earlier update's).  For timing loops that keep filter() overlapped. */
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5);
+/* The first n (<= 6) per-update times of mppi_kernel_times_nowait, where [5] is the rollout
+ * (dynamics) kernel alone: [1] spans it and the FrankaRidgeback cost kernel that sums the step
+ * costs from its records. */
+mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n);
 
 #ifdef __cplusplus
 }

@@ -1636,8 +1636,10 @@ double oracle_rollout(const mppi_frankaridgeback_desc *desc, const mppi_assisted
 // Algorithmic FLOPs of one rollout-step of the minimal arithmetic the device executes:
 // zero-bias ABA (a = M^-1 tau_u) + kinematics/Jacobian/frame velocity + full default cost +
 // integration.  Counted with a FLOP-counting scalar over `steps` steps from x0.
-double oracle_count_flops(const mppi_frankaridgeback_desc *desc, const mppi_assisted_manipulation_desc *cost,
-                          const double *x0, int64_t steps)
+// cost_part (optional): the FLOPs of that total spent in get_cost (the device's cost kernel; the
+// rest is the rollout kernel's FK, kinematics, ABA and integration).
+double oracle_count_flops_split(const mppi_frankaridgeback_desc *desc, const mppi_assisted_manipulation_desc *cost,
+                                const double *x0, int64_t steps, double *cost_part)
 {
     orc::Model<orc::CF> m;
     m.load(*desc);
@@ -1654,14 +1656,24 @@ double oracle_count_flops(const mppi_frankaridgeback_desc *desc, const mppi_assi
     orc::CF state[MPPI_FR_STATE];
     for (int i = 0; i < MPPI_FR_STATE; i++) state[i] = orc::CF(x0[i]);
     orc::FlopCount::flops = 0;
+    uint64_t in_cost = 0;
     for (int64_t k = 0; k < steps; k++) {
         orc::CF uu[12];
         for (int i = 0; i < 12; i++) uu[i] = orc::CF(0.1 * (double)((i * 7 + k) % 5 - 2));
+        const uint64_t f0 = orc::FlopCount::flops;
         c.get_cost(state, d, k);
+        in_cost += orc::FlopCount::flops - f0;
         const orc::CF *x = d.step(uu, orc::CF(0.01));
         for (int i = 0; i < MPPI_FR_STATE; i++) state[i] = x[i];
     }
+    if (cost_part) *cost_part = (double)in_cost / (double)steps;
     return (double)orc::FlopCount::flops / (double)steps;
+}
+
+double oracle_count_flops(const mppi_frankaridgeback_desc *desc, const mppi_assisted_manipulation_desc *cost,
+                          const double *x0, int64_t steps)
+{
+    return oracle_count_flops_split(desc, cost, x0, steps, nullptr);
 }
 
 // Savitzky-Golay weights (ComputeWeights(m, t, n, s)).

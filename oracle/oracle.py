@@ -67,6 +67,9 @@ def lib(path=None):
     L.oracle_rollout.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
                                  C.POINTER(abi.mppi_assisted_manipulation_desc), dp, dp, i64,
                                  C.c_double, C.c_double, dp, C.c_int, C.c_int, dp, dp]
+    L.oracle_count_flops_split.restype = C.c_double
+    L.oracle_count_flops_split.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
+                                           C.POINTER(abi.mppi_assisted_manipulation_desc), dp, C.c_int64, dp]
     L.oracle_count_flops.restype = C.c_double
     L.oracle_count_flops.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
                                      C.POINTER(abi.mppi_assisted_manipulation_desc), dp, i64]
@@ -119,6 +122,13 @@ def rollout(model, cost, x0, u_HxC, dt, t0=0.0, forecast=None, scalar=0, mode=0)
     total = lib().oracle_rollout(C.byref(model), C.byref(cost), _p(x0), _p(u), H, dt, t0,
                                  None if f is None else _p(f), scalar, mode, _p(sc), _p(xf))
     return total, sc, xf
+
+
+def count_flops_split(model, cost, x0, steps=64):
+    """(total, cost part) algorithmic FLOPs per rollout-step; total - cost is the rollout kernel's."""
+    part = C.c_double(0.0)
+    tot = lib().oracle_count_flops_split(C.byref(model), C.byref(cost), _p(x0), steps, C.byref(part))
+    return tot, part.value
 
 
 def count_flops(model, cost, x0, steps=64):

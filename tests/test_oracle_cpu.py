@@ -159,6 +159,8 @@ def test_flop_count_constant(model):
     import bench
     n = O.count_flops(model, O.default_cost(), am.huddled_state(), 64)
     assert n == bench.FLOPS_PER_ROLLOUT_STEP
+    tot, cost = O.count_flops_split(model, O.default_cost(), am.huddled_state(), 64)
+    assert tot == n and cost == bench.FLOPS_COST_PER_ROLLOUT_STEP
 
 
 def test_fp32_dynamics_diverge_fp64_do_not(model):

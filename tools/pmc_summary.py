@@ -9,7 +9,9 @@ def summarize(path):
     rows = list(csv.DictReader(open(path)))
     disp = collections.defaultdict(dict)
     for r in rows:
-        key = (r["Dispatch_Id"], r["Kernel_Name"].split("(")[0])
+        name = r["Kernel_Name"]
+        name = name[:name.rfind("(")] if name.endswith(")") else name   # drop the argument list
+        key = (r["Dispatch_Id"], name.replace("(anonymous namespace)::", ""))
         disp[key][r["Counter_Name"]] = float(r["Counter_Value"])
         disp[key]["_grid"] = int(r["Grid_Size"])
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
