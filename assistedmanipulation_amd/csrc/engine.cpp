@@ -45,11 +45,6 @@ struct mppi_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
-    // sample()'s stable order of this update's costs, ranked as soon as the costs are final
-    // (after the cost all-reduce) so it runs beside optimise() instead of on the next update's
-    // critical path
-    hipStream_t stream_rank = nullptr;
-    hipEvent_t ev_costs = nullptr, ev_rank = nullptr;
 
     hipEvent_t ev[6] = {};
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
@@ -60,6 +55,9 @@ struct mppi_handle {
     const StepConst *opt_steps = nullptr;   // the step constants its update used
     // sample, rollout (dynamics + cost kernels), reduce, optimal rollout, update, dynamics kernel
     float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
+    // HIP-event timing on the update path (mppi_set_timing): 0 none, 1 the rollout kernel alone
+    // ([5]), 2 every phase.  Each event record costs the stream a few microseconds between kernels.
+    int timing = 0;
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
     double dt = 0, gradient_step = 0, cost_scale = 0, gamma = 1;
@@ -109,7 +107,7 @@ struct mppi_handle {
     DevPointMass *d_pm = nullptr;
     StepConst *d_steps = nullptr;
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
-    double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr, *d_out = nullptr;
+    double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
@@ -122,9 +120,9 @@ struct mppi_handle {
     Status *d_status = nullptr;
     double *d_sg_w = nullptr, *d_sg_uu = nullptr, *d_sg_tt = nullptr, *d_sg_last = nullptr;
     int64_t *d_sg_start = nullptr;
-    double *h_out = nullptr;     // pinned [HC + 8]
+    double *h_out = nullptr;     // pinned [HC + 8], mapped: finish_kernel writes it over the bus
+    double *h_out_dev = nullptr; // its device address
     double *h_opt = nullptr;     // pinned: optimal cost copied back on the side stream
-    double *h_stage = nullptr;   // pinned staging for the state
     std::vector<void *> allocations;
     std::string err;
     // per-update phase state
@@ -482,9 +480,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     }
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
-    CREATE_TRY(hipStreamCreateWithFlags(&h->stream_rank, hipStreamNonBlocking));
-    CREATE_TRY(hipEventCreateWithFlags(&h->ev_costs, hipEventDisableTiming));
-    CREATE_TRY(hipEventCreateWithFlags(&h->ev_rank, hipEventDisableTiming));
     for (auto &e : h->ev) CREATE_TRY(hipEventCreate(&e));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_pub, hipEventDisableTiming));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
@@ -503,7 +498,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
     CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_NREC)));
-    CREATE_TRY(dalloc(h, &h->d_out, HC + 8));
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
@@ -519,8 +513,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         for (int64_t k = 0; k < h->H; k++) g[(size_t)k] = std::pow(h->gamma, (double)k);
         CREATE_TRY(hipMemcpy(h->d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
     }
-    CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocDefault));
-    CREATE_TRY(hipHostMalloc((void **)&h->h_stage, 64 * sizeof(double), hipHostMallocDefault));
+    CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    CREATE_TRY(hipHostGetDevicePointer((void **)&h->h_out_dev, h->h_out, 0));
     CREATE_TRY(hipHostMalloc((void **)&h->h_opt, 8 * sizeof(double), hipHostMallocDefault));
     h->h_opt[0] = 0.0;
     CREATE_TRY(hipMemcpy(h->d_T, h->T.data(), h->T.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -657,8 +651,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     // the first update's order: every previous cost is 0 (mppi.cpp:222-231: identity).  The
     // zero-fills above run on the null stream, which the non-blocking streams do not wait for.
     CREATE_TRY(hipDeviceSynchronize());
-    CREATE_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream_rank));
-    CREATE_TRY(hipEventRecord(h->ev_rank, h->stream_rank));
+    CREATE_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
     if (!h->trace_path.empty()) CREATE_TRY(dalloc(h, &h->d_trace, (size_t)(4 * (h->R / 4 + 2))));
 #undef CREATE_TRY
     *out = h;
@@ -671,20 +664,15 @@ void mppi_destroy(mppi_handle *h)
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
-    if (h->stream_rank) (void)hipStreamSynchronize(h->stream_rank);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
-    if (h->h_stage) (void)hipHostFree(h->h_stage);
     if (h->h_opt) (void)hipHostFree(h->h_opt);
     if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
     if (h->ev_dyn) (void)hipEventDestroy(h->ev_dyn);
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
-    if (h->ev_costs) (void)hipEventDestroy(h->ev_costs);
-    if (h->ev_rank) (void)hipEventDestroy(h->ev_rank);
-    if (h->stream_rank) (void)hipStreamDestroy(h->stream_rank);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1048,9 +1036,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
     h->rollout_time = time;
-    std::memcpy(h->h_stage, state, (size_t)h->X * sizeof(double));
-    HIP_TRY(hipEventRecord(h->ev[0], h->stream));
-    HIP_TRY(hipMemcpyAsync(h->d_x0, h->h_stage, (size_t)h->X * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[0], h->stream));
     if (h->fc.type != FC_NONE) {   // this update's forecast samples, t0 + k dt (mppi.cpp:326)
         h->d_steps = h->d_steps_buf[(h->update_count + 1) & 1];   // the previous filter() reads the other
         HIP_TRY(launch_forecast_steps(forecast_args(h), step_params(h), h->d_gamma, (int)h->H, time, h->dt, h->d_steps, h->stream));
@@ -1083,8 +1069,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         if (need) HIP_TRY(hipMemcpy(h->d_inj, h->inj_pending.data(), need * sizeof(double), hipMemcpyHostToDevice));
         h->inj_pending.erase(h->inj_pending.begin(), h->inj_pending.begin() + (long)need);
     }
-    // the stable order of the previous costs, ranked beside the previous optimise() (phase 2)
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_rank, 0));
+    // the stable order of the previous costs was ranked behind the previous publish (phase 3)
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
@@ -1102,9 +1087,12 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         sa.Rpad = h->Rpad;
         sa.H = (int)h->H;
         sa.C = (int)h->C;
+        std::memcpy(sa.x0v, state, (size_t)h->X * sizeof(double));   // the state rides in the launch
+        sa.x0_out = h->d_x0;
+        sa.X = (int)h->X;
         HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
     }
-    HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         FrRolloutArgs a{};
         a.model = h->d_model;
@@ -1138,16 +1126,15 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         bool folded = false;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, &folded));
-            HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+            if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
             HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
-            HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+            if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
         }
-        if (folded) {   // the optimal cost is ready with this update's rollouts
-            HIP_TRY(hipMemcpyAsync(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-            HIP_TRY(hipEventRecord(h->ev_opt_done, h->stream));
+        if (folded) {   // the optimal cost is ready with this update's rollouts; phase 3's host block
+                        // carries it back (finish_kernel copies d_opt), on the same stream
             h->kernel_ms[3] = 0.0f;   // timed inside the rollout launch
             h->opt_state = mppi_handle::OPT_FOLDED;
         }
@@ -1166,9 +1153,9 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.H = (int)h->H;
         a.optimal = 0;
         HIP_TRY(launch_pm_rollout(a, h->stream));
-        HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+        if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
     }
-    HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     h->updated_once = true;
     h->phase_open = true;
     return MPPI_OK;
@@ -1178,11 +1165,6 @@ mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
-    // the costs are final here (all-reduced when sharded): rank them for the next sample()
-    HIP_TRY(hipEventRecord(h->ev_costs, h->stream));
-    HIP_TRY(hipStreamWaitEvent(h->stream_rank, h->ev_costs, 0));
-    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream_rank));
-    HIP_TRY(hipEventRecord(h->ev_rank, h->stream_rank));
     HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
@@ -1221,11 +1203,12 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     f.sg_last_trim = h->d_sg_last;
     f.U = h->d_U;
     f.opt_cost = h->d_opt;
-    f.out = h->d_out;
+    f.out = h->h_out_dev;   // the host block, written in place (no copy launch behind the finish)
+    f.x0 = h->d_x0;
+    f.x0_opt = h->d_x0_opt;
+    f.X = (int)h->X;
     HIP_TRY(launch_finish(f, h->stream));
-    HIP_TRY(hipEventRecord(h->ev[3], h->stream));
-    HIP_TRY(hipMemcpyAsync(h->d_x0_opt, h->d_x0, (size_t)h->X * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)(HC + 8) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
     // filter(): cost of the published U* (mppi.cpp:450-479).  With the cooperative kernel it rides
     // in the next update's remainder launch (it then shares a SIMD with rollouts 0 and 1 instead of
@@ -1236,12 +1219,22 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         mppi_status st = launch_filter_standalone(h);
         if (st != MPPI_OK) return st;
     }
-    HIP_TRY(hipEventRecord(h->ev[5], h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[5], h->stream));
+    // sample()'s stable order of this update's costs (final here: all-reduced when sharded), for
+    // the next update.  On the engine stream behind the published block, it runs while the host
+    // takes the result and comes back with the next state.
+    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
+    // wait for the published block by polling its event: a blocking synchronize sleeps the thread
+    // and the wake-up sat on the update's critical path (the GPU idles until the next update)
+    hipError_t q;
+    while ((q = hipEventQuery(h->timing >= 2 ? h->ev[5] : h->ev_pub)) == hipErrorNotReady) {}
+    HIP_TRY(q);
     h->phase_open = false;
-    for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
-    (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
-    (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
+    if (h->timing >= 2) {
+        for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
+        (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
+    }
+    if (h->timing >= 1) (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
     if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
@@ -1338,6 +1331,10 @@ static mppi_status wait_optimal(mppi_handle *h)
     if (h->opt_state == mppi_handle::OPT_PENDING) {
         mppi_status st = launch_filter_standalone(h);
         if (st != MPPI_OK) return st;
+    }
+    if (h->opt_state == mppi_handle::OPT_FOLDED) {   // read mid-update: it rode in the rollout launch
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipMemcpy(h->h_opt, h->d_opt, sizeof(double), hipMemcpyDeviceToHost));
     }
     if (h->opt_state != mppi_handle::OPT_LAUNCHED && h->opt_state != mppi_handle::OPT_FOLDED) return MPPI_OK;
     HIP_TRY(hipEventSynchronize(h->ev_opt_done));
@@ -1437,6 +1434,14 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
 {
     return mppi_kernel_times_detail(h, ms5, 5);
+}
+
+mppi_status mppi_set_timing(mppi_handle *h, int level)
+{
+    if (!h || level < 0 || level > 2) return MPPI_ERR_INVALID;
+    h->timing = level;
+    for (float &m : h->kernel_ms) m = 0.0f;
+    return MPPI_OK;
 }
 
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)

@@ -628,10 +628,10 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / fcost).
-// Step record stores (layout: kernels.hpp FR_NREC).  After a calculate(), the dummy lanes 12..15
-// write its row-uniform kinematics (two 16-byte stores: EE, arm mount, J v, J_a J_a^T but the last
-// entry); at the end of the step, lanes 0..11 write (q_j, qd_j) of the new state and lane 12 the
-// last J_a J_a^T entry with the tank energy.
+// Step record store (layout: kernels.hpp FR_NREC), two 16-byte stores per lane with the whole row
+// active (no branch splits the step's basic block): lanes 0..11 write (q_j, qd_j) and lanes
+// 12..15 the first eight kinematic values, then lane j writes pair j mod 4 of the remaining eight
+// (lanes 4..15 repeat lanes 0..3: same address, same value).
 // register value the optimiser cannot trace back to a memory location (keeps the record selects
 // as v_cndmask instead of a dynamically indexed private copy of CoopKin)
 __device__ __forceinline__ double vreg(double x)
@@ -639,27 +639,23 @@ __device__ __forceinline__ double vreg(double x)
     asm volatile("" : "+v"(x));
     return x;
 }
-__device__ __forceinline__ void store_kin(double *rp, int j, const CoopKin &kin)
+__device__ __forceinline__ void store_record(double *rp, int j, double q, double qd, const CoopKin &kin, double E)
 {
-    if (j < 12) return;
-    const int s = j - 12;
+#ifdef ABL_NOREC
+    return;
+#endif
     const double e0 = vreg(kin.ee[0]), e1 = vreg(kin.ee[1]), e2 = vreg(kin.ee[2]);
     const double m0 = vreg(kin.am[0]), m1 = vreg(kin.am[1]), m2 = vreg(kin.am[2]);
     const double l0 = vreg(kin.vl[0]), l1 = vreg(kin.vl[1]), l2 = vreg(kin.vl[2]);
-    const double k0 = vreg(kin.jj[0]), k1 = vreg(kin.jj[1]), k2 = vreg(kin.jj[2]), k3 = vreg(kin.jj[3]), k4 = vreg(kin.jj[4]);
-    const double a0 = (s == 0) ? e0 : (s == 1) ? e2 : (s == 2) ? m1 : l0;
-    const double a1 = (s == 0) ? e1 : (s == 1) ? m0 : (s == 2) ? m2 : l1;
-    *reinterpret_cast<double2 *>(rp + REC_EE + 2 * s) = double2{a0, a1};
-    if (s == 3) return;
-    const double b0 = (s == 0) ? l2 : (s == 1) ? k1 : k3;
-    const double b1 = (s == 0) ? k0 : (s == 1) ? k2 : k4;
+    const double k0 = vreg(kin.jj[0]), k1 = vreg(kin.jj[1]), k2 = vreg(kin.jj[2]);
+    const double k3 = vreg(kin.jj[3]), k4 = vreg(kin.jj[4]), k5 = vreg(kin.jj[5]);
+    const double a0 = (j < 12) ? q : (j == 12) ? e0 : (j == 13) ? e2 : (j == 14) ? m1 : l0;
+    const double a1 = (j < 12) ? qd : (j == 12) ? e1 : (j == 13) ? m0 : (j == 14) ? m2 : l1;
+    *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
+    const int s = j & 3;
+    const double b0 = (s == 0) ? l2 : (s == 1) ? k1 : (s == 2) ? k3 : k5;
+    const double b1 = (s == 0) ? k0 : (s == 1) ? k2 : (s == 2) ? k4 : E;
     *reinterpret_cast<double2 *>(rp + REC_VL + 2 + 2 * s) = double2{b0, b1};
-}
-__device__ __forceinline__ void store_state(double *rp, int j, double q, double qd, double jj5, double E)
-{
-    if (j > 12) return;
-    const bool st = j < 12;
-    *reinterpret_cast<double2 *>(rp + 2 * j + (st ? 0 : REC_JJ + 5 - 24)) = double2{st ? q : jj5, st ? qd : E};
 }
 static_assert(REC_EE == 24 && REC_AM == 27 && REC_VL == 30 && REC_JJ == 33 && REC_E == 39 && FR_NREC == 40, "record layout");
 
@@ -707,28 +703,35 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     sincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, grav);   // set_state -> calculate() at (q0, v0)
-    store_kin(rp, j, kin);
-    store_state(rp, j, q, qd, kin.jj[5], E);
 
     // eps and U*_shifted of step k: loaded at the top of the step
     const bool sampled = !opt_row && jl;
-    const int64_t nstride = a.Rpad * FR_C;
+    int smask = sampled ? -1 : 0, jmask = jl ? -1 : 0;
+    asm volatile("" : "+v"(smask), "+v"(jmask));   // opaque: kept as data, not folded into control flow
+    int64_t nstride = sampled ? a.Rpad * FR_C : 0;   // unsampled rows re-read their first element
+    asm volatile("" : "+v"(nstride));
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
 #ifdef NO_EPS_PREFETCH
+    store_record(rp, j, q, qd, kin, E);
     for (int k = 0; k < H - 1; k++) {
-        const double eps_l = np[sampled ? (int64_t)k * nstride : 0];
+        const double eps_l = np[(int64_t)k * nstride];
         const double ub_l = Up[k * FR_C + jb];
 #else
     // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
     // whose latency a single wave per SIMD cannot hide within one step
+    // (issued before the first record store: the loop header then waits for the loads alone,
+    // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[0], ub_n = Up[jb];
+    store_record(rp, j, q, qd, kin, E);
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = eps_n, ub_l = ub_n;
-        eps_n = np[sampled ? (int64_t)(k + 1) * nstride : 0];
+        eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[(k + 1) * FR_C + jb];
 #endif
-        const double eps = sampled ? eps_l : 0.0;
-        const double ub = jl ? ub_l : 0.0;
+        // bit masks, not selects: a select here became a branch around the eps use, and the
+        // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
+        const double eps = __hiloint2double(__double2hiint(eps_l) & smask, __double2loint(eps_l) & smask);
+        const double ub = __hiloint2double(__double2hiint(ub_l) & jmask, __double2loint(ub_l) & jmask);
         double *rn = rp + (k + 1) * FR_NREC;   // record of step k + 1
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
         const double u = ub + eps;
@@ -743,7 +746,6 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #ifndef ABL_NOFK
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, grav);
 #endif
-        store_kin(rn, j, kin);
         double pe = 0.0;
 #ifdef ABL_NOABA
         const double qdd = Lw[L_TAU + j] * 1e-3;
@@ -757,7 +759,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             const double power = bsum<0, FR_NB>(tau_l * qd + kin.pw, 1.0) + a.dt * bsum<0, 6>(pe, 1.0);
             E = smax(0.0, E + power * a.dt);
         }
-        store_state(rn, j, q, qd, kin.jj[5], E);
+        store_record(rn, j, q, qd, kin, E);
         sincos(q, &sq, &cq);
     }
     // the final step's dynamics are never observed (deviation 5)

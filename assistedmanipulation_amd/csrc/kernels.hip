@@ -607,6 +607,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
 {
     constexpr int NB = DIAG ? (C + 3) / 4 : 1;   // thread pieces per (step, rollout)
     const int k = blockIdx.y;
+    if (blockIdx.x == 0 && k == 0 && (int)threadIdx.x < a.X) a.x0_out[threadIdx.x] = a.x0v[threadIdx.x];
     if (blockIdx.x == 0 && a.sp.shift_by > 0 && (int)threadIdx.x < C) {
         const int c = threadIdx.x;
         const int64_t sh = a.sp.shift_by, kept = a.sp.shifted;
@@ -1028,6 +1029,7 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
         if (ok) a.U[t] = v;
         a.out[t] = v;
     }
+    if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
     if (threadIdx.x == 0) {
         a.status_w->sg_error = sg_err;
         a.out[HC + 0] = *a.opt_cost;

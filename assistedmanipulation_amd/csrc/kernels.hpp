@@ -73,6 +73,9 @@ struct FrCostArgs {
     double *fcost;
 };
 
+constexpr int MAX_X = 32;   // state dimension bound of the by-value state (FrankaRidgeback 31)
+static_assert(FR_X <= MAX_X, "state dimension");
+
 // sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
 struct SampleArgs {
     const int *rank;          // [R] stable-order rank of rollouts 2..R-1
@@ -85,6 +88,11 @@ struct SampleArgs {
     SampleParams sp;
     int64_t begin, count, Rpad;
     int H, C;
+    // the update's state, passed by value (no host-to-device copy on the update path): block
+    // (0, 0) writes it to x0_out for the rollout kernels
+    double x0v[MAX_X];
+    double *x0_out;
+    int X;
 };
 
 struct PmRolloutArgs {
@@ -124,6 +132,10 @@ struct FinishArgs {
     double *U;
     const double *opt_cost;
     double *out;
+    // filter()'s state: the update's x0 copied for the optimal rollout that runs after it
+    const double *x0;
+    double *x0_opt;
+    int X;
 };
 
 // stable rank of rollouts 2..S+1 by cost; `sorted` is scratch of rank_scratch(S) keys

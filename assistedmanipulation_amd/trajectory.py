@@ -395,6 +395,11 @@ class Trajectory:
                                                    st.ctypes.data_as(C.POINTER(C.c_int64))))
         return uu, tt, st
 
+    def set_timing(self, level):
+        """HIP-event timing of the update path: 0 none (default), 1 the rollout kernel alone,
+        2 every phase (mppi_set_timing)."""
+        self._check(self._L.mppi_set_timing(self._h, int(level)))
+
     def kernel_times(self, wait=True, detail=False):
         """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
         wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's).

@@ -117,16 +117,25 @@ def main():
         j += 1
     if dist:
         dist.barrier()
-    kt = np.zeros(6)
+    traj.set_timing(1)   # HIP events around the rollout kernel only (each event delays the stream)
+    dyn = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         traj.update(x, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
-        kt += np.array(traj.kernel_times(detail=True))   # HIP-event times of this update
+        dyn += traj.kernel_times(detail=True)[5]   # the rollout kernel's HIP-event time, this update
         j += 1
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
-    kt /= args.steps
-    kt[3] = traj.kernel_times()[3]   # the optimal rollout (side stream) of the last timed update
+    # the per-phase breakdown from a few further updates with every event recorded (untimed)
+    traj.set_timing(2)
+    kt = np.zeros(6)
+    nb = 5
+    for _ in range(nb):
+        traj.update(x, 0.05 * j)
+        kt += np.array(traj.kernel_times(detail=True))
+        j += 1
+    kt /= nb
+    kt[3] = traj.kernel_times()[3]   # the optimal rollout (side stream) of the last update
     if dist:
         dist.barrier()
         import torch
@@ -136,8 +145,8 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = S_total * traj.H / (elapsed / args.steps)
     lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
-    dyn_ms = float(kt[1] if lane else kt[5])             # the rollout (dynamics) kernel alone
-    cost_ms = 0.0 if lane else float(kt[1] - kt[5])      # fr_step_cost_kernel
+    dyn_ms = dyn / args.steps                             # the rollout (dynamics) kernel alone, timed loop
+    cost_ms = 0.0 if lane else float(kt[1] - kt[5])      # fr_step_cost_kernel (breakdown pass)
     traffic = None
     if os.path.exists(PMC_JSON) and world == 1 and args.samples_per_gpu == SAMPLES_PER_GPU:
         with open(PMC_JSON) as f:
@@ -167,8 +176,8 @@ def main():
                                "full AssistedManipulation cost stack%s" % (2 if world == 1 else 3, S_total, traj.H,
                                                                           ", sample-sharded over RCCL" if world > 1 else ""),
                    "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
-        "kernel_ms": {"sample": kt[0], "rollout": kt[1], "rollout_dynamics": dyn_ms, "rollout_cost": cost_ms,
-                      "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]},
+        "kernel_ms": {"rollout_dynamics": dyn_ms, "rollout_cost": cost_ms, "breakdown_untimed": {
+                      "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]}},
         "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
                      "kernel": "fr_rollout_kernel" if lane else "fr_coop_x_kernel", "achieved": achieved_tflops,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,

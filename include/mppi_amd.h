@@ -359,7 +359,11 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
  * dimension the value and time buffers (C x (H + 2w + 1), row per dimension) and start index. */
 mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64_t *start_idx);
 
-/* Kernel timing of the last update (HIP events on the engine stream), milliseconds:
+/* HIP-event timing of the update path: 0 (default) none, 1 the rollout kernel alone (slot [5] of
+ * mppi_kernel_times_detail), 2 every slot.  Each event recorded between two kernels delays the
+ * second by a few microseconds, so timing is off unless asked for. */
+mppi_status mppi_set_timing(mppi_handle *h, int level);
+/* Kernel timing of the last update (HIP events on the engine stream, timing level 2), milliseconds:
  * [0] sample/rank, [1] rollout, [2] weight-reduce, [3] optimal rollout, [4] whole update. */
 mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
 /* As mppi_kernel_times without waiting for the side stream: [3] is the latest optimal rollout
