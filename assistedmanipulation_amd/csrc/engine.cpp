@@ -1161,24 +1161,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     return MPPI_OK;
 }
 
-mppi_status mppi_update_phase2(mppi_handle *h)
+static FinishArgs finish_args(mppi_handle *h)
 {
-    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
-    // sharded: the partial gradient is summed here and all-reduced before phase 3
-    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
-                            h->d_gsplit, h->d_gpart, h->world > 1, h->stream));
-    return MPPI_OK;
-}
-
-mppi_status mppi_update_phase3(mppi_handle *h)
-{
-    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
-    HIP_TRY(hipSetDevice(h->device));
-    const int HC = (int)(h->H * h->C);
-    // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     FinishArgs f{};
     f.status = h->d_status;
     f.status_w = h->d_status;
@@ -1207,7 +1191,30 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     f.x0 = h->d_x0;
     f.x0_opt = h->d_x0_opt;
     f.X = (int)h->X;
-    HIP_TRY(launch_finish(f, h->stream));
+    f.rank_zero = h->d_rank;
+    f.rank_n = h->S <= RANK_TILED_MAX ? h->R : 0;
+    return f;
+}
+
+mppi_status mppi_update_phase2(mppi_handle *h)
+{
+    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
+    // sharded: the partial gradient is summed here and all-reduced before phase 3
+    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
+                            h->d_gsplit, h->d_gpart, h->world > 1, h->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_update_phase3(mppi_handle *h)
+{
+    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    const int HC = (int)(h->H * h->C);
+    // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+    HIP_TRY(launch_finish(finish_args(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
     // filter(): cost of the published U* (mppi.cpp:450-479).  With the cooperative kernel it rides

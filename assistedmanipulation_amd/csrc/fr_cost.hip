@@ -179,9 +179,18 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const double2 *src = rec + (int64_t)base * NREC2;
-        for (int t = lane; t < n * NREC2; t += 64) {
-            const int r = t / NREC2;
-            L[r * LREC2 + (t - r * NREC2)] = src[t];
+        {   // all NREC2 loads in flight before the first LDS store
+            double2 v[NREC2];
+#pragma unroll
+            for (int i = 0; i < NREC2; i++) {
+                const int t = lane + 64 * i;
+                v[i] = (t < n * NREC2) ? src[t] : double2{0.0, 0.0};
+            }
+#pragma unroll
+            for (int i = 0; i < NREC2; i++) {
+                const int t = lane + 64 * i, r = t / NREC2;
+                L[r * LREC2 + (t - r * NREC2)] = v[i];
+            }
         }
         __syncthreads();
         double c = 0.0;

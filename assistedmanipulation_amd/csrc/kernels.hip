@@ -596,6 +596,35 @@ __global__ __launch_bounds__(RANK_T) void rank_merge_kernel(const double *__rest
 }
 
 
+// Small S (<= RANK_TILED_MAX): all-pairs in tiles, one launch.  Grid (ceil(S/256), ceil(S/256)):
+// block (x, y) ranks its 256 rollouts against the 256 of tile y staged in LDS; off the diagonal
+// tile the index tie-break is block-uniform, so one compare per pair.  rank[] is zeroed by the
+// finish kernel that precedes this launch on the engine stream.
+__global__ __launch_bounds__(RANK_T) void rank_tiled_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
+{
+    __shared__ uint64_t kj[RANK_T];
+    const int64_t i = (int64_t)blockIdx.x * RANK_T + threadIdx.x;
+    const int64_t j0 = (int64_t)blockIdx.y * RANK_T;
+    const int64_t jl = j0 + threadIdx.x;
+    kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
+    __syncthreads();
+    if (i >= S) return;
+    const uint64_t ki = cost_key(cost[2 + i]);
+    const int jn = (int)((S - j0) < RANK_T ? (S - j0) : RANK_T);
+    int cnt = 0;
+    if (blockIdx.y < blockIdx.x) {          // every j < i: equal keys count
+#pragma unroll 8
+        for (int t = 0; t < jn; t++) cnt += (kj[t] <= ki) ? 1 : 0;
+    } else if (blockIdx.y > blockIdx.x) {   // every j > i
+#pragma unroll 8
+        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki) ? 1 : 0;
+    } else {
+        const int il = threadIdx.x;
+        for (int t = 0; t < jn; t++) cnt += (kj[t] < ki || (kj[t] == ki && t < il)) ? 1 : 0;
+    }
+    if (cnt) atomicAdd(&rank[2 + i], cnt);
+}
+
 // sample(): eps column k of local rollout lr (mppi.cpp:242-269).  Rollout 0 is the zero-noise
 // rollout; rollout 1 carries -U*; kept rollouts shift the previous update's eps; the rest draw.
 // Diagonal noise transform: one thread per (step, rollout, Philox block of 4 components), so
@@ -932,9 +961,8 @@ __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, i
 
 // U* += step * gradient; Savitzky-Golay; clamp (mppi.cpp:421-447).  One workgroup.
 // SG: one thread per control dimension runs its MovingExtendedWindow (filter.cpp:19-116).
-__global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
+__device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
 {
-    __shared__ int sg_err;
     const Status &stt = *a.status;
     const int HC = a.H * a.C;
     if (threadIdx.x == 0) sg_err = 0;
@@ -1030,6 +1058,7 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
         a.out[t] = v;
     }
     if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
+    for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
         a.status_w->sg_error = sg_err;
         a.out[HC + 0] = *a.opt_cost;
@@ -1039,6 +1068,12 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
     }
+}
+
+__global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
+{
+    __shared__ int sg_err;
+    finish_block(a, sg_err);
 }
 
 
@@ -1051,6 +1086,11 @@ namespace mppi_eng {
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s)
 {
     if (S <= 0) return hipSuccess;
+    if (S <= RANK_TILED_MAX) {   // rank[] zeroed by the finish kernel (or at create)
+        const unsigned nb = (unsigned)((S + RANK_T - 1) / RANK_T);
+        hipLaunchKernelGGL(rank_tiled_kernel, dim3(nb, nb), dim3(RANK_T), 0, s, cost, S, rank);
+        return hipGetLastError();
+    }
     const unsigned nch = (unsigned)((S + RANK_T - 1) / RANK_T);
     hipLaunchKernelGGL(rank_chunk_kernel, dim3(nch), dim3(RANK_T), 0, s, cost, S, rank, sorted);
     if (nch > 1)

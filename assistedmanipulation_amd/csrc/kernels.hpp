@@ -136,7 +136,11 @@ struct FinishArgs {
     const double *x0;
     double *x0_opt;
     int X;
+    // the next rank launch accumulates into rank[]: zeroed here when it is the tiled kernel
+    int *rank_zero;
+    int64_t rank_n;
 };
+
 
 // stable rank of rollouts 2..S+1 by cost; `sorted` is scratch of rank_scratch(S) keys
 // ---- wrench forecast on the device (forecast.hip) --------------------------------------------
@@ -181,6 +185,9 @@ hipError_t launch_forecast_steps(const ForecastArgs &f, const StepParams &p, con
 hipError_t launch_kalman_observe(DevKalman *kf, double *pred, const KalmanObserve &a, hipStream_t s);
 hipError_t launch_forecast_eval(const ForecastArgs &f, double time, double *out, hipStream_t s);
 
+// stable rank of rollouts 2..S+1 by cost: one all-pairs tiled launch up to RANK_TILED_MAX (rank[]
+// must be zero: finish_kernel clears it), chunk sort + merge beyond
+constexpr int64_t RANK_TILED_MAX = 8192;
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s);
 inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
