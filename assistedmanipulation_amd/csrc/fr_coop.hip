@@ -59,17 +59,21 @@ constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 stor
 // Row strides are 128 B modulo 256 B: ds_read_b64 serves lanes 0..31 (rows 0, 1) and 32..63 in
 // one bank cycle each with bank (a/4) mod 64, so rows 0/1 (2/3) must sit half a bank sweep apart.
 constexpr int L_I = 0;
-constexpr int L_S = 274;                    // 16-byte aligned
-constexpr int LDS_KIN = 368;                // >= L_S + NSLOT * 6, = 16 (mod 32) doubles
-constexpr int L_F = 352;                    // energy tank: spatial force f of each body slot
-constexpr int LDS_KIN_EN = 432;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
+constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x ROW) over L_I
+constexpr int L_TP = L_COL + 16 * ROW;      // no tank: the solved right-hand side (12)
+constexpr int L_S = 274;                    // 16-byte aligned; per slot S (6), qd, pad
+constexpr int S_STR = 8;
+constexpr int LDS_KIN = 400;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
+constexpr int L_F = 378;                    // energy tank: spatial force f of each body slot
+constexpr int LDS_KIN_EN = 464;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
 constexpr int L_U = 0;
 constexpr int L_DU = L_U + FR_NB * ROW;
 constexpr int L_QDD = L_DU + FR_NB * 2;
 constexpr int L_TAU = L_QDD + ROW;
 constexpr int LDS_SCR = 272;                // >= L_TAU + ROW, = 16 (mod 32) doubles
-static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * 6 <= LDS_KIN && L_TAU + ROW <= LDS_SCR, "LDS row layout");
-static_assert(L_S + NSLOT * 6 <= L_F && L_F + NSLOT * 6 <= LDS_KIN_EN, "LDS row layout (energy)");
+static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * S_STR <= LDS_KIN && L_TAU + ROW <= LDS_SCR, "LDS row layout");
+static_assert(L_TP + 12 <= L_S && L_TP % 2 == 0, "LDS row layout (mass-matrix block)");
+static_assert(L_S + NSLOT * S_STR <= L_F && L_F + NSLOT * 6 <= LDS_KIN_EN && L_F % 2 == 0, "LDS row layout (energy)");
 static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16, "row stride bank offset");
 
 // Per-block body table (doubles per body): scan placement R p (body 11: relative to body 10),
@@ -97,6 +101,8 @@ template <int N>
 __device__ __forceinline__ double bcast(double x) { return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + N, 0xF, 0xF, true); }
 template <int S>
 __device__ __forceinline__ double shr(double x) { return dmov<0x110 + S>(x); }     // row_shr:S
+template <int S>
+__device__ __forceinline__ double shl(double x) { return dmov<0x100 + S>(x); }     // row_shl:S
 
 // acc + sum_{r<6} x[lane r] * y[r]: six v_fmac_f64_dpp row_newbcast:r (broadcast and multiply-add
 // in one instruction; the compiler does not form 64-bit DPP FMAs).  The leading s_nop covers the
@@ -116,6 +122,17 @@ __device__ __forceinline__ double bfma6(double x, const double *y, double acc)
         : "v"(x), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]));
     return acc;
 }
+#ifdef PHASE_TRACE
+// diagnostics: shader-clock stamp once `dep` has been computed and the wave's LDS ops are done
+__device__ __forceinline__ uint64_t stamp(double dep)
+{
+    uint64_t t;
+    uint32_t tmp;
+    asm volatile("v_readfirstlane_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(t), "=s"(tmp) : "v"(__double2loint(dep)) : "memory");
+    return t;
+}
+#endif
 // c[k] += x[lane k] * y for k < 6 (the rank-1 update of the articulated inertia rows)
 __device__ __forceinline__ void bfma6_rank1(double x, double y, double *c)
 {
@@ -215,6 +232,19 @@ __device__ __forceinline__ void bfma6_pair(double U, double P, const double *S, 
     D = d0;
     sp = p0;
 }
+// bfma6_pair as four chains of three (D and sp each split at row 3)
+__device__ __forceinline__ void bfma6_quad(double U, double P, const double *S, double &D, double &sp)
+{
+    double d0 = 0.0, p0 = 0.0, d1 = 0.0, p1 = 0.0;
+    asm("s_nop 1\n\t"
+        DPPF("%0", "%4", "%6", 0) DPPF("%1", "%5", "%6", 0) DPPF("%2", "%4", "%9", 3) DPPF("%3", "%5", "%9", 3)
+        DPPF("%0", "%4", "%7", 1) DPPF("%1", "%5", "%7", 1) DPPF("%2", "%4", "%10", 4) DPPF("%3", "%5", "%10", 4)
+        DPPF("%0", "%4", "%8", 2) DPPF("%1", "%5", "%8", 2) DPPF("%2", "%4", "%11", 5) DPPF("%3", "%5", "%11", 5)
+        : "+&v"(d0), "+&v"(p0), "+&v"(d1), "+&v"(p1)
+        : "v"(U), "v"(P), "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]));
+    D = d0 + d1;
+    sp = p0 + p1;
+}
 // sum over lanes 0..5 of x: two chains (lanes 0..2, 3..5)
 __device__ __forceinline__ double bsum6_split(double x, double one)
 {
@@ -243,24 +273,7 @@ __device__ __forceinline__ void bsum12_pair(double x, double y, double one, doub
     sx = a0 + a1;
     sy = b0 + b1;
 }
-// The EE frame velocity J v (three sums over lanes 0..9) and J_a J_a^T (six sums over lanes 3..9):
-// nine chains round-robin.
-__device__ __forceinline__ void kin_sums(const double *v, const double *m, double one, double *vl, double *jj)
-{
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0, b4 = 0.0, b5 = 0.0;
-#define KV(l) DPPF("%0", "%9", "%18", l) DPPF("%1", "%10", "%18", l) DPPF("%2", "%11", "%18", l)
-#define KJ(l) DPPF("%3", "%12", "%18", l) DPPF("%4", "%13", "%18", l) DPPF("%5", "%14", "%18", l) \
-              DPPF("%6", "%15", "%18", l) DPPF("%7", "%16", "%18", l) DPPF("%8", "%17", "%18", l)
-    asm("s_nop 1\n\t"
-        KV(0) KV(1) KV(2) KV(3) KJ(3) KV(4) KJ(4) KV(5) KJ(5) KV(6) KJ(6) KV(7) KJ(7) KV(8) KJ(8) KV(9) KJ(9)
-        : "+&v"(a0), "+&v"(a1), "+&v"(a2), "+&v"(b0), "+&v"(b1), "+&v"(b2), "+&v"(b3), "+&v"(b4), "+&v"(b5)
-        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(m[5]), "v"(one));
-#undef KV
-#undef KJ
-    vl[0] = a0; vl[1] = a1; vl[2] = a2;
-    jj[0] = b0; jj[1] = b1; jj[2] = b2; jj[3] = b3; jj[4] = b4; jj[5] = b5;
-}
-static_assert(FR_EE_PARENT == 9 && FR_ARM0 == 3 && FR_ARM1 == 10, "kin_sums lane ranges");
+static_assert(FR_EE_PARENT == 9 && FR_ARM0 == 3 && FR_ARM1 == 10, "kinematic sum ranges");
 
 // 1/d by v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; d finite, normal)
 __device__ __forceinline__ double frcp(double d)
@@ -271,6 +284,336 @@ __device__ __forceinline__ double frcp(double d)
     e = __builtin_fma(-d, r, 1.0);
     return __builtin_fma(r, e, r);
 }
+
+// ---- BEGIN generated by tools/gen_gj.py: mass-matrix solve helpers ----
+// m[i] = S_i . F for i = 0..10, S_i broadcast from lane i: eleven chains of six, round-robin
+__device__ __forceinline__ void column_dots(const double *S, const double *F, double *m)
+{
+#pragma unroll
+    for (int i = 0; i < 11; i++) m[i] = 0.0;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %11, %17 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %11, %17 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %17 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %11, %17 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %11, %17 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %11, %17 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %12, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %18 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %12, %18 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %12, %18 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %12, %18 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %13, %19 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %13, %19 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %19 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %13, %19 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %13, %19 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %13, %19 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %14, %20 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %14, %20 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %14, %20 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %20 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %14, %20 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %14, %20 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %14, %20 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %14, %20 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %15, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %15, %21 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %15, %21 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %15, %21 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %15, %21 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %15, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %15, %21 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %15, %21 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %15, %21 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %15, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %16, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %16, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %16, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %16, %22 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %16, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %16, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %16, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %16, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        : "+&v"(m[0]), "+&v"(m[1]), "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
+        : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
+}
+// pivot 0
+__device__ __forceinline__ void gj_pivot_0(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[0]));
+    const double nt = -(Mc[0] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 1
+__device__ __forceinline__ void gj_pivot_1(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[1]));
+    const double nt = -(Mc[1] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[2]), "+v"(Mc[0]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 2
+__device__ __forceinline__ void gj_pivot_2(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
+    const double nt = -(Mc[2] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[3]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 3
+__device__ __forceinline__ void gj_pivot_3(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
+    const double nt = -(Mc[3] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[4]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 4
+__device__ __forceinline__ void gj_pivot_4(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
+    const double nt = -(Mc[4] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[5]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 5
+__device__ __forceinline__ void gj_pivot_5(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
+    const double nt = -(Mc[5] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[6]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 6
+__device__ __forceinline__ void gj_pivot_6(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
+    const double nt = -(Mc[6] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[7]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 7
+__device__ __forceinline__ void gj_pivot_7(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
+    const double nt = -(Mc[7] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[8]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 8
+__device__ __forceinline__ void gj_pivot_8(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
+    const double nt = -(Mc[8] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[9]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[10]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 9
+__device__ __forceinline__ void gj_pivot_9(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
+    const double nt = -(Mc[9] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[10]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[11])
+        : "v"(nt));
+}
+// pivot 10
+__device__ __forceinline__ void gj_pivot_10(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
+    const double nt = -(Mc[10] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9])
+        : "v"(nt));
+}
+// pivot 11
+__device__ __forceinline__ void gj_pivot_11(double *Mc)
+{
+    double d;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
+    const double nt = -(Mc[11] * frcp(d));
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10])
+        : "v"(nt));
+}
+// ---- END generated by tools/gen_gj.py ----
 
 // One level of the delta-form prefix scan: (I + Da)(I + D) = I + Da + D + Da D,
 // pa + (I + Da) p = pa + p + Da p.
@@ -302,9 +645,12 @@ __host__ __device__ constexpr int pidx(int r, int c)
     return (r <= c) ? (r * 6 - r * (r - 1) / 2 + (c - r)) : (c * 6 - c * (c - 1) / 2 + (r - c));
 }
 
-// World spatial inertia of the lane's body (packed 21), from its world pose; M = body table row.
-__device__ __forceinline__ void world_inertia_to_lds(const double *M, const double *R, const double *p, double *dst,
-                                                     double *c, double *Iw)
+// World spatial inertia of the lane's body, from its world pose (M = body table row): world com c,
+// rotational inertia about the com Iw, and Ib = Iw + m (|c|^2 E - c c^T), the angular block about
+// the origin (packed xx xy xz yy yz zz); with h = m c the 6x6 is [[m E, -[h]x], [[h]x, Ib]].
+// The energy variant's articulated-body pass reads it from LDS, packed upper triangle (21).
+__device__ __forceinline__ void world_inertia(const double *M, const double *R, const double *p, double *c, double *Iw,
+                                              double *Ib)
 {
     const double m = M[T_M];
     const double lc0 = M[T_C], lc1 = M[T_C + 1], lc2 = M[T_C + 2];
@@ -326,16 +672,21 @@ __device__ __forceinline__ void world_inertia_to_lds(const double *M, const doub
     Iw[3] = (RI[3] * R[3] + RI[4] * R[4]) + RI[5] * R[5];
     Iw[4] = (RI[3] * R[6] + RI[4] * R[7]) + RI[5] * R[8];
     Iw[5] = (RI[6] * R[6] + RI[7] * R[7]) + RI[8] * R[8];
-    // [[m E, -m[c]x], [m[c]x, Iw + m(|c|^2 E - c c^T)]], packed upper triangle
+    Ib[0] = Iw[0] + (m * cc2 - mc0 * c[0]);
+    Ib[1] = Iw[1] - mc0 * c[1];
+    Ib[2] = Iw[2] - mc0 * c[2];
+    Ib[3] = Iw[3] + (m * cc2 - mc1 * c[1]);
+    Ib[4] = Iw[4] - mc1 * c[2];
+    Ib[5] = Iw[5] + (m * cc2 - mc2 * c[2]);
+}
+__device__ __forceinline__ void inertia_to_lds(double m, const double *c, const double *Ib, double *dst)
+{
+    const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
+    // [[m E, -m[c]x], [m[c]x, Ib]], packed upper triangle
     dst[0] = m; dst[1] = 0.0; dst[2] = 0.0; dst[3] = 0.0; dst[4] = mc2; dst[5] = -mc1;
     dst[6] = m; dst[7] = 0.0; dst[8] = -mc2; dst[9] = 0.0; dst[10] = mc0;
     dst[11] = m; dst[12] = mc1; dst[13] = -mc0; dst[14] = 0.0;
-    dst[15] = Iw[0] + (m * cc2 - mc0 * c[0]);
-    dst[16] = Iw[1] - mc0 * c[1];
-    dst[17] = Iw[2] - mc0 * c[2];
-    dst[18] = Iw[3] + (m * cc2 - mc1 * c[1]);
-    dst[19] = Iw[4] - mc1 * c[2];
-    dst[20] = Iw[5] + (m * cc2 - mc2 * c[2]);
+    dst[15] = Ib[0]; dst[16] = Ib[1]; dst[17] = Ib[2]; dst[18] = Ib[3]; dst[19] = Ib[4]; dst[20] = Ib[5];
 }
 
 // Inclusive prefix sum over the row's lanes of a 6-vector (Hillis-Steele, row_shr 1, 2, 4, 8).
@@ -373,20 +724,29 @@ __device__ __forceinline__ void inertia_mul(double m, const double *c, const dou
 // What the cost of the next step needs from a calculate() (row-uniform): EE and arm-mount
 // positions, the EE frame velocity J v and J_a J_a^T.  Written to the step record.
 struct CoopKin {
-    double ee[3], am[3], vl[3], jj[6];
+    double ee[3], am[3];
+    double ks;   // lane m = min(j, 8): kinematic sum m, J v (m < 3) or J_a J_a^T (packed, m - 3)
     double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
+};
+
+// The mass-matrix solve's inputs from a calculate(): the lane's world motion subspace and its body's
+// world spatial inertia as (m, h = m c, Ib) (zero on lanes 12..15).
+struct CoopBody {
+    double S[6], m, h[3], Ib[6];
 };
 
 // Lane-constant data of the row's body j (the doubles live in the body table).
 struct LaneConst {
     int slot;       // LDS body slot (dummy for lanes 12..15)
     bool is_rz;
+    int ka, kb;     // kinematic sum min(j, 8): S component x, y slot (S component or qd)
+    bool vsum;      // the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
 template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
-                                        double *Lk, CoopKin &kin, const double *grav)
+                                        double *Lk, CoopKin &kin, CoopBody &bd, const double *grav)
 {
     const double cz = L.is_rz ? cq : 1.0;
     const double sz = L.is_rz ? sq : 0.0;
@@ -424,10 +784,27 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     S[3] = w[0] * rotf;
     S[4] = w[1] * rotf;
     S[5] = w[2] * rotf;
-    double com[3], Iw[6];
-    world_inertia_to_lds(M, R, p, Lk + L_I + L.slot * 21, com, Iw);
+    double com[3], Iw[6], Ib[6];
+    world_inertia(M, R, p, com, Iw, Ib);
+#ifdef OLD_ABA
+    inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);
+#else
+    if constexpr (EN) inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);   // coop_aba's input
+#endif
+    {
+        const double live = M[T_NROT] + M[T_ROT];   // 1 for a real body, 0 on lanes 12..15
+        bd.m = M[T_M] * live;
 #pragma unroll
-    for (int k = 0; k < 6; k++) Lk[L_S + L.slot * 6 + k] = S[k];
+        for (int k = 0; k < 3; k++) bd.h[k] = (M[T_M] * com[k]) * live;
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            bd.Ib[k] = Ib[k] * live;
+            bd.S[k] = S[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) Lk[L_S + L.slot * S_STR + k] = S[k];
+    Lk[L_S + L.slot * S_STR + 6] = qd;
     kin.pw = 0.0;
     if constexpr (EN) {
         // The energy tank's power needs tau = tau_u + nonLinearEffects(q, v) (pinocchio_dynamics.cpp:
@@ -480,24 +857,31 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
-#pragma unroll
-    for (int k = 0; k < 3; k++) kin.vl[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) kin.jj[k] = 0.0;
+    kin.ks = 0.0;
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
-    // frame velocity J v over the EE chain (bodies 0..9), J_a J_a^T over the arm (bodies 3..9)
-    const double v3[3] = {S[0] * qd, S[1] * qd, S[2] * qd};
-    const double m6[6] = {S[0] * S[0], S[0] * S[1], S[0] * S[2], S[1] * S[1], S[1] * S[2], S[2] * S[2]};
-    kin_sums(v3, m6, 1.0, kin.vl, kin.jj);
+    // The frame velocity J v over the EE chain (bodies 0..9) and J_a J_a^T over the arm (bodies
+    // 3..9): nine sums, lane m computes sum m from the S / qd slots the row just wrote to LDS
+    // (ten LDS-read FMAs per lane instead of 72 DPP-broadcast FMAs that every lane repeats).
+    const double *xs = Lk + L_S + L.ka, *ys = Lk + L_S + L.kb;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i <= FR_EE_PARENT; i++) {
+        double y = ys[i * S_STR];
+        if (i < FR_ARM0) y = L.vsum ? y : 0.0;
+        acc = __builtin_fma(xs[i * S_STR], y, acc);
+    }
+    kin.ks = acc;
 }
 
-// Articulated-body passes over the world inertias / S staged in LDS; returns qdd of the lane's
-// joint.  The 6x6 articulated inertia is distributed by rows over each 8-lane half of the row:
-// lanes 0..5 and 8..13 hold rows 0..5 (lanes 6, 7, 14, 15 mirror row 5 and are masked out of the
-// sums), so one 3-stage butterfly leaves the full sum in every lane.  tau_i and U of body i are
-// LDS broadcasts.
+// Articulated-body passes over the world inertias / S staged in LDS (energy-tank rollouts, whose
+// power needs the forward pass's spatial accelerations; the others use coop_solve); returns qdd of
+// the lane's joint.  Backward pass: the 6x6 articulated inertia is distributed by rows (lane r < 6
+// holds row r; lanes 6..15 mirror row 5, unused); U = A S per row, D = S.U and S.pA as DPP
+// broadcast-FMA chains, and the rank-1 update A_parent = (A + I_parent) - U U^T / D with the
+// parent's own inertia added before the update.  Forward pass per level: qdd_i = (u_i - U_i . a_p)
+// / D_i, a_i = a_p + S_i qdd_i.
 template <bool EN>
-__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, double &pe)
+__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, double &pe, uint64_t &t_bwd)
 {
     const int r = j < 6 ? j : 5;   // lanes 0..5 hold rows 0..5; the others mirror row 5, unused
     int off[6];
@@ -507,7 +891,7 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
     double An[6], Sn[6], taun;
     auto fetch = [&](int i) {
         const double *Ii = Lk + L_I + i * 21;
-        const double *Si = Lk + L_S + i * 6;
+        const double *Si = Lk + L_S + i * S_STR;
 #pragma unroll
         for (int k = 0; k < 6; k++) An[k] = Ii[off[k]];
 #pragma unroll
@@ -515,15 +899,14 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         taun = Lw[L_TAU + i];
     };
     fetch(FR_NB - 1);
-    double C[6], pA = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) C[k] = 0.0;
+    double A[6], C[6], pA = 0.0;
 #pragma unroll
     for (int i = FR_NB - 1; i >= 0; i--) {
-        double A[6], S[6];
+        double S[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
-            A[k] = (i >= 10) ? An[k] : An[k] + C[k];
+            if (i >= 10) A[k] = An[k];      // finger leaves
+            else if (i == 9) A[k] = C[k];   // C: the fingers' parts plus body 9's own inertia
             S[k] = Sn[k];
         }
         const double tau = taun;
@@ -533,7 +916,11 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         // D = S.U and S.pA: rows 0..5 broadcast from lanes 0..5, every lane holds S
         double D, sp;
         bfma6_pair(U, pAr, S, D, sp);
+#ifdef ABL_RCP1
+        const double Dinv = __builtin_amdgcn_rcp(D);
+#else
         const double Dinv = frcp(D);
+#endif
         const double u = tau - sp;
         Lw[L_U + i * ROW + j] = U;
         Lw[L_DU + 2 * i] = Dinv;
@@ -541,43 +928,131 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         if (i > 0) {
             const double Ud = U * Dinv;
             const double ud = u * Dinv;
-            // C = A - U U^T / D, row r: C[k] = A[k] - (U_r / D) U_k (U_k broadcast from lane k)
-            if (i == 10) {
-#pragma unroll
-                for (int k = 0; k < 6; k++) C[k] += A[k];
-                pA += pAr + U * ud;
-            } else {
+            // parent's articulated inertia, row r: (A + I_parent)[k] - (U_r / D) U_k
+            if (i == 11) {   // first finger: parent 9 is reached through finger 10's level
 #pragma unroll
                 for (int k = 0; k < 6; k++) C[k] = A[k];
                 pA = pAr + U * ud;
-            }
-            bfma6_rank1(U, -Ud, C);
-        }
-    }
-    double acc = 0.0, a9 = 0.0;
-    double Srf = Lk[L_S + r], Uf = Lw[L_U + j], Dvf = Lw[L_DU], uf = Lw[L_DU + 1];
-    double Ff = EN ? Lk[L_F + r] : 0.0;
-    pe = 0.0;
+                bfma6_rank1(U, -Ud, C);
+            } else if (i == 10) {   // An now holds body 9 (fetched above)
 #pragma unroll
-    for (int i = 0; i < FR_NB; i++) {
-        const double Sr = Srf, Ui = Uf, Dv = Dvf, ui = uf, Fr = Ff;
-        if (i + 1 < FR_NB) {
-            Srf = Lk[L_S + (i + 1) * 6 + r];
-            Uf = Lw[L_U + (i + 1) * ROW + j];
-            Dvf = Lw[L_DU + 2 * (i + 1)];
-            uf = Lw[L_DU + 2 * (i + 1) + 1];
-            if constexpr (EN) Ff = Lk[L_F + (i + 1) * 6 + r];
+                for (int k = 0; k < 6; k++) C[k] = (C[k] + A[k]) + An[k];
+                pA += pAr + U * ud;
+                bfma6_rank1(U, -Ud, C);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 6; k++) A[k] = A[k] + An[k];
+                pA = pAr + U * ud;
+                bfma6_rank1(U, -Ud, A);
+            }
         }
-        const double ap = (i == 11) ? a9 : acc;
-        const double ua = bsum6_split(Ui * ap, 1.0);
-        const double dd = Dv * (ui - ua);
-        acc = ap + Sr * dd;
-        if (i == 9) a9 = acc;
-        if constexpr (EN) pe += Fr * acc;   // row r of f_i . sum_{k <= i} S_k qdd_k
-        Lw[L_QDD + i] = dd;
     }
-    const double qdd = Lw[L_QDD + (j < FR_NB ? j : 0)];
-    return j < FR_NB ? qdd : 0.0;   // lanes 12..15 keep q = qd = 0
+    pe = 0.0;
+#ifdef PHASE_TRACE
+    t_bwd = stamp(pA);
+#endif
+    {
+        double acc = 0.0, a9 = 0.0;
+        double Srf = Lk[L_S + r], Uf = Lw[L_U + j], Dvf = Lw[L_DU], uf = Lw[L_DU + 1];
+        double Ff = EN ? Lk[L_F + r] : 0.0;
+#pragma unroll
+        for (int i = 0; i < FR_NB; i++) {
+            const double Sr = Srf, Ui = Uf, Dv = Dvf, ui = uf, Fr = Ff;
+            if (i + 1 < FR_NB) {
+                Srf = Lk[L_S + (i + 1) * S_STR + r];
+                Uf = Lw[L_U + (i + 1) * ROW + j];
+                Dvf = Lw[L_DU + 2 * (i + 1)];
+                uf = Lw[L_DU + 2 * (i + 1) + 1];
+                if constexpr (EN) Ff = Lk[L_F + (i + 1) * 6 + r];
+            }
+            const double ap = (i == 11) ? a9 : acc;
+            const double ua = bsum6_split(Ui * ap, 1.0);
+            const double dd = Dv * (ui - ua);
+            acc = ap + Sr * dd;
+            if (i == 9) a9 = acc;
+            if constexpr (EN) pe += Fr * acc;   // row r of f_i . sum_{k <= i} S_k qdd_k
+            Lw[L_QDD + i] = dd;
+        }
+        const double qdd = Lw[L_QDD + (j < FR_NB ? j : 0)];
+        return j < FR_NB ? qdd : 0.0;
+    }
+}
+
+
+// Mass-matrix solve for the rollouts without the energy tank: qdd = M(q)^-1 tau_u, M by the
+// composite-rigid-body algorithm in world coordinates and eliminated by Gauss-Jordan, one column
+// per lane.  Equal to the zero-bias articulated-body pass in exact arithmetic; its serial chain is
+// twelve scalar pivots (the pivot d_k is already on lane k) instead of twelve 6x6 levels whose
+// D = S^T A S needs a six-deep cross-lane chain each.
+//   composite inertia   Ic_j = sum over the subtree of j, as (m, h, Ib): a suffix sum over lanes
+//                       0..11 (row_shl 1, 2, 4, 8); finger 10's subtree is itself.
+//   column j            M_ij = S_i . Ic_j S_j for the ancestors i of j (S_i broadcast from lane i),
+//                       M_jj on the diagonal; the entries below the diagonal by symmetry through
+//                       LDS.  Lane 12 holds the right-hand side tau.
+//   Gauss-Jordan        twelve pivots, each one broadcast of the pivot, a reciprocal and eleven
+//                       broadcast FMAs per lane; then qdd_j = tau'_j / M'_jj.
+__device__ __forceinline__ double coop_solve(int j, const CoopBody &bd, double tau_l, double *Lk, uint64_t &t_mid)
+{
+    double v[10] = {bd.m, bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
+    double own[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) own[k] = v[k];
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] += shl<1>(v[k]);
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] += shl<2>(v[k]);
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] += shl<4>(v[k]);
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] += shl<8>(v[k]);
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] = (j == 10) ? own[k] : v[k];
+    // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
+    const double *S = bd.S;
+    const double m = v[0], h0 = v[1], h1 = v[2], h2 = v[3];
+    const double I00 = v[4], I01 = v[5], I02 = v[6], I11 = v[7], I12 = v[8], I22 = v[9];
+    double F[6];
+    F[0] = m * S[0] - (h1 * S[5] - h2 * S[4]);
+    F[1] = m * S[1] - (h2 * S[3] - h0 * S[5]);
+    F[2] = m * S[2] - (h0 * S[4] - h1 * S[3]);
+    F[3] = (h1 * S[2] - h2 * S[1]) + ((I00 * S[3] + I01 * S[4]) + I02 * S[5]);
+    F[4] = (h2 * S[0] - h0 * S[2]) + ((I01 * S[3] + I11 * S[4]) + I12 * S[5]);
+    F[5] = (h0 * S[1] - h1 * S[0]) + ((I02 * S[3] + I12 * S[4]) + I22 * S[5]);
+    double Mc[12];
+    column_dots(S, F, Mc);
+    const double diag = ((S[0] * F[0] + S[1] * F[1]) + (S[2] * F[2] + S[3] * F[3])) + (S[4] * F[4] + S[5] * F[5]);
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const bool anc = i < j && !(j == FR_NB - 1 && i == FR_NB - 2);   // finger 11 hangs off body 9
+        Mc[i] = anc ? Mc[i] : ((i == j) ? diag : 0.0);
+    }
+    Mc[11] = (j == 11) ? diag : 0.0;
+    // row j of the block: column j's entries (upper part valid) and, in slot 12, tau_j
+    double *Row = Lk + L_COL + j * ROW;
+#pragma unroll
+    for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Row + i) = double2{Mc[i], Mc[i + 1]};
+    Row[12] = tau_l;
+    // below the diagonal: M_ij = M_ji, written by lane i; lane 12 reads the tau column
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        const double x = Lk[L_COL + i * ROW + j];
+        Mc[i] = (i > j || j == 12) ? x : Mc[i];
+    }
+#ifdef PHASE_TRACE
+    t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
+#endif
+    gj_pivot_0(Mc); gj_pivot_1(Mc); gj_pivot_2(Mc); gj_pivot_3(Mc); gj_pivot_4(Mc); gj_pivot_5(Mc);
+    gj_pivot_6(Mc); gj_pivot_7(Mc); gj_pivot_8(Mc); gj_pivot_9(Mc); gj_pivot_10(Mc); gj_pivot_11(Mc);
+    // the matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj, tau' on lane 12
+    if (j == 12) {
+#pragma unroll
+        for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Lk + L_TP + i) = double2{Mc[i], Mc[i + 1]};
+    }
+    double dj = Mc[0];
+#pragma unroll
+    for (int i = 1; i < 12; i++) dj = (j == i) ? Mc[i] : dj;
+    const double tp = Lk[L_TP + (j < FR_NB ? j : 0)];
+    return j < FR_NB ? tp / dj : 0.0;   // lanes 12..15 keep q = qd = 0
 }
 
 }  // namespace
@@ -628,12 +1103,12 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / fcost).
-// Step record store (layout: kernels.hpp FR_NREC), two 16-byte stores per lane with the whole row
-// active (no branch splits the step's basic block): lanes 0..11 write (q_j, qd_j) and lanes
-// 12..15 the first eight kinematic values, then lane j writes pair j mod 4 of the remaining eight
-// (lanes 4..15 repeat lanes 0..3: same address, same value).
-// register value the optimiser cannot trace back to a memory location (keeps the record selects
-// as v_cndmask instead of a dynamically indexed private copy of CoopKin)
+// Step record store (layout: kernels.hpp FR_NREC), the whole row active (no branch splits the
+// step's basic block): lanes 0..11 write (q_j, qd_j) and lanes 12..15 the EE / arm-mount
+// positions and the tank energy (one 16-byte store), then lane j writes kinematic sum min(j, 8)
+// (lanes 9..15 repeat lane 8: same address, same value).
+// vreg: a register value the optimiser cannot trace back to a memory location (keeps the record
+// selects as v_cndmask instead of a dynamically indexed private copy of CoopKin)
 __device__ __forceinline__ double vreg(double x)
 {
     asm volatile("" : "+v"(x));
@@ -646,18 +1121,12 @@ __device__ __forceinline__ void store_record(double *rp, int j, double q, double
 #endif
     const double e0 = vreg(kin.ee[0]), e1 = vreg(kin.ee[1]), e2 = vreg(kin.ee[2]);
     const double m0 = vreg(kin.am[0]), m1 = vreg(kin.am[1]), m2 = vreg(kin.am[2]);
-    const double l0 = vreg(kin.vl[0]), l1 = vreg(kin.vl[1]), l2 = vreg(kin.vl[2]);
-    const double k0 = vreg(kin.jj[0]), k1 = vreg(kin.jj[1]), k2 = vreg(kin.jj[2]);
-    const double k3 = vreg(kin.jj[3]), k4 = vreg(kin.jj[4]), k5 = vreg(kin.jj[5]);
-    const double a0 = (j < 12) ? q : (j == 12) ? e0 : (j == 13) ? e2 : (j == 14) ? m1 : l0;
-    const double a1 = (j < 12) ? qd : (j == 12) ? e1 : (j == 13) ? m0 : (j == 14) ? m2 : l1;
+    const double a0 = (j < 12) ? q : (j == 12) ? e0 : (j == 13) ? e2 : (j == 14) ? m1 : E;
+    const double a1 = (j < 12) ? qd : (j == 12) ? e1 : (j == 13) ? m0 : (j == 14) ? m2 : 0.0;
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
-    const int s = j & 3;
-    const double b0 = (s == 0) ? l2 : (s == 1) ? k1 : (s == 2) ? k3 : k5;
-    const double b1 = (s == 0) ? k0 : (s == 1) ? k2 : (s == 2) ? k4 : E;
-    *reinterpret_cast<double2 *>(rp + REC_VL + 2 + 2 * s) = double2{b0, b1};
+    rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
 }
-static_assert(REC_EE == 24 && REC_AM == 27 && REC_VL == 30 && REC_JJ == 33 && REC_E == 39 && FR_NREC == 40, "record layout");
+static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC_JJ == 35 && FR_NREC == 42, "record layout");
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / frec).  The
@@ -694,6 +1163,12 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     LaneConst L;
     L.is_rz = jl && FR_KIND[jb] == KIND_RZ;
     L.slot = jl ? j : FR_NB;
+    {
+        const int m = j < 9 ? j : 8;   // kinematic sum of the lane: a, b component nibbles
+        L.ka = (int)((0x211000210ull >> (4 * m)) & 0xF);
+        L.kb = (int)((0x221210666ull >> (4 * m)) & 0xF);
+        L.vsum = m < 3;
+    }
 
     double q = jl ? x0p[jb] : 0.0;
     double qd = jl ? x0p[FR_NB + jb] : 0.0;
@@ -702,7 +1177,8 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     double sq, cq;
     sincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
-    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, grav);   // set_state -> calculate() at (q0, v0)
+    CoopBody bd;
+    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step
     const bool sampled = !opt_row && jl;
@@ -723,6 +1199,10 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[0], ub_n = Up[jb];
     store_record(rp, j, q, qd, kin, E);
+#ifdef PHASE_TRACE
+    uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
+    uint64_t t_top = stamp(sq);
+#endif
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
@@ -742,15 +1222,34 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             const double vy = s * u0 + c * u1;
             qd = (j == 0) ? vx : ((j == 1) ? vy : ((j == 2) ? u : qd));
         }
-        Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;
+#ifndef OLD_ABA
+        if constexpr (EN)
+#endif
+            Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
 #ifndef ABL_NOFK
-        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, grav);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
 #endif
         double pe = 0.0;
+        uint64_t t_bwd = 0;
+#ifdef PHASE_TRACE
+        const uint64_t t_fk = stamp(kin.ee[0]);
+        ph[0] += t_fk - t_top;
+#endif
 #ifdef ABL_NOABA
-        const double qdd = Lw[L_TAU + j] * 1e-3;
+        const double qdd = u * 1e-3;
 #else
-        const double qdd = coop_aba<EN>(j, Lk, Lw, pe);
+#ifdef OLD_ABA
+        const double qdd = coop_aba<EN>(j, Lk, Lw, pe, t_bwd);
+#else
+        double qdd;
+        if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe, t_bwd);
+        else qdd = coop_solve(j, bd, (j >= 3 && j < 10) ? u : 0.0, Lk, t_bwd);
+#endif
+#endif
+#ifdef PHASE_TRACE
+        const uint64_t t_fwd = stamp(qdd);
+        ph[1] += t_bwd - t_fk;
+        ph[2] += t_fwd - t_bwd;
 #endif
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
@@ -760,9 +1259,23 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             E = smax(0.0, E + power * a.dt);
         }
         store_record(rn, j, q, qd, kin, E);
+#ifdef ABL_SINCOS
+        sq = q - q * q * q * (1.0 / 6.0);
+        cq = 1.0 - q * q * 0.5;
+#else
         sincos(q, &sq, &cq);
+#endif
+#ifdef PHASE_TRACE
+        const uint64_t t_end = stamp(sq);
+        ph[3] += t_end - t_fwd;
+        t_top = t_end;
+#endif
     }
     // the final step's dynamics are never observed (deviation 5)
+#ifdef PHASE_TRACE
+    if (a.trace && lane == 0 && !FROW)
+        for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)ph[i];
+#endif
 #ifdef COOP_TRACE
     if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -825,13 +1338,39 @@ static unsigned g_cu_count = 256;   // set by fr_coop_set_cu_count (hipDevicePro
 
 void fr_coop_set_cu_count(unsigned n) { g_cu_count = n ? n : 256; }
 
+// Dynamic LDS that lifts a multi-wave workgroup above half of the CU's 160 KiB, so that the
+// dispatcher places one workgroup per CU (one wave per SIMD) whatever the kernel's static LDS
+// (which the compiler trims per variant): two workgroups on a CU would double up its SIMDs.
+template <typename K>
+static unsigned one_per_cu_pad(K kernel, int wpb)
+{
+    if (wpb == 1) return 0;
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, reinterpret_cast<const void *>(kernel)) != hipSuccess) return 0;
+    const size_t want = 80 * 1024 + 256;
+    return at.sharedSizeBytes >= want ? 0u : (unsigned)(want - at.sharedSizeBytes);
+}
+
+template <int CK, bool EN, int WPB, bool FROW>
+static void launch_k(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
+{
+    static const unsigned pad = one_per_cu_pad(fr_coop_kernel<CK, EN, WPB, FROW>, WPB);
+    hipLaunchKernelGGL((fr_coop_kernel<CK, EN, WPB, FROW>), dim3(nb), dim3(64 * WPB), pad, s, a);
+}
+
+template <int CK, bool EN>
+static void launch_x(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
+{
+    static const unsigned pad = one_per_cu_pad(fr_coop_x_kernel<CK, EN>, 5);
+    hipLaunchKernelGGL((fr_coop_x_kernel<CK, EN>), dim3(nb), dim3(320), pad, s, a);
+}
+
 template <int WPB, bool FROW>
 static void launch_one(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
-    const dim3 grid(nb), block(64 * WPB);
-    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_coop_kernel<CK_TRACK_POINT, false, WPB, FROW>), grid, block, 0, s, a);
-    else if (a.energy) hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, true, WPB, FROW>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fr_coop_kernel<CK_ASSISTED_MANIPULATION, false, WPB, FROW>), grid, block, 0, s, a);
+    if (a.cost_kind == CK_TRACK_POINT) launch_k<CK_TRACK_POINT, false, WPB, FROW>(a, nb, s);
+    else if (a.energy) launch_k<CK_ASSISTED_MANIPULATION, true, WPB, FROW>(a, nb, s);
+    else launch_k<CK_ASSISTED_MANIPULATION, false, WPB, FROW>(a, nb, s);
 }
 
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
@@ -860,16 +1399,10 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, bool *f
     if (!frow) a.fcost = nullptr;
     a.xbase = groups * WG_ROWS;
     a.xrows = xrows;
-    const dim3 grid((unsigned)groups);
-    if (xrows == 0) {
-        launch_one<4, false>(a, (unsigned)groups, s);
-    } else if (a.cost_kind == CK_TRACK_POINT) {
-        hipLaunchKernelGGL((fr_coop_x_kernel<CK_TRACK_POINT, false>), grid, dim3(320), 0, s, a);
-    } else if (a.energy) {
-        hipLaunchKernelGGL((fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, true>), grid, dim3(320), 0, s, a);
-    } else {
-        hipLaunchKernelGGL((fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, false>), grid, dim3(320), 0, s, a);
-    }
+    if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
+    else if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, (unsigned)groups, s);
+    else if (a.energy) launch_x<CK_ASSISTED_MANIPULATION, true>(a, (unsigned)groups, s);
+    else launch_x<CK_ASSISTED_MANIPULATION, false>(a, (unsigned)groups, s);
     *folded = frow;
     return hipGetLastError();
 }

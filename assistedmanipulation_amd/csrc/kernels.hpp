@@ -46,13 +46,13 @@ struct FrRolloutArgs {
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
 // the state x_k the cost is evaluated at and the kinematics of the calculate() before it.
-constexpr int FR_NREC = 40;
+constexpr int FR_NREC = 42;   // 41 used, padded to 16 bytes
 constexpr int REC_QQD = 0;    // [2j], [2j + 1]: q_j, qd_j (j < 12)
 constexpr int REC_EE = 24;    // EE position (world)
 constexpr int REC_AM = 27;    // arm-mount position (world)
-constexpr int REC_VL = 30;    // EE linear frame velocity J v (bodies 0..9)
-constexpr int REC_JJ = 33;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11 12 22
-constexpr int REC_E = 39;     // energy tank level (enable_energy_limit)
+constexpr int REC_E = 30;     // energy tank level (enable_energy_limit)
+constexpr int REC_VL = 32;    // EE linear frame velocity J v (bodies 0..9)
+constexpr int REC_JJ = 35;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11 12 22     // energy tank level (enable_energy_limit)
 
 // The rollout costs from the records (fr_cost.hip): one wave per rollout, one lane per step, the
 // step costs summed in step order (the reference's J += cost, mppi.cpp:322-337).

@@ -37,9 +37,9 @@ FLOPS_PER_ROLLOUT_STEP = 6518.0
 FLOPS_COST_PER_ROLLOUT_STEP = 690.0
 FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STEP
 # Algorithmic HBM bytes per rollout-step: the rollout kernel reads its eps column (C = 12 fp64)
-# once and writes one step record (FR_NREC = 40 fp64); the cost kernel reads the record back.
+# once and writes one step record (FR_NREC = 42 fp64); the cost kernel reads the record back.
 BYTES_EPS_PER_ROLLOUT_STEP = 96.0
-BYTES_REC_PER_ROLLOUT_STEP = 320.0
+BYTES_REC_PER_ROLLOUT_STEP = 336.0
 BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
 # HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
 # tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
