@@ -122,7 +122,7 @@ __device__ __forceinline__ double bfma6(double x, const double *y, double acc)
         : "v"(x), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]));
     return acc;
 }
-#ifdef PHASE_TRACE
+#if defined(PHASE_TRACE) || defined(PHASE_FK)
 // diagnostics: shader-clock stamp once `dep` has been computed and the wave's LDS ops are done
 __device__ __forceinline__ uint64_t stamp(double dep)
 {
@@ -746,8 +746,14 @@ struct LaneConst {
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
 template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
-                                        double *Lk, CoopKin &kin, CoopBody &bd, const double *grav)
+                                        double *Lk, CoopKin &kin, CoopBody &bd, const double *grav, uint64_t *phf = nullptr)
 {
+#ifdef PHASE_FK
+#define FKSTAMP(i, dep) if (phf) { const uint64_t t_ = stamp(dep); phf[i] += t_ - phf[4]; phf[4] = t_; }
+    FKSTAMP(0, q)
+#else
+#define FKSTAMP(i, dep)
+#endif
     const double cz = L.is_rz ? cq : 1.0;
     const double sz = L.is_rz ? sq : 0.0;
     const double qprev = shr<1>(q);
@@ -763,10 +769,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     D[0] -= 1.0;
     D[4] -= 1.0;
     D[8] -= 1.0;
+    FKSTAMP(0, D[8])
     scan_level<1>(D, p);
     scan_level<2>(D, p);
     scan_level<4>(D, p);
     scan_level<8>(D, p);
+    FKSTAMP(1, p[2])
     double R[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) R[k] = D[k];
@@ -849,6 +857,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         for (int k = 0; k < 6; k++) Lk[L_F + L.slot * 6 + k] = f[k];
         kin.pw = ((f[0] * V[0] + f[1] * V[1]) + f[2] * V[2]) + ((f[3] * V[3] + f[4] * V[4]) + f[5] * V[5]);
     }
+    FKSTAMP(2, bd.S[5])
     double fpos[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) fpos[r] = p[r] + ((R[3 * r] * M[T_F] + R[3 * r + 1] * M[T_F + 1]) + R[3 * r + 2] * M[T_F + 2]);
@@ -862,6 +871,9 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     // The frame velocity J v over the EE chain (bodies 0..9) and J_a J_a^T over the arm (bodies
     // 3..9): nine sums, lane m computes sum m from the S / qd slots the row just wrote to LDS
     // (ten LDS-read FMAs per lane instead of 72 DPP-broadcast FMAs that every lane repeats).
+#ifdef ABL_NOKIN
+    return;
+#endif
     const double *xs = Lk + L_S + L.ka, *ys = Lk + L_S + L.kb;
     double acc = 0.0;
 #pragma unroll
@@ -871,6 +883,8 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         acc = __builtin_fma(xs[i * S_STR], y, acc);
     }
     kin.ks = acc;
+    FKSTAMP(3, acc)
+#undef FKSTAMP
 }
 
 // Articulated-body passes over the world inertias / S staged in LDS (energy-tank rollouts, whose
@@ -1111,7 +1125,7 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
 // selects as v_cndmask instead of a dynamically indexed private copy of CoopKin)
 __device__ __forceinline__ double vreg(double x)
 {
-    asm volatile("" : "+v"(x));
+    asm("" : "+v"(x));   // not volatile: a volatile asm would end the scheduling region here
     return x;
 }
 __device__ __forceinline__ void store_record(double *rp, int j, double q, double qd, const CoopKin &kin, double E)
@@ -1199,6 +1213,9 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[0], ub_n = Up[jb];
     store_record(rp, j, q, qd, kin, E);
+#ifdef PHASE_FK
+    uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
+#endif
 #ifdef PHASE_TRACE
     uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
     uint64_t t_top = stamp(sq);
@@ -1227,7 +1244,12 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #endif
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
 #ifndef ABL_NOFK
+#ifdef PHASE_FK
+        phf[4] = stamp(q);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav, phf);
+#else
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
+#endif
 #endif
         double pe = 0.0;
         uint64_t t_bwd = 0;
@@ -1275,6 +1297,10 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #ifdef PHASE_TRACE
     if (a.trace && lane == 0 && !FROW)
         for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)ph[i];
+#endif
+#ifdef PHASE_FK
+    if (a.trace && lane == 0 && !FROW)
+        for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)phf[i];
 #endif
 #ifdef COOP_TRACE
     if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();

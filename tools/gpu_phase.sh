@@ -7,7 +7,7 @@ for d in gpurun_variants/phase*/; do
     n=$(basename $d)
     rm -f gpurun_out/phase/$n.bin
     MPPI_WAVE_TRACE=$PWD/gpurun_out/phase/$n.bin MPPI_AMD_LIB=$PWD/$d/libmppi_amd.so timeout -k 10 120 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/phase/$n.json 2> gpurun_out/phase/$n.err || exit 1
-    echo "== $n"; python3 tools/phase_trace.py gpurun_out/phase/$n.bin 1026 || exit 1
+    echo "== $n"; case $n in *fk*) m=fk;; *) m=;; esac; python3 tools/phase_trace.py gpurun_out/phase/$n.bin 1026 $m || exit 1
 done
 mkdir -p gpurun_out/ab
 for d in gpurun_variants/*/; do
