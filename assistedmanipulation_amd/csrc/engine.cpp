@@ -112,6 +112,7 @@ struct mppi_handle {
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
+    bool fuse_cost = false;   // MPPI_COST_KERNEL=fused: costs inside the rollout launch (LDS record rings; slower)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
     size_t inj_capacity = 0;   // doubles
@@ -457,6 +458,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     {
         const char *kv = std::getenv("MPPI_FR_KERNEL");
         h->coop = !(kv && std::string(kv) == "lane");
+        const char *cv = std::getenv("MPPI_COST_KERNEL");   // A/B: "fused" = step costs in the rollout launch
+        h->fuse_cost = cv && std::string(cv) == "fused";
     }
     noise_transform((int)Cd, cfg->covariance, h->T, h->tdiag);
     if (h->H < 1 || h->H > (1 << 20)) { delete h; return fail(nullptr, MPPI_ERR_INVALID, "horizon steps out of range"); }
@@ -1090,9 +1093,13 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         std::memcpy(sa.x0v, state, (size_t)h->X * sizeof(double));   // the state rides in the launch
         sa.x0_out = h->d_x0;
         sa.X = (int)h->X;
+        if (h->tdiag)
+            for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
         HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
     }
-    if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    // timing level 1 with the cooperative kernel: the rollout launch records its own events
+    const bool ev_in_launch = h->timing == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
+    if (h->timing >= 1 && !ev_in_launch) HIP_TRY(hipEventRecord(h->ev[1], h->stream));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         FrRolloutArgs a{};
         a.model = h->d_model;
@@ -1125,10 +1132,12 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         }
         bool folded = false;
         if (use_coop(h)) {
-            HIP_TRY(launch_fr_coop_update(a, h->stream, &folded));
-            if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+            bool costs_done = false;   // the rollout launch evaluated the costs as well
+            HIP_TRY(launch_fr_coop_update(a, h->stream, h->fuse_cost, ev_in_launch ? h->ev[1] : nullptr,
+                                          ev_in_launch ? h->ev_dyn : nullptr, &folded, &costs_done));
+            if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
-            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+            if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
             if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
@@ -1200,10 +1209,21 @@ mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(launch_weights(h->d_costs, h->R, h->cost_scale, h->d_weights, h->d_status, h->stream));
+    WGradArgs w{};
+    w.cost = h->d_costs;
+    w.R = h->R;
+    w.cost_scale = h->cost_scale;
+    w.weights = h->d_weights;
+    w.status = h->d_status;
+    w.noise = h->d_noise;
+    w.begin = h->begin;
+    w.count = h->count;
+    w.Rpad = h->Rpad;
+    w.H = (int)h->H;
+    w.C = (int)h->C;
+    w.gsplit = h->d_gsplit;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
-    HIP_TRY(launch_gradient(h->d_noise, h->d_weights, h->begin, h->count, h->Rpad, (int)h->H, (int)h->C, h->d_status,
-                            h->d_gsplit, h->d_gpart, h->world > 1, h->stream));
+    HIP_TRY(launch_weights_gradient(w, h->d_gpart, h->world > 1, h->stream));
     return MPPI_OK;
 }
 
@@ -1213,7 +1233,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     HIP_TRY(hipSetDevice(h->device));
     const int HC = (int)(h->H * h->C);
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+    if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     HIP_TRY(launch_finish(finish_args(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     HIP_TRY(hipEventRecord(h->ev_pub, h->stream));

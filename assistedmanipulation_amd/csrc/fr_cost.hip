@@ -22,139 +22,14 @@
 #include "device_common.hpp"
 #include "engine_types.hpp"
 #include "kernels.hpp"
+#include "fr_cost_terms.hpp"
 
 using namespace mppi_eng;
 using mppi_dev::smin;
 
 namespace {
 
-constexpr int CK_ASSISTED_MANIPULATION = 1, CK_TRACK_POINT = 3;   // mppi_cost_kind
-
-// AssistedManipulation barriers (assisted_manipulation.cpp), written as selects
-__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v)
-{
-    const double d = v - b.bound;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (b.bound - v), b.max);
-    return (v >= b.bound) ? over : under;
-}
-__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v)
-{
-    const double d = b.bound - v;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (v - b.bound), b.max);
-    return (v <= b.bound) ? over : under;
-}
-
-// trajectory_cost's velocity part on the EE frame velocity (assisted_manipulation.cpp:237-290)
-__device__ __forceinline__ double trajectory_term(const DevCost &Cs, const StepConst &sc, const double *vl)
-{
-    double proj = ((vl[0] * sc.target[0] + vl[1] * sc.target[1]) + vl[2] * sc.target[2]) / sc.tt;
-    const double p0 = proj * sc.target[0], p1 = proj * sc.target[1], p2 = proj * sc.target[2];
-    proj = copysign(1.0, proj) * sqrt((p0 * p0 + p1 * p1) + p2 * p2);
-    const double err = fabs(sc.vtarget - proj);
-    const double tc = sc.pos_cost + ((Cs.traj_vel_c + Cs.traj_vel_l * fabs(err)) + Cs.traj_vel_q * err * err);
-    return sc.active ? tc : 0.0;
-}
-
-// manipulability_cost on J_a J_a^T (assisted_manipulation.cpp:224-235)
-__device__ __forceinline__ double manipulability_term(const DevCost &Cs, const double *jj)
-{
-    const double m00 = jj[0], m01 = jj[1], m02 = jj[2], m11 = jj[3], m12 = jj[4], m22 = jj[5];
-    const double det = (m00 * (m11 * m22 - m12 * m12) - m01 * (m01 * m22 - m12 * m02)) + m02 * (m01 * m12 - m11 * m02);
-    double vol = sqrt(det);
-    vol = isnan(vol) ? 1e-5 : ((vol < 1e-5) ? 1e-5 : ((1e5 < vol) ? 1e5 : vol));
-    const double iv = 1.0 / vol;
-    return (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
-}
-
-// AssistedManipulation::get_cost at the record's state with its kinematics
-template <bool EN>
-__device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r)
-{
-    double j0 = 0.0, j1 = 0.0, v0 = 0.0, v1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < FR_NB; j++) {
-        const double q = r[REC_QQD + 2 * j], vq = fabs(r[REC_QQD + 2 * j + 1]);
-        const double lj = left_barrier(Cs.lower[j], q) + right_barrier(Cs.upper[j], q);
-        const double lv = Cs.vel_q[j] * (vq * vq);
-        if (j < 6) { j0 += lj; v0 += lv; }
-        else { j1 += lj; v1 += lv; }
-    }
-    const double joint = j0 + j1, vel = v0 + v1;
-    double s, c;
-    sincos(r[REC_QQD + 4], &s, &c);   // base yaw q_2
-    const double *ee = r + REC_EE, *am = r + REC_AM;
-    double wc = 0.0;
-    {
-        const double r22 = (1.0 - c) + c;
-        const double fw0 = c, fw1 = s, fw2 = 0.0;
-        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
-        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
-        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
-        const double rb2 = am[2] + off2;
-        const double t0 = ee[0] - (am[0] + off0), t1 = ee[1] - (am[1] + off1), t2 = ee[2] - rb2;
-        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
-        wc += left_barrier(Cs.ws_infront, proj);
-        wc += right_barrier(Cs.ws_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
-        const double n1 = sqrt(t0 * t0 + t1 * t1);
-        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
-        const double yaw = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
-        const double ay = fabs(yaw);
-        const double yc = (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
-        wc += isnan(yaw) ? 0.0 : yc;
-        wc += left_barrier(Cs.ws_above, ee[2] - rb2);
-    }
-    double cost = 0.0;
-    cost += Cs.en_joint ? joint : 0.0;
-    cost += Cs.en_self ? Cs.self_collision : 0.0;
-    cost += Cs.en_work ? wc : 0.0;
-    if constexpr (EN) {   // energy_cost (:211-222)
-        const double E = r[REC_E];
-        cost += left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);
-    }
-    cost += Cs.en_vel ? vel : 0.0;
-    cost += Cs.en_traj ? trajectory_term(Cs, sc, r + REC_VL) : 0.0;
-    cost += Cs.en_manip ? manipulability_term(Cs, r + REC_JJ) : 0.0;
-    return cost;
-}
-
-// TrackPoint::get_cost: the joint terms sum joints 0..9 in order; reach_cost's robot point is the
-// arm mount + R_z(yaw) (0.3, 0, 0.15) (track_point.cpp:162-186)
-__device__ __forceinline__ double track_point_cost(const DevCost &Cs, const double *r)
-{
-    const double *ee = r + REC_EE, *am = r + REC_AM;
-    const double d0 = ee[0] - Cs.tp_point[0], d1 = ee[1] - Cs.tp_point[1], d2 = ee[2] - Cs.tp_point[2];
-    const double distance = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
-    double cost = 100.0 * (distance * distance);   // point_cost: 100 pow(distance, 2)
-    double joint = 0.0;
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-        const double q = r[REC_QQD + 2 * j], lo = Cs.tp_lo[j], up = Cs.tp_up[j];
-        const double below = (q < lo) ? 1000.0 + 100000.0 * ((lo - q) * (lo - q)) : 0.0;
-        const double above = (q > up) ? 1000.0 + 100000.0 * ((q - up) * (q - up)) : 0.0;
-        joint += below + above;
-    }
-    double s, c;
-    sincos(r[REC_QQD + 4], &s, &c);
-    const double r22 = (1.0 - c) + c;
-    const double off0 = (0.3 * c + (-s) * 0.0) + 0.0 * 0.15;
-    const double off1 = (0.3 * s + c * 0.0) + 0.0 * 0.15;
-    const double off2 = (0.0 * 0.3 + 0.0 * 0.0) + r22 * 0.15;
-    const double t0 = ee[0] - (am[0] + off0), t1 = ee[1] - (am[1] + off1), t2 = ee[2] - (am[2] + off2);
-    const double reach = right_barrier(Cs.tp_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
-    cost += Cs.tp_en_joint ? joint : 0.0;
-    cost += Cs.tp_en_self ? Cs.tp_self : 0.0;
-    cost += Cs.tp_en_reach ? reach : 0.0;
-    return cost;
-}
-
-__device__ __forceinline__ double readlane_f64(double x, int l)
-{
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-    return __hiloint2double(hi, lo);
-}
+using namespace mppi_cost;
 
 // Records of one rollout are contiguous ([R][H][FR_NREC]): a wave stages up to 64 of them into LDS
 // with 1 KiB-contiguous loads, then each lane reads its step's record back.  The LDS record stride
@@ -202,9 +77,7 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
                 r[2 * i] = v.x;
                 r[2 * i + 1] = v.y;
             }
-            const StepConst &sc = stp[base + lane];
-            if constexpr (CK == CK_TRACK_POINT) c = sc.gamma_k * track_point_cost(Cs, r);
-            else c = sc.gamma_k * assisted_manipulation_cost<EN>(Cs, sc, r);
+            c = step_cost<CK, EN>(Cs, stp[base + lane], r);
         }
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
         __syncthreads();

@@ -10,8 +10,8 @@
 //                    rollout of the dynamics with the per-step cost fused, cost[r]
 //                                                                  (mppi.cpp:242-342)
 //   [RCCL all-reduce of cost[R] when sharded]
-//   weights_kernel   min/max over non-NaN, softmin weights          (optimise(), mppi.cpp:344-408)
-//   gradient_kernel  partial gradient sum_r w_r eps_r over the local shard (mppi.cpp:415-418)
+//   weights_gradient_kernel  softmin weights and the partial gradient sum_r w_r eps_r over the
+//                    local shard, one launch (optimise(), mppi.cpp:344-418)
 //   [RCCL all-reduce of the partial gradient when sharded]
 //   finish_kernel    U* += step * g, Savitzky-Golay, clamp          (mppi.cpp:421-447)
 //   fr_rollout_kernel(optimal) / pm_rollout_kernel(optimal)
@@ -691,10 +691,17 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
             mppi_dev::box_muller(r.x, r.y, z[0], z[1]);
             mppi_dev::box_muller(r.z, r.w, z[2], z[3]);
 #pragma unroll
-            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.T[(c0 + c) * C + c0 + c] * (double)z[c] : 0.0;
+            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.tdv[c0 + c] * (double)z[c] : 0.0;
         }
     }
     double *o = a.noise + ((int64_t)k * a.Rpad + lr) * C + c0;
+    if constexpr (CW == 4) {   // a full piece: two 16-byte stores (C = 12: c0 = 0, 4, 8 doubles, 32-B aligned)
+        if (cw == 4) {
+            reinterpret_cast<double2 *>(o)[0] = double2{eps[0], eps[1]};
+            reinterpret_cast<double2 *>(o)[1] = double2{eps[2], eps[3]};
+            return;
+        }
+    }
 #pragma unroll
     for (int c = 0; c < CW; c++)
         if (c < cw) o[c] = eps[c];
@@ -829,123 +836,160 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
-constexpr int WT = 1024;   // weights_kernel: one workgroup
-constexpr int WU = 8;      // costs in flight per thread and pass
-__global__ __launch_bounds__(WT) void weights_kernel(const double *__restrict__ cost, int64_t R, double cost_scale,
-                                                     double *__restrict__ weights, Status *__restrict__ status)
+// optimise() and the partial gradient in one launch (mppi.cpp:344-418), grid (H, GRAD_SPLIT).
+// Block (k, s) sums w_r eps_r over a contiguous eighth of the local rollouts of step k, one
+// rollout's C contiguous components per thread, then its 256 partials in a fixed tree into
+// gsplit[s][k] (deterministic, no atomics); the finish kernel adds the GRAD_SPLIT partials in a
+// fixed order.  The weights need min / max / count of the costs and the softmin normaliser: every
+// block computes them itself from the costs (out of L2) instead of waiting for another block, in
+// the order of one 1024-thread block - each real wave carries four of its sixteen waves lane for
+// lane, so the butterflies pair the same values and every block holds the same bits.  The block's
+// eps loads are issued first and land during the reductions.  Each block writes the weights of its
+// slice of [0, R), block (0, 0) the status words.
+constexpr int WV = 16;       // waves of the 1024-thread reduction order
+constexpr int WU = 8;        // costs per (virtual) thread and pass
+constexpr int NV = WV / 4;   // virtual waves per real wave
+constexpr int GR = 2;        // rollouts per thread whose eps is loaded up front
+
+template <int C>
+__global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
-    __shared__ double smn[WT / 64], smx[WT / 64], ssum[WT / 64];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    double mn = INFINITY, mx = -INFINITY, cnt = 0.0;
-    for (int64_t base = 0; base < R; base += WT * WU) {
-        double c[WU];
+    __shared__ double red[256 * C];
+    __shared__ double smn[WV], smx[WV], ssum[WV];
+    const int t = threadIdx.x, rw = t >> 6, l = t & 63;
+    const int64_t R = a.R;
+    const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
+    const int64_t chunk = (a.count + ns - 1) / ns;
+    const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
+    double ne[GR][C];   // eps of rollouts r0 + t + 256 m (row 0 stands in past r1, unused)
 #pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const int64_t i = base + (int64_t)u * WT + t;
-            c[u] = (i < R) ? cost[i] : NAN;
-        }
+    for (int m = 0; m < GR; m++) {
+        const int64_t r = r0 + t + 256 * m;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C;
 #pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const bool ok = !isnan(c[u]);
-            cnt += ok ? 1.0 : 0.0;
-            mn = (ok && c[u] < mn) ? c[u] : mn;
-            mx = (ok && c[u] > mx) ? c[u] : mx;
+        for (int c = 0; c < C; c++) ne[m][c] = n[c];
+    }
+    // min / max / count over the non-NaN costs
+    double mn[NV], mx[NV], cn[NV];
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        mn[v] = INFINITY;
+        mx[v] = -INFINITY;
+        cn[v] = 0.0;
+    }
+    for (int64_t base = 0; base < R; base += WV * 64 * WU) {
+        double cv[WU][NV];
+#pragma unroll
+        for (int u = 0; u < WU; u++)
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                const int64_t i = base + (int64_t)u * (WV * 64) + (NV * rw + v) * 64 + l;
+                cv[u][v] = (i < R) ? a.cost[i] : (double)NAN;
+            }
+#pragma unroll
+        for (int u = 0; u < WU; u++)
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                const double c = cv[u][v];
+                const bool ok = !isnan(c);
+                cn[v] += ok ? 1.0 : 0.0;
+                mn[v] = (ok && c < mn[v]) ? c : mn[v];
+                mx[v] = (ok && c > mx[v]) ? c : mx[v];
+            }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        const double v0 = wave_min(mn[v]), v1 = wave_max(mx[v]), v2 = wave_sum(cn[v]);
+        if (l == 0) {
+            smn[NV * rw + v] = v0;
+            smx[NV * rw + v] = v1;
+            ssum[NV * rw + v] = v2;
         }
     }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    cnt = wave_sum(cnt);
-    if (l == 0) { smn[w] = mn; smx[w] = mx; ssum[w] = cnt; }
     __syncthreads();
     double minimum = smn[0], maximum = smx[0], valid = ssum[0];
 #pragma unroll
-    for (int i = 1; i < WT / 64; i++) {
+    for (int i = 1; i < WV; i++) {
         minimum = smin(minimum, smn[i]);
         maximum = smax(maximum, smx[i]);
         valid += ssum[i];
     }
     __syncthreads();
+    const bool lead = k == 0 && s == 0 && t == 0;
+    Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
-        if (t == 0) { status->all_nan = 1; status->early = 1; status->minimum = minimum; status->maximum = maximum; }
+        if (lead) { st->all_nan = 1; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
         return;
     }
     const double difference = maximum - minimum;
     if (difference < 1e-6) {   // early return, weights/gradient stale (mppi.cpp:373-375)
-        if (t == 0) { status->all_nan = 0; status->early = 1; status->minimum = minimum; status->maximum = maximum; }
+        if (lead) { st->all_nan = 0; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
         return;
     }
-    double tot = 0.0;
-    for (int64_t base = 0; base < R; base += WT * WU) {
-        double c[WU];
+    auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
+    double tot[NV];
 #pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const int64_t i = base + (int64_t)u * WT + t;
-            c[u] = (i < R) ? cost[i] : NAN;
-        }
+    for (int v = 0; v < NV; v++) tot[v] = 0.0;
+    for (int64_t base = 0; base < R; base += WV * 64 * WU) {
+        double cv[WU][NV];
 #pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const int64_t i = base + (int64_t)u * WT + t;
-            const double e = isnan(c[u]) ? 0.0 : exp(-cost_scale * (c[u] - minimum) / difference);
-            tot += e;
-            if (i < R) weights[i] = e;
-        }
+        for (int u = 0; u < WU; u++)
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                const int64_t i = base + (int64_t)u * (WV * 64) + (NV * rw + v) * 64 + l;
+                cv[u][v] = (i < R) ? a.cost[i] : (double)NAN;
+            }
+#pragma unroll
+        for (int u = 0; u < WU; u++)
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                const int64_t i = base + (int64_t)u * (WV * 64) + (NV * rw + v) * 64 + l;
+                if (i < R) tot[v] += expw(cv[u][v]);   // past R the one-block sum added +0.0
+            }
     }
-    tot = wave_sum(tot);
-    if (l == 0) ssum[w] = tot;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        const double sv = wave_sum(tot[v]);
+        if (l == 0) ssum[NV * rw + v] = sv;
+    }
     __syncthreads();
     double total = ssum[0];
 #pragma unroll
-    for (int i = 1; i < WT / 64; i++) total += ssum[i];
-    for (int64_t base = 0; base < R; base += WT * WU) {
-        double e[WU];
-#pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const int64_t i = base + (int64_t)u * WT + t;
-            e[u] = (i < R) ? weights[i] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < WU; u++) {
-            const int64_t i = base + (int64_t)u * WT + t;
-            if (i < R) weights[i] = e[u] / total;
-        }
+    for (int i = 1; i < WV; i++) total += ssum[i];
+    {   // this block's slice of the weights
+        const int64_t nb = (int64_t)gridDim.x * ns, b = (int64_t)s * gridDim.x + k;
+        const int64_t wc = (R + nb - 1) / nb, w0 = b * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
+        for (int64_t i = w0 + t; i < w1; i += 256) a.weights[i] = expw(a.cost[i]) / total;
     }
-    if (t == 0) { status->all_nan = 0; status->early = 0; status->minimum = minimum; status->maximum = maximum; status->total = total; }
-}
-
-// Partial gradient over the local shard (mppi.cpp:415-418), noise layout [H][Rpad][C]:
-// stage 1, grid (H, GRAD_SPLIT): each block sums a contiguous range of rollouts of step k, one
-// rollout's C contiguous components per thread (coalesced 8*C-byte rows), into gsplit[s][k][c];
-// stage 2 adds the GRAD_SPLIT partials in a fixed order (deterministic, no atomics).
-template <int C>
-__global__ __launch_bounds__(256) void gradient_kernel(const double *__restrict__ noise, const double *__restrict__ weights,
-                                                       int64_t begin, int64_t count, int64_t Rpad, int H,
-                                                       const Status *__restrict__ status, double *__restrict__ gsplit)
-{
-    __shared__ double red[256 * (C <= 4 ? 4 : 12)];
-    if (status->early) return;
-    const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
-    const int64_t chunk = (count + ns - 1) / ns;
-    const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < count) ? r0 + chunk : count;
-    const double *w = weights + begin;
+    if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; st->total = total; }
     double acc[C];
 #pragma unroll
     for (int c = 0; c < C; c++) acc[c] = 0.0;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
-        const double wr = w[r];
-        const double *n = noise + ((int64_t)k * Rpad + r) * C;
+#pragma unroll
+    for (int m = 0; m < GR; m++) {
+        const int64_t r = r0 + t + 256 * m;
+        if (r < r1) {
+            const double wr = expw(a.cost[a.begin + r]) / total;
+#pragma unroll
+            for (int c = 0; c < C; c++) acc[c] += wr * ne[m][c];
+        }
+    }
+    for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
+        const double wr = expw(a.cost[a.begin + r]) / total;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] += wr * n[c];
     }
 #pragma unroll
-    for (int c = 0; c < C; c++) red[c * 256 + threadIdx.x] = acc[c];
+    for (int c = 0; c < C; c++) red[c * 256 + t] = acc[c];
     __syncthreads();
     for (int h = 128; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h)
+        if (t < h)
 #pragma unroll
-            for (int c = 0; c < C; c++) red[c * 256 + threadIdx.x] += red[c * 256 + threadIdx.x + h];
+            for (int c = 0; c < C; c++) red[c * 256 + t] += red[c * 256 + t + h];
         __syncthreads();
     }
-    if ((int)threadIdx.x < C) gsplit[((int64_t)s * H + k) * C + threadIdx.x] = red[threadIdx.x * 256];
+    if (t < C) a.gsplit[((int64_t)s * a.H + k) * C + t] = red[t * 256];
 }
 
 __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
@@ -1076,6 +1120,52 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
     finish_block(a, sg_err);
 }
 
+// finish() without the Savitzky-Golay filter, one U* element per thread: every load is issued
+// before the first store, so the block makes one dependent memory trip where finish_block makes
+// five (gradient splits, U*_shifted, the bounds, U*, then the host block).
+__global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
+{
+    const int HC = a.H * a.C;
+    const bool upd = !a.status->early, ok = !a.status->all_nan;   // no filter: no SG error
+    const double oc = threadIdx.x == 0 ? *a.opt_cost : 0.0;
+    const int nsp = a.ns > 0 ? a.ns : 1;
+    const double *__restrict__ gs = a.ns > 0 ? a.gsplit : a.gpart;
+    double *__restrict__ Us = a.Ushift;
+    double *__restrict__ U = a.U;
+    for (int t = threadIdx.x; t < HC; t += blockDim.x) {
+        const int c = t % a.C;
+        double g = gs[t];
+        for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
+        double u = Us[t];
+        const double uo = U[t];
+        const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
+        if (upd) {
+            a.gradient[t] = g;
+            u += g * a.gradient_step;
+            if (a.control_bound) {
+                u = smin(u, hi);
+                u = smax(u, lo);
+            }
+            Us[t] = u;
+        }
+        const double v = ok ? u : uo;
+        if (ok) U[t] = v;
+        a.out[t] = v;
+    }
+    if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
+    for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
+    if (threadIdx.x == 0) {
+        const Status stt = *a.status;
+        a.status_w->sg_error = 0;
+        a.out[HC + 0] = oc;
+        a.out[HC + 1] = (double)stt.all_nan;
+        a.out[HC + 2] = (double)stt.early;
+        a.out[HC + 3] = 0.0;
+        a.out[HC + 4] = stt.minimum;
+        a.out[HC + 5] = stt.maximum;
+    }
+}
+
 
 
 // ---------------------------------------------------------------------------------------------
@@ -1133,32 +1223,24 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s)
+hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s)
 {
-    hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(WT), 0, s, cost, R, cost_scale, weights, status);
-    return hipGetLastError();
-}
-
-hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int H, int C, const Status *status, double *gsplit, double *gpart, bool sum_splits, hipStream_t s)
-{
-    if (C == FR_C)
-        hipLaunchKernelGGL(gradient_kernel<FR_C>, dim3(H, GRAD_SPLIT), dim3(256), 0, s, noise, weights, begin, count, Rpad, H,
-                           status, gsplit);
-    else
-        hipLaunchKernelGGL(gradient_kernel<3>, dim3(H, GRAD_SPLIT), dim3(256), 0, s, noise, weights, begin, count, Rpad, H,
-                           status, gsplit);
+    const dim3 grid((unsigned)a.H, GRAD_SPLIT);
+    if (a.C == FR_C) hipLaunchKernelGGL(weights_gradient_kernel<FR_C>, grid, dim3(256), 0, s, a);
+    else if (a.C == 3) hipLaunchKernelGGL(weights_gradient_kernel<3>, grid, dim3(256), 0, s, a);
+    else return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (!sum_splits) return hipSuccess;   // finish_kernel adds the splits itself
-    const int HC = H * C;
-    hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, gsplit, GRAD_SPLIT, HC, status, gpart);
+    if (e != hipSuccess || !sum_splits) return e;   // unsharded: the finish kernel adds the splits itself
+    const int HC = a.H * a.C;
+    hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, a.gsplit, GRAD_SPLIT, HC,
+                       (const Status *)a.status, gpart);
     return hipGetLastError();
 }
 
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, a);
+    if (a.sg_window > 0) hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(finish_flat_kernel, dim3(1), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

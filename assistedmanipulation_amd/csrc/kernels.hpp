@@ -93,6 +93,7 @@ struct SampleArgs {
     double x0v[MAX_X];
     double *x0_out;
     int X;
+    double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
 };
 
 struct PmRolloutArgs {
@@ -193,16 +194,30 @@ inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
-hipError_t launch_weights(const double *cost, int64_t R, double cost_scale, double *weights, Status *status, hipStream_t s);
 constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
-hipError_t launch_gradient(const double *noise, const double *weights, int64_t begin, int64_t count, int64_t Rpad,
-                           int H, int C, const Status *status, double *gsplit, double *gpart, bool sum_splits, hipStream_t s);
+// optimise() and the partial gradient in one launch (kernels.hip weights_gradient_kernel)
+struct WGradArgs {
+    const double *cost;    // [R], global rollout index
+    int64_t R;
+    double cost_scale;
+    double *weights;       // [R]
+    Status *status;
+    const double *noise;   // [H][Rpad][C]
+    int64_t begin, count, Rpad;
+    int H, C;
+    double *gsplit;        // [GRAD_SPLIT][H][C]
+};
+// sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
+hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
 void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split leaves one CU to the remainder)
 // The update's rollouts (fr_coop_x_kernel): one workgroup per CU of four one-SIMD waves of rollouts
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, bool *folded);
+// The update's rollouts (fr_coop.hip): fuse_cost = evaluate the step costs in the launch when there is
+// no energy tank (*costs_done); e0 / e1 = optional timing events around the launch.
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, bool fuse_cost, hipEvent_t e0, hipEvent_t e1,
+                                 bool *folded, bool *costs_done);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
 

@@ -32,12 +32,13 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; t
 # Algorithmic FLOPs of one rollout-step of the minimal arithmetic the device executes
 # (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
 # FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins these values):
-# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel.
+# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel (with the A/B
+# switch MPPI_COST_KERNEL=fused both run in the rollout launch, fr_coop_xc_kernel).
 FLOPS_PER_ROLLOUT_STEP = 6518.0
 FLOPS_COST_PER_ROLLOUT_STEP = 690.0
 FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STEP
-# Algorithmic HBM bytes per rollout-step: the rollout kernel reads its eps column (C = 12 fp64)
-# once and writes one step record (FR_NREC = 42 fp64); the cost kernel reads the record back.
+# Algorithmic HBM bytes per rollout-step: the rollout launch reads its eps column (C = 12 fp64)
+# once; on the records path it also writes a step record (FR_NREC = 42 fp64) the cost kernel reads.
 BYTES_EPS_PER_ROLLOUT_STEP = 96.0
 BYTES_REC_PER_ROLLOUT_STEP = 336.0
 BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
@@ -146,14 +147,16 @@ def main():
     value = S_total * traj.H / (elapsed / args.steps)
     lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
     dyn_ms = dyn / args.steps                             # the rollout (dynamics) kernel alone, timed loop
-    cost_ms = 0.0 if lane else float(kt[1] - kt[5])      # fr_step_cost_kernel (breakdown pass)
+    records = not lane and os.environ.get("MPPI_COST_KERNEL") != "fused"   # A/B: costs in the rollout launch
+    cost_ms = float(kt[1] - kt[5]) if records else 0.0      # fr_step_cost_kernel (breakdown pass)
     traffic = None
     if os.path.exists(PMC_JSON) and world == 1 and args.samples_per_gpu == SAMPLES_PER_GPU:
         with open(PMC_JSON) as f:
             traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
     units = count_local * traj.H
-    flops = (FLOPS_PER_ROLLOUT_STEP if lane else FLOPS_DYN_PER_ROLLOUT_STEP) * units
+    flops_unit = FLOPS_DYN_PER_ROLLOUT_STEP if records else FLOPS_PER_ROLLOUT_STEP
+    flops = flops_unit * units
     achieved_tflops = flops / (dyn_ms * 1e-3) / 1e12
     if rank != 0:
         if dist:
@@ -179,14 +182,14 @@ def main():
         "kernel_ms": {"rollout_dynamics": dyn_ms, "rollout_cost": cost_ms, "breakdown_untimed": {
                       "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]}},
         "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
-                     "kernel": "fr_rollout_kernel" if lane else "fr_coop_x_kernel", "achieved": achieved_tflops,
+                     "kernel": "fr_rollout_kernel" if lane else ("fr_coop_x_kernel" if records else "fr_coop_xc_kernel"), "achieved": achieved_tflops,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
                      "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
-                     "flops_per_rollout_step": FLOPS_PER_ROLLOUT_STEP if lane else FLOPS_DYN_PER_ROLLOUT_STEP},
-        "hbm": {"rollout_algorithmic_GBs": (BYTES_EPS_PER_ROLLOUT_STEP if lane else BYTES_PER_ROLLOUT_STEP) * units
+                     "flops_per_rollout_step": flops_unit},
+        "hbm": {"rollout_algorithmic_GBs": (BYTES_PER_ROLLOUT_STEP if records else BYTES_EPS_PER_ROLLOUT_STEP) * units
                 / (dyn_ms * 1e-3) / 1e9,
-                "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if cost_ms > 0 else None,
+                "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if records and cost_ms > 0 else None,
                 "peak_GBs": HBM_PEAK_GBS},
     }
     if not args.no_cpu_baseline:

@@ -16,4 +16,4 @@ run flops SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 S
 run fetch FETCH_SIZE GRBM_GUI_ACTIVE && \
 run write WRITE_SIZE && \
 for n in sq lat flops fetch write; do python3 tools/pmc_summary.py $D/${n}_counter_collection.csv > $D/${n}_summary.txt; done && \
-cat $D/*_summary.txt | grep -E 'coop|step_cost|sample_kernel|rank_|gradient_kernel'
+cat $D/*_summary.txt | grep -E 'coop|step_cost|sample_kernel|rank_|gradient|finish'
