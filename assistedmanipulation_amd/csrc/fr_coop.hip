@@ -60,14 +60,31 @@ constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 stor
 // (row-uniform, per body), qdd and tau per body.
 // Row strides are 128 B modulo 256 B: ds_read_b64 serves lanes 0..31 (rows 0, 1) and 32..63 in
 // one bank cycle each with bank (a/4) mod 64, so rows 0/1 (2/3) must sit half a bank sweep apart.
+// Per-lane strides of the arrays that every lane of a row writes at once (mass-matrix rows, S
+// slots) are 144 B and 80 B: their 16-byte stores then start at 36 j and 20 j (mod 64) dwords,
+// sixteen disjoint four-bank groups per row.  With 128 B / 64 B strides the lanes of a row fell
+// on two / four bank groups (8- / 4-way conflicts on the solve's transpose and the S stores).
+#ifdef LDS_NOPAD
+constexpr int CSTR = ROW;
 constexpr int L_I = 0;
-constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x ROW) over L_I
-constexpr int L_TP = L_COL + 16 * ROW;      // no tank: the solved right-hand side (12)
+constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x CSTR) over L_I
+constexpr int L_TP = L_COL + 16 * CSTR;     // no tank: the solved right-hand side (12)
 constexpr int L_S = 274;                    // 16-byte aligned; per slot S (6), qd, pad
 constexpr int S_STR = 8;
 constexpr int LDS_KIN = 400;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
 constexpr int L_F = 378;                    // energy tank: spatial force f of each body slot
 constexpr int LDS_KIN_EN = 464;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
+#else
+constexpr int CSTR = 18;
+constexpr int L_I = 0;
+constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x CSTR) over L_I
+constexpr int L_TP = L_COL + 16 * CSTR;     // no tank: the solved right-hand side (12)
+constexpr int L_S = 300;                    // 16-byte aligned; per slot S (6), qd, pad
+constexpr int S_STR = 10;
+constexpr int LDS_KIN = 432;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
+constexpr int L_F = 430;                    // energy tank: spatial force f of each body slot
+constexpr int LDS_KIN_EN = 528;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
+#endif
 constexpr int L_U = 0;
 constexpr int L_DU = L_U + FR_NB * ROW;
 constexpr int L_QDD = L_DU + FR_NB * 2;
@@ -1044,14 +1061,14 @@ __device__ __forceinline__ double coop_solve(int j, const CoopBody &bd, double t
     }
     Mc[11] = (j == 11) ? diag : 0.0;
     // row j of the block: column j's entries (upper part valid) and, in slot 12, tau_j
-    double *Row = Lk + L_COL + j * ROW;
+    double *Row = Lk + L_COL + j * CSTR;
 #pragma unroll
     for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Row + i) = double2{Mc[i], Mc[i + 1]};
     Row[12] = tau_l;
     // below the diagonal: M_ij = M_ji, written by lane i; lane 12 reads the tau column
 #pragma unroll
     for (int i = 0; i < 12; i++) {
-        const double x = Lk[L_COL + i * ROW + j];
+        const double x = Lk[L_COL + i * CSTR + j];
         Mc[i] = (i > j || j == 12) ? x : Mc[i];
     }
 #ifdef PHASE_TRACE
