@@ -304,6 +304,54 @@ __device__ __forceinline__ double frcp(double d)
     return __builtin_fma(r, __builtin_fma(e, e, e), r);
 }
 
+// b on the lanes whose mask m is all ones, a on the lanes where it is zero (m: a loop-invariant
+// per-lane mask in a VGPR, made opaque where it is built).  One v_bfi_b32 per dword and no compare:
+// C++ selects on the row index were compares per use, and LLVM turns a select whose operand is a
+// load or a division into a branch - the step was ~40 basic blocks (exec-mask scaffolding that
+// takes issue slots at one wave per SIMD, and scheduling regions the chains could not cross).
+__device__ __forceinline__ double msel(int m, double a, double b)
+{
+    int lo, hi;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"(m), "v"(__double2loint(b)), "v"(__double2loint(a)));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hi) : "v"(m), "v"(__double2hiint(b)), "v"(__double2hiint(a)));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int opaque_mask(bool c)
+{
+    int m = c ? -1 : 0;
+    asm volatile("" : "+v"(m));
+    return m;
+}
+
+// sin and cos of a joint angle, branch-free (the library sincos branches to a Payne-Hanek
+// reduction for |x| >= 2^30, which ended the step's last scheduling region).  Valid for
+// |x| < 2^26: k = rint(2x / pi), r = x - k pi/2 with pi/2 in two parts (the first FMA is exact
+// for these k), fdlibm's __kernel_sin / __kernel_cos polynomials on [-pi/4, pi/4] (< 1 ulp), and
+// the quadrant by selects and a sign flip.  Joint angles are O(10); inf / NaN give NaN as sin does.
+__device__ __forceinline__ void fsincos(double x, double *sp, double *cp)
+{
+    const double k = __builtin_rint(x * 0.63661977236758134308);
+    double r = __builtin_fma(-k, 1.5707963267948966, x);
+    r = __builtin_fma(-k, 6.123233995736766e-17, r);
+    const double z = r * r;
+    const double ps = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                      __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                      2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
+                      -1.66666666666666324348e-01);
+    const double s = __builtin_fma(r * z, ps, r);
+    const double pc = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                      __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                      -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
+                      4.16666666666666019037e-02);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + (z * z) * pc);
+    const int n = (int)k;
+    const bool swap = (n & 1) != 0;
+    const double sv = swap ? c : s, cv = swap ? s : c;
+    *sp = __hiloint2double(__double2hiint(sv) ^ (int)((unsigned)(n & 2) << 30), __double2loint(sv));
+    *cp = __hiloint2double(__double2hiint(cv) ^ (int)((unsigned)((n + 1) & 2) << 30), __double2loint(cv));
+}
+
 // ---- BEGIN generated by tools/gen_gj.py: mass-matrix solve helpers ----
 // m[i] = S_i . F for i = 0..10, S_i broadcast from lane i: eleven chains of six, round-robin
 __device__ __forceinline__ void column_dots(const double *S, const double *F, double *m)
@@ -760,6 +808,12 @@ struct LaneConst {
     bool is_rz;
     int ka, kb;     // kinematic sum min(j, 8): S component x, y slot (S component or qd)
     bool vsum;      // the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
+    // opaque lane masks (0 / -1) for msel, built once before the horizon loop
+    int m_vsum;     // vsum
+    int m_j0, m_j1, m_j2, m_j10, m_j12, m_j13, m_j14, m_j15;   // j == n
+    int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
+    int m_live;     // j < 12: the lane owns a body
+    int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
@@ -898,7 +952,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 #pragma unroll
     for (int i = 0; i <= FR_EE_PARENT; i++) {
         double y = ys[i * S_STR];
-        if (i < FR_ARM0) y = L.vsum ? y : 0.0;
+        if (i < FR_ARM0) y = msel(L.m_vsum, 0.0, y);
         acc = __builtin_fma(xs[i * S_STR], y, acc);
     }
     kin.ks = acc;
@@ -1024,7 +1078,8 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 //                       LDS.  Lane 12 holds the right-hand side tau.
 //   Gauss-Jordan        twelve pivots, each one broadcast of the pivot, a reciprocal and eleven
 //                       broadcast FMAs per lane; then qdd_j = tau'_j / M'_jj.
-__device__ __forceinline__ double coop_solve(int j, const CoopBody &bd, double tau_l, double *Lk, uint64_t &t_mid)
+__device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const CoopBody &bd, double tau_l, double *Lk,
+                                             uint64_t &t_mid)
 {
     double v[10] = {bd.m, bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
     double own[10];
@@ -1039,7 +1094,7 @@ __device__ __forceinline__ double coop_solve(int j, const CoopBody &bd, double t
 #pragma unroll
     for (int k = 0; k < 10; k++) v[k] += shl<8>(v[k]);
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] = (j == 10) ? own[k] : v[k];
+    for (int k = 0; k < 10; k++) v[k] = msel(L.m_j10, v[k], own[k]);
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
     const double m = v[0], h0 = v[1], h1 = v[2], h2 = v[3];
@@ -1054,38 +1109,38 @@ __device__ __forceinline__ double coop_solve(int j, const CoopBody &bd, double t
     double Mc[12];
     column_dots(S, F, Mc);
     const double diag = ((S[0] * F[0] + S[1] * F[1]) + (S[2] * F[2] + S[3] * F[3])) + (S[4] * F[4] + S[5] * F[5]);
+    // strictly-upper part of column j: M_ij for the ancestors i of j (finger 11 hangs off body 9,
+    // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column
 #pragma unroll
-    for (int i = 0; i < 11; i++) {
-        const bool anc = i < j && !(j == FR_NB - 1 && i == FR_NB - 2);   // finger 11 hangs off body 9
-        Mc[i] = anc ? Mc[i] : ((i == j) ? diag : 0.0);
-    }
-    Mc[11] = (j == 11) ? diag : 0.0;
-    // row j of the block: column j's entries (upper part valid) and, in slot 12, tau_j
+    for (int i = 0; i < 11; i++) Mc[i] = msel(__builtin_amdgcn_sbfe(L.anc, i, 1), 0.0, Mc[i]);
+    Mc[11] = 0.0;
+    // row j of the block: that column, then tau_j and zeros in slots 12..15, then the diagonal over
+    // slot j (LDS stores of a wave land in order).  Entry (i, j) of the block is then column i's
+    // row-j entry: M_ji = M_ij below the diagonal, the diagonal, and zero above it - so column j is
+    // its strictly-upper part plus a read of block column j, with no select; lane 12 reads the
+    // right-hand side tau, lanes 13..15 zeros.
     double *Row = Lk + L_COL + j * CSTR;
 #pragma unroll
     for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Row + i) = double2{Mc[i], Mc[i + 1]};
-    Row[12] = tau_l;
-    // below the diagonal: M_ij = M_ji, written by lane i; lane 12 reads the tau column
+    *reinterpret_cast<double2 *>(Row + 12) = double2{tau_l, 0.0};
+    *reinterpret_cast<double2 *>(Row + 14) = double2{0.0, 0.0};
+    Row[j] = diag;
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-        const double x = Lk[L_COL + i * CSTR + j];
-        Mc[i] = (i > j || j == 12) ? x : Mc[i];
-    }
+    for (int i = 0; i < 12; i++) Mc[i] += Lk[L_COL + i * CSTR + j];
 #ifdef PHASE_TRACE
     t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
 #endif
     gj_pivot_0(Mc); gj_pivot_1(Mc); gj_pivot_2(Mc); gj_pivot_3(Mc); gj_pivot_4(Mc); gj_pivot_5(Mc);
     gj_pivot_6(Mc); gj_pivot_7(Mc); gj_pivot_8(Mc); gj_pivot_9(Mc); gj_pivot_10(Mc); gj_pivot_11(Mc);
-    // the matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj, tau' on lane 12
-    if (j == 12) {
+    // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
+    // tau' at L_TP and every other lane its column in its own block row (read above, dead now), so
+    // lane j reads M'_jj back at slot j of that row: no per-lane register select, no branch.
+    double *dst = (j == 12) ? Lk + L_TP : Row;
 #pragma unroll
-        for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Lk + L_TP + i) = double2{Mc[i], Mc[i + 1]};
-    }
-    double dj = Mc[0];
-#pragma unroll
-    for (int i = 1; i < 12; i++) dj = (j == i) ? Mc[i] : dj;
+    for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(dst + i) = double2{Mc[i], Mc[i + 1]};
     const double tp = Lk[L_TP + (j < FR_NB ? j : 0)];
-    return j < FR_NB ? tp / dj : 0.0;   // lanes 12..15 keep q = qd = 0
+    const double dj = Row[j];
+    return msel(L.m_live, 0.0, tp * frcp(dj));   // lanes 12..15 keep q = qd = 0
 }
 
 }  // namespace
@@ -1145,15 +1200,19 @@ __device__ __forceinline__ double vreg(double x)
     asm("" : "+v"(x));   // not volatile: a volatile asm would end the scheduling region here
     return x;
 }
-__device__ __forceinline__ void store_record(double *rp, int j, double q, double qd, const CoopKin &kin, double E)
+__device__ __forceinline__ void store_record(double *rp, int j, const LaneConst &L, double q, double qd, const CoopKin &kin,
+                                             double E)
 {
 #ifdef ABL_NOREC
     return;
 #endif
-    const double e0 = vreg(kin.ee[0]), e1 = vreg(kin.ee[1]), e2 = vreg(kin.ee[2]);
-    const double m0 = vreg(kin.am[0]), m1 = vreg(kin.am[1]), m2 = vreg(kin.am[2]);
-    const double a0 = (j < 12) ? q : (j == 12) ? e0 : (j == 13) ? e2 : (j == 14) ? m1 : E;
-    const double a1 = (j < 12) ? qd : (j == 12) ? e1 : (j == 13) ? m0 : (j == 14) ? m2 : 0.0;
+    double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
+    a0 = msel(L.m_j13, a0, kin.ee[2]);
+    a1 = msel(L.m_j13, a1, kin.am[0]);
+    a0 = msel(L.m_j14, a0, kin.am[1]);
+    a1 = msel(L.m_j14, a1, kin.am[2]);
+    a0 = msel(L.m_j15, a0, E);
+    a1 = msel(L.m_j15, a1, 0.0);
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
     rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
 }
@@ -1245,13 +1304,30 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         L.kb = (int)((0x221210666ull >> (4 * m)) & 0xF);
         L.vsum = m < 3;
     }
+    L.m_vsum = opaque_mask(L.vsum);
+    L.m_j0 = opaque_mask(j == 0);
+    L.m_j1 = opaque_mask(j == 1);
+    L.m_j2 = opaque_mask(j == 2);
+    L.m_j10 = opaque_mask(j == 10);
+    L.m_j12 = opaque_mask(j == 12);
+    L.m_j13 = opaque_mask(j == 13);
+    L.m_j14 = opaque_mask(j == 14);
+    L.m_j15 = opaque_mask(j == 15);
+    L.m_tau = opaque_mask(j >= 3 && j < 10);
+    L.m_live = opaque_mask(jl);
+    {
+        int anc = (1 << (j < 11 ? j : 11)) - 1;   // bodies i < j
+        if (j == FR_NB - 1) anc &= ~(1 << (FR_NB - 2));   // finger 11 is not under finger 10
+        asm volatile("" : "+v"(anc));
+        L.anc = anc;
+    }
 
     double q = jl ? x0p[jb] : 0.0;
     double qd = jl ? x0p[FR_NB + jb] : 0.0;
     double E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
     const double *grav = a.model->gravity;
     double sq, cq;
-    sincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
+    fsincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
     coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
@@ -1264,7 +1340,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     asm volatile("" : "+v"(nstride));
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
 #ifdef NO_EPS_PREFETCH
-    store_record(recp(0), j, q, qd, kin, E);
+    store_record(recp(0), j, L, q, qd, kin, E);
     after_record(0);
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[(int64_t)k * nstride];
@@ -1275,7 +1351,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[0], ub_n = Up[jb];
-    store_record(recp(0), j, q, qd, kin, E);
+    store_record(recp(0), j, L, q, qd, kin, E);
     after_record(0);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
@@ -1300,7 +1376,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             const double u0 = bcast<0>(u), u1 = bcast<1>(u);
             const double vx = c * u0 + (-s) * u1;
             const double vy = s * u0 + c * u1;
-            qd = (j == 0) ? vx : ((j == 1) ? vy : ((j == 2) ? u : qd));
+            qd = msel(L.m_j0, msel(L.m_j1, msel(L.m_j2, qd, u), vy), vx);
         }
 #ifndef OLD_ABA
         if constexpr (EN)
@@ -1328,7 +1404,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #else
         double qdd;
         if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe, t_bwd);
-        else qdd = coop_solve(j, bd, (j >= 3 && j < 10) ? u : 0.0, Lk, t_bwd);
+        else qdd = coop_solve(j, L, bd, msel(L.m_tau, 0.0, u), Lk, t_bwd);
 #endif
 #endif
 #ifdef PHASE_TRACE
@@ -1343,12 +1419,12 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
             const double power = bsum<0, FR_NB>(tau_l * qd + kin.pw, 1.0) + a.dt * bsum<0, 6>(pe, 1.0);
             E = smax(0.0, E + power * a.dt);
         }
-        store_record(recp(k + 1), j, q, qd, kin, E);
+        store_record(recp(k + 1), j, L, q, qd, kin, E);
 #ifdef ABL_SINCOS
         sq = q - q * q * q * (1.0 / 6.0);
         cq = 1.0 - q * q * 0.5;
 #else
-        sincos(q, &sq, &cq);
+        fsincos(q, &sq, &cq);
 #endif
         after_record(k + 1);   // RING: a complete batch of records -> their step costs
 #ifdef PHASE_TRACE
