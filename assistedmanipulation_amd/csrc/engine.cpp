@@ -109,10 +109,10 @@ struct mppi_handle {
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
+    double *d_wexp = nullptr, *d_wpart = nullptr;   // large-R softmin scratch (kernels.hip SM_LARGE_R)
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
-    bool fuse_cost = false;   // MPPI_COST_KERNEL=fused: costs inside the rollout launch (LDS record rings; slower)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
     size_t inj_capacity = 0;   // doubles
@@ -458,8 +458,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     {
         const char *kv = std::getenv("MPPI_FR_KERNEL");
         h->coop = !(kv && std::string(kv) == "lane");
-        const char *cv = std::getenv("MPPI_COST_KERNEL");   // A/B: "fused" = step costs in the rollout launch
-        h->fuse_cost = cv && std::string(cv) == "fused";
     }
     noise_transform((int)Cd, cfg->covariance, h->T, h->tdiag);
     if (h->H < 1 || h->H > (1 << 20)) { delete h; return fail(nullptr, MPPI_ERR_INVALID, "horizon steps out of range"); }
@@ -498,6 +496,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
+    CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_wpart, 4 * 64));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
     CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_NREC)));
@@ -1132,12 +1132,11 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         }
         bool folded = false;
         if (use_coop(h)) {
-            bool costs_done = false;   // the rollout launch evaluated the costs as well
-            HIP_TRY(launch_fr_coop_update(a, h->stream, h->fuse_cost, ev_in_launch ? h->ev[1] : nullptr,
-                                          ev_in_launch ? h->ev_dyn : nullptr, &folded, &costs_done));
+            HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? h->ev[1] : nullptr,
+                                          ev_in_launch ? h->ev_dyn : nullptr, &folded));
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
-            if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
             if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
@@ -1222,6 +1221,8 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.H = (int)h->H;
     w.C = (int)h->C;
     w.gsplit = h->d_gsplit;
+    w.wexp = h->d_wexp;
+    w.wpart = h->d_wpart;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_weights_gradient(w, h->d_gpart, h->world > 1, h->stream));
     return MPPI_OK;

@@ -1218,48 +1218,14 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
 }
 static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC_JJ == 35 && FR_NREC == 42, "record layout");
 
-// ---- step costs inside the update's launch (no energy tank) ---------------------------------
-// The wave keeps its rows' step records in a ring of CB steps in LDS instead of HBM, and after
-// every CB steps (and after the last) evaluates the objective on the batch, one lane per record:
-// lane (r, s) = (lane / 16, lane % 16) takes step base + s of its own row r (52 of 64 lanes work).
-// The step costs are added in step order (the reference's J += cost, mppi.cpp:322-337) with the
-// association fr_step_cost_kernel uses.  The batch runs at the end of a step, when the eps
-// prefetched at its top has long landed.
-constexpr int CB = 13;                                 // ring steps = batch
-constexpr int RING_W = CB * ROWS_PER_WAVE * FR_NREC;   // doubles per wave
-static_assert(CB <= ROW, "a lane per record of a batch");
-
-// steps base .. base + n - 1 of the wave's four rows: their step costs added to Jw[row] in order
-template <int CK>
-__device__ __forceinline__ void batch_cost(const FrRolloutArgs &a, const double *ring, int lane, bool frow, int base, int n,
-                                           double (&Jw)[ROWS_PER_WAVE])
-{
-    const int r = lane >> 4, s = lane & (ROW - 1);
-    const bool on = s < n;
-    const int ss = on ? s : 0;
-    double rec[FR_NREC];
-    const double2 *src = reinterpret_cast<const double2 *>(ring + (ss * ROWS_PER_WAVE + r) * FR_NREC);
-#pragma unroll
-    for (int i = 0; i < FR_NREC / 2; i++) {
-        const double2 v = src[i];
-        rec[2 * i] = v.x;
-        rec[2 * i + 1] = v.y;
-    }
-    const StepConst *stp = frow ? a.fsteps : a.steps;
-    const double c = on ? mppi_cost::step_cost<CK, false>(*a.cost, stp[base + ss], rec) : 0.0;
-#pragma unroll
-    for (int i = 0; i < ROWS_PER_WAVE; i++)
-        for (int t = 0; t < n; t++) Jw[i] += mppi_cost::readlane_f64(c, i * ROW + t);
-}
-
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / frec).  The
 // costs are not summed here: every step's record goes to HBM and fr_step_cost_kernel evaluates
 // the objective for all (rollout, step) pairs at once, a lane each, instead of 16 lanes of a row
 // repeating its row-uniform terms.
-template <int CK, bool EN, bool FROW, bool RING = false>
+template <int CK, bool EN, bool FROW>
 __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
-                                          const double *Lmodel, double *ring = nullptr)
+                                          const double *Lmodel)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1281,17 +1247,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     const double *x0p = FROW && frow ? a.fx0 : a.x0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
     double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_NREC;   // [rollout][step][FR_NREC]
-    // record k: HBM, or slot k mod CB of the wave's ring (RING)
-    auto recp = [&](int k) -> double * {
-        if constexpr (RING) return ring + ((k % CB) * ROWS_PER_WAVE + (lane >> 4)) * FR_NREC;
-        else return rp + (int64_t)k * FR_NREC;
-    };
-    double Jw[ROWS_PER_WAVE] = {0.0, 0.0, 0.0, 0.0};   // RING: the rows' costs so far
-    auto after_record = [&](int k) {
-        if constexpr (RING) {
-            if ((k + 1) % CB == 0 || k + 1 == H) batch_cost<CK>(a, ring, lane, frow, k - k % CB, k % CB + 1, Jw);
-        }
-    };
+    auto recp = [&](int k) -> double * { return rp + (int64_t)k * FR_NREC; };
     const bool jl = j < FR_NB;   // lane owns a body / control component
     const int jb = jl ? j : 0;
     const double *M = Lmodel + (jl ? j : FR_NB) * MB;
@@ -1341,7 +1297,6 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
 #ifdef NO_EPS_PREFETCH
     store_record(recp(0), j, L, q, qd, kin, E);
-    after_record(0);
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[(int64_t)k * nstride];
         const double ub_l = Up[k * FR_C + jb];
@@ -1352,7 +1307,6 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[0], ub_n = Up[jb];
     store_record(recp(0), j, L, q, qd, kin, E);
-    after_record(0);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
 #endif
@@ -1426,7 +1380,6 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #else
         fsincos(q, &sq, &cq);
 #endif
-        after_record(k + 1);   // RING: a complete batch of records -> their step costs
 #ifdef PHASE_TRACE
         const uint64_t t_end = stamp(sq);
         ph[3] += t_end - t_fwd;
@@ -1434,15 +1387,6 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #endif
     }
     // the final step's dynamics are never observed (deviation 5)
-    if constexpr (RING) {
-        const int r = lane >> 4;
-        const double Jr = r == 0 ? Jw[0] : (r == 1 ? Jw[1] : (r == 2 ? Jw[2] : Jw[3]));
-        const double Jc = isnan(Jr) ? (double)NAN : Jr;   // the reference's quiet NaN
-        if (j == 0) {
-            if (!frow) a.cost_out[a.begin + lr] = Jc;
-            else if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = Jc;   // no filter() after a throw
-        }
-    }
 #ifdef PHASE_TRACE
     if (a.trace && lane == 0 && !FROW)
         for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)ph[i];
@@ -1507,32 +1451,6 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
-// The update's launch without the energy tank: fr_coop_x_kernel with the step costs evaluated in
-// the launch from LDS record rings (batch_cost), so the records never reach HBM and the cost kernel
-// is not launched.
-template <int CK>
-__global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_xc_kernel(FrRolloutArgs a)
-{
-    __shared__ double lds_kin[5 * ROWS_PER_WAVE * LDS_KIN];
-    __shared__ double ring[5 * RING_W];
-    __shared__ double Lmodel[LDS_MODEL];
-    const int wv = (int)(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int rowi = lane >> 4;
-    const int wrow = wv * ROWS_PER_WAVE + rowi;
-    stage_body_table(a, Lmodel, 320);
-    __syncthreads();
-    double *Lk = lds_kin + wrow * LDS_KIN, *rg = ring + wv * RING_W;
-    if (wv < 4) {
-        const int wblk = blockIdx.x * 4 + wv;
-        coop_rows<CK, false, false, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, nullptr, Lmodel, rg);
-    } else if ((int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows) {
-        const int wblk = gridDim.x * 4 + blockIdx.x;
-        coop_rows<CK, false, true, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, nullptr, Lmodel,
-                                         rg);
-    }
-}
-
 namespace mppi_eng {
 
 static unsigned g_cu_count = 256;   // set by fr_coop_set_cu_count (hipDeviceProp multiProcessorCount)
@@ -1566,13 +1484,6 @@ static void launch_x(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
     hipLaunchKernelGGL((fr_coop_x_kernel<CK, EN>), dim3(nb), dim3(320), pad, s, a);
 }
 
-template <int CK>
-static void launch_xc(const FrRolloutArgs &a, unsigned nb, hipStream_t s, hipEvent_t e0, hipEvent_t e1)
-{
-    static const unsigned pad = one_per_cu_pad(fr_coop_xc_kernel<CK>, 5);
-    hipExtLaunchKernelGGL((fr_coop_xc_kernel<CK>), dim3(nb), dim3(320), pad, s, e0, e1, 0u, a);
-}
-
 template <int WPB, bool FROW>
 static void launch_one(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
@@ -1589,16 +1500,12 @@ hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
-// The update's rollouts.  fuse_cost: without the energy tank the launch evaluates the step costs
-// too (*costs_done).  e0 / e1 (may be null): timing events around the rollout launch; the fused
-// launch carries them in its dispatch (hipExtLaunchKernelGGL), so they add no gap.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, bool fuse_cost, hipEvent_t e0, hipEvent_t e1,
-                                 bool *folded, bool *costs_done)
+// The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     *folded = false;
-    *costs_done = false;
     // the previous update's filter() rides along when there are extra rows anyway (the fifth wave
     // of the first workgroup has room); alone it would add a wave, so then it stays pending
     const bool frow = a0.fcost != nullptr && extra > 0;
@@ -1615,12 +1522,6 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, bool fu
     a.xbase = groups * WG_ROWS;
     a.xrows = xrows;
     *folded = frow;
-    if (fuse_cost && !a.energy) {   // rollouts and their costs in one launch
-        if (a.cost_kind == CK_TRACK_POINT) launch_xc<CK_TRACK_POINT>(a, (unsigned)groups, s, e0, e1);
-        else launch_xc<CK_ASSISTED_MANIPULATION>(a, (unsigned)groups, s, e0, e1);
-        *costs_done = true;
-        return hipGetLastError();
-    }
     if (e0) (void)hipEventRecord(e0, s);
     if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
     else if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, (unsigned)groups, s);

@@ -851,7 +851,91 @@ constexpr int WU = 8;        // costs per (virtual) thread and pass
 constexpr int NV = WV / 4;   // virtual waves per real wave
 constexpr int GR = 2;        // rollouts per thread whose eps is loaded up front
 
-template <int C>
+// Large R (R > SM_LARGE_R, configs 4 / 5: every rank weighs all R global costs): recomputing
+// min / max / normaliser over all R in each of the H x GRAD_SPLIT blocks costs O(H R) exps, so
+// the reductions run once, in two small launches over SM_NB contiguous chunks:
+//   softmin_minmax_kernel   chunk b's min / max / count of the non-NaN costs -> wpart[0..3 NB)
+//   softmin_exp_kernel      every block folds the NB partials in one fixed order (same bits in
+//                           every block), then writes e_r = exp(-lambda (c_r - min) / (max - min))
+//                           of its chunk to wexp and the chunk's sum to wpart[3 NB + b]
+// and weights_gradient_kernel<C, true> folds the NB sums the same way for the normaliser and
+// reads e_r instead of recomputing it.
+constexpr int SM_NB = 64;
+constexpr int64_t SM_LARGE_R = 16384;
+
+__device__ __forceinline__ void sm_chunk(int64_t R, int b, int64_t &r0, int64_t &r1)
+{
+    const int64_t cs = (R + SM_NB - 1) / SM_NB;
+    r0 = (int64_t)b * cs;
+    r1 = (r0 + cs < R) ? r0 + cs : R;
+}
+
+// the NB chunk partials folded by the first wave (lane b holds chunk b): min, max, count [, sum]
+__device__ __forceinline__ void sm_fold(const double *wpart, int l, bool with_sum, double &mn, double &mx, double &cn,
+                                        double &sm)
+{
+    static_assert(SM_NB == 64, "one partial per lane");
+    mn = wave_min(wpart[l]);
+    mx = wave_max(wpart[SM_NB + l]);
+    cn = wave_sum(wpart[2 * SM_NB + l]);
+    sm = with_sum ? wave_sum(wpart[3 * SM_NB + l]) : 0.0;
+}
+
+__global__ __launch_bounds__(256) void softmin_minmax_kernel(WGradArgs a)
+{
+    __shared__ double smn[4], smx[4], scn[4];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    int64_t r0, r1;
+    sm_chunk(a.R, blockIdx.x, r0, r1);
+    double mn = INFINITY, mx = -INFINITY, cn = 0.0;
+    for (int64_t r = r0 + t; r < r1; r += 256) {
+        const double c = a.cost[r];
+        const bool ok = !isnan(c);
+        cn += ok ? 1.0 : 0.0;
+        mn = (ok && c < mn) ? c : mn;
+        mx = (ok && c > mx) ? c : mx;
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    cn = wave_sum(cn);
+    if (l == 0) { smn[w] = mn; smx[w] = mx; scn[w] = cn; }
+    __syncthreads();
+    if (t == 0) {
+        a.wpart[blockIdx.x] = smin(smin(smn[0], smn[1]), smin(smn[2], smn[3]));
+        a.wpart[SM_NB + blockIdx.x] = smax(smax(smx[0], smx[1]), smax(smx[2], smx[3]));
+        a.wpart[2 * SM_NB + blockIdx.x] = (scn[0] + scn[1]) + (scn[2] + scn[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
+{
+    __shared__ double sfold[3], ssum[4];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    if (w == 0) {
+        double mn, mx, cn, sm;
+        sm_fold(a.wpart, l, false, mn, mx, cn, sm);
+        if (l == 0) { sfold[0] = mn; sfold[1] = mx; sfold[2] = cn; }
+    }
+    __syncthreads();
+    const double minimum = sfold[0], maximum = sfold[1], valid = sfold[2];
+    if (valid <= 1.0 || maximum - minimum < 1e-6) return;   // weights_gradient_kernel reports it
+    const double difference = maximum - minimum;
+    int64_t r0, r1;
+    sm_chunk(a.R, blockIdx.x, r0, r1);
+    double acc = 0.0;
+    for (int64_t r = r0 + t; r < r1; r += 256) {
+        const double c = a.cost[r];
+        const double e = isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference);
+        a.wexp[r] = e;
+        acc += e;
+    }
+    acc = wave_sum(acc);
+    if (l == 0) ssum[w] = acc;
+    __syncthreads();
+    if (t == 0) a.wpart[3 * SM_NB + blockIdx.x] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
+}
+
+template <int C, bool LARGE>
 __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
     __shared__ double red[256 * C];
@@ -869,6 +953,19 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 #pragma unroll
         for (int c = 0; c < C; c++) ne[m][c] = n[c];
     }
+    double minimum, maximum, valid, total;
+    if constexpr (LARGE) {
+        if (rw == 0) {
+            double mn, mx, cn, sm;
+            sm_fold(a.wpart, l, true, mn, mx, cn, sm);
+            if (l == 0) { smn[0] = mn; smx[0] = mx; ssum[0] = cn; ssum[1] = sm; }
+        }
+        __syncthreads();
+        minimum = smn[0];
+        maximum = smx[0];
+        valid = ssum[0];
+        total = ssum[1];
+    } else {
     // min / max / count over the non-NaN costs
     double mn[NV], mx[NV], cn[NV];
 #pragma unroll
@@ -907,7 +1004,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         }
     }
     __syncthreads();
-    double minimum = smn[0], maximum = smx[0], valid = ssum[0];
+    minimum = smn[0];
+    maximum = smx[0];
+    valid = ssum[0];
 #pragma unroll
     for (int i = 1; i < WV; i++) {
         minimum = smin(minimum, smn[i]);
@@ -915,6 +1014,8 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         valid += ssum[i];
     }
     __syncthreads();
+    total = 0.0;
+    }
     const bool lead = k == 0 && s == 0 && t == 0;
     Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
@@ -927,6 +1028,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         return;
     }
     auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
+    // e_r of global rollout i: recomputed, or (LARGE) written by softmin_exp_kernel
+    auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
+    if constexpr (!LARGE) {
     double tot[NV];
 #pragma unroll
     for (int v = 0; v < NV; v++) tot[v] = 0.0;
@@ -953,13 +1057,14 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         if (l == 0) ssum[NV * rw + v] = sv;
     }
     __syncthreads();
-    double total = ssum[0];
+    total = ssum[0];
 #pragma unroll
     for (int i = 1; i < WV; i++) total += ssum[i];
+    }
     {   // this block's slice of the weights
         const int64_t nb = (int64_t)gridDim.x * ns, b = (int64_t)s * gridDim.x + k;
         const int64_t wc = (R + nb - 1) / nb, w0 = b * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
-        for (int64_t i = w0 + t; i < w1; i += 256) a.weights[i] = expw(a.cost[i]) / total;
+        for (int64_t i = w0 + t; i < w1; i += 256) a.weights[i] = wexp(i) / total;
     }
     if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; st->total = total; }
     double acc[C];
@@ -969,13 +1074,13 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
         if (r < r1) {
-            const double wr = expw(a.cost[a.begin + r]) / total;
+            const double wr = wexp(a.begin + r) / total;
 #pragma unroll
             for (int c = 0; c < C; c++) acc[c] += wr * ne[m][c];
         }
     }
     for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
-        const double wr = expw(a.cost[a.begin + r]) / total;
+        const double wr = wexp(a.begin + r) / total;
         const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] += wr * n[c];
@@ -1168,6 +1273,201 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
 
 
 
+// finish() with the Savitzky-Golay filter (configs[4]), one wave per control dimension with its
+// MovingExtendedWindow (filter.cpp:19-116) staged in LDS.  finish_block runs the reference's loops
+// literally on one thread per dimension over global memory: its add_measurement refills the whole
+// window tail per step (O(H W) stores) and apply() binary-searches per step, 0.89 ms at H = 128.
+// Here, per dimension:
+//   trim(t0)        first index >= t0 by ballots; the left rotation (tail repeating the last kept
+//                   element) as one gather new[i] = old[min(i + offset, W - 1)].
+//   add_measurement the window's final state in one pass: uu[w + k] = U*_k, tt[w + k] = t_k, and
+//                   the last measurement repeated past w + H (the reference's successive fills).
+//                   Its "older than the new time" check cannot fire: t_k = t0 + k dt is monotone
+//                   and trim just set tt[w] = t0.
+//   apply           with lower_bound(t_k) = w + k for every k (checked: tt[w + k - 1] < t_k), step
+//                   k reads uu[k .. k + 2w] and then writes its output over uu[w + k - 1].  Terms
+//                   j >= w - 1 are measurements or old history no step has overwritten yet, so
+//                   P_k = sum_{j >= w-1} wt_j uu[k + j] is formed for all k at once; the rest is the
+//                   order-(w-1) recurrence res_k = P_k + sum_{j < w-1} wt_j z(k + j), with z(p) the
+//                   output written at p (res_{p-w+1}) or, before the first, the old history uu[p].
+//                   Any other lower_bound pattern falls back to the literal loop in LDS.
+// Sums are associated differently from the reference's left-to-right loop (rounding only).
+constexpr int SGK_MAXW = 384;   // largest window W = H + 2w + 1 this kernel stages (else finish_kernel)
+
+__device__ __forceinline__ int lds_lower_bound(const double *tt, int W, double t)
+{
+    int lo = 0, hi = W;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tt[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+constexpr int SGK_ZM = 15;   // w - 1 <= SGK_ZM: the recurrence's outputs in registers
+
+__global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
+{
+    extern __shared__ double sg_lds[];   // per dimension: uu[W], tt[W], res[H]; then wt[2w + 1]
+    __shared__ int sg_err, sg_mode[16];  // per dimension: 0 trim error, 1 literal loop, 2 recurrence
+    const Status &stt = *a.status;
+    const int H = a.H, C = a.C, HC = H * C, w = a.sg_window, W = H + 2 * w + 1, nw = 2 * w + 1;
+    const int t = threadIdx.x, c = t >> 6, l = t & 63;
+    const bool upd = !stt.early;   // optimise() returned before the filter (mppi.cpp:373-375)
+    double *wl = sg_lds + (int64_t)C * (2 * W + H);
+    if (t == 0) sg_err = 0;
+    if (t < nw) wl[t] = a.sg_weights[t];
+    if (upd) {
+        for (int i = t; i < HC; i += blockDim.x) {
+            double g;
+            if (a.ns > 0) {   // stage 2 of the gradient, fixed order
+                g = a.gsplit[i];
+                for (int k = 1; k < a.ns; k++) g += a.gsplit[(int64_t)k * HC + i];
+            } else {
+                g = a.gpart[i];
+            }
+            a.gradient[i] = g;
+            a.Ushift[i] += g * a.gradient_step;
+        }
+    }
+    __syncthreads();
+    double *uu = sg_lds + (int64_t)(c < C ? c : 0) * (2 * W + H), *tt = uu + W, *res = tt + W;
+    double *guu = a.sg_uu + (int64_t)c * W, *gtt = a.sg_tt + (int64_t)c * W;
+    const double t0 = a.t0;
+    if (upd && c < C) {   // phase 1, wave c: trim + add_measurement, then P_k or the literal loop
+        for (int i = l; i < W; i += 64) {
+            uu[i] = guu[i];
+            tt[i] = gtt[i];
+        }
+        const int start_idx = (int)a.sg_start[c];
+        if (t0 < a.sg_last_trim[c]) {   // trim: "Resetting the window back in the past." - untouched
+            if (l == 0) { sg_mode[c] = 0; sg_err = 1; }
+        } else {
+            __builtin_amdgcn_wave_barrier();
+            int trim_idx = start_idx;
+            for (int base = 0; base < start_idx; base += 64) {
+                const int i = base + l;
+                const uint64_t b = __ballot(i < start_idx && tt[i] >= t0);
+                if (b) {
+                    trim_idx = base + __builtin_ctzll(b);
+                    break;
+                }
+            }
+            const int offset = trim_idx - w;
+            if (offset > 0) {
+                double ru[SGK_MAXW / 64], rt[SGK_MAXW / 64];
+#pragma unroll
+                for (int m = 0; m < SGK_MAXW / 64; m++) {
+                    const int i = l + 64 * m, src = (i + offset < W) ? i + offset : W - 1;
+                    if (i < W) { ru[m] = uu[src]; rt[m] = tt[src]; }
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int m = 0; m < SGK_MAXW / 64; m++) {
+                    const int i = l + 64 * m;
+                    if (i < W) { uu[i] = ru[m]; tt[i] = rt[m]; }
+                }
+            }
+            for (int i = w + l; i < W; i += 64) {   // the H measurements, then the last one repeated
+                const int k = (i - w < H) ? i - w : H - 1;
+                uu[i] = a.Ushift[k * C + c];
+                tt[i] = step_time(t0, k, a.dt);
+            }
+            __builtin_amdgcn_wave_barrier();
+            bool ok = w - 1 <= SGK_ZM;   // and lower_bound(t_k) == w + k for every k
+            for (int k = l; k < H; k += 64) ok = ok && tt[w + k - 1] < step_time(t0, k, a.dt);
+            if (__ballot(!ok) == 0) {
+                for (int k = l; k < H; k += 64) {   // P_k: the terms no earlier step has overwritten
+                    double p = 0.0;
+                    for (int j = w - 1; j < nw; j++) p += wl[j] * uu[k + j];
+                    res[k] = p;
+                }
+                if (l == 0) sg_mode[c] = 2;
+            } else if (l == 0) {   // the literal loop (filter.cpp:92-110)
+                sg_mode[c] = 1;
+                for (int k = 0; k < H; k++) {
+                    const int idx = lds_lower_bound(tt, W, step_time(t0, k, a.dt));
+                    double r = wl[0] * uu[idx - w];
+                    for (int j = 1; j < nw; j++) r += wl[j] * uu[idx - w + j];
+                    a.Ushift[k * C + c] = r;
+                    uu[idx - 1] = r;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (upd && t < C && sg_mode[t] == 2) {   // phase 2, lane d of wave 0: dimension d's recurrence
+        // z: the last w - 1 window entries below the current step's P_k terms, right-aligned (the
+        // newest, output k - 1, in z[ZM - 1]); slots left of the window have weight 0
+        const int d = t, nz = w - 1;
+        double *uud = sg_lds + (int64_t)d * (2 * W + H), *resd = uud + 2 * W;
+        double z[SGK_ZM], wr[SGK_ZM];
+#pragma unroll
+        for (int j = 0; j < SGK_ZM; j++) {
+            const int q = j - (SGK_ZM - nz);   // window offset of slot j
+            wr[j] = q >= 0 ? wl[q] : 0.0;
+            z[j] = q >= 0 ? uud[q] : 0.0;      // old history uu[0 .. w - 2]
+        }
+        for (int k = 0; k < H; k++) {
+            // four partial sums: output k - 1 (slot ZM - 1) is three dependent ops from output k
+            double ac[4] = {resd[k], 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < SGK_ZM; j++) ac[j & 3] = __builtin_fma(wr[j], z[j], ac[j & 3]);
+            const double acc = (ac[0] + ac[1]) + (ac[2] + ac[3]);
+            resd[k] = acc;
+#pragma unroll
+            for (int j = 0; j + 1 < SGK_ZM; j++) z[j] = z[j + 1];
+            z[SGK_ZM - 1] = acc;
+        }
+    }
+    __syncthreads();
+    if (upd && c < C && sg_mode[c] != 0) {   // phase 3, wave c: outputs into U* and the window
+        if (sg_mode[c] == 2) {
+            for (int k = l; k < H; k += 64) {   // output k over the window at w + k - 1
+                a.Ushift[k * C + c] = res[k];
+                uu[w + k - 1] = res[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int i = l; i < W; i += 64) {
+            guu[i] = uu[i];
+            gtt[i] = tt[i];
+        }
+        if (l == 0) {
+            a.sg_start[c] = w + H;
+            a.sg_last_trim[c] = t0;
+        }
+    }
+    __syncthreads();
+    if (upd && a.control_bound) {
+        for (int i = t; i < HC; i += blockDim.x) {
+            const int cc = i % C;
+            a.Ushift[i] = smax(smin(a.Ushift[i], a.cmax[cc]), a.cmin[cc]);
+        }
+    }
+    __syncthreads();
+    // publish (mppi.cpp:178-182): U* <- U*_shifted unless the update threw
+    const int err = sg_err;
+    const bool ok = !stt.all_nan && !err;
+    for (int i = t; i < HC; i += blockDim.x) {
+        const double v = ok ? a.Ushift[i] : a.U[i];
+        if (ok) a.U[i] = v;
+        a.out[i] = v;
+    }
+    if (t < a.X) a.x0_opt[t] = a.x0[t];
+    for (int64_t i = t; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
+    if (t == 0) {
+        a.status_w->sg_error = err;
+        a.out[HC + 0] = *a.opt_cost;
+        a.out[HC + 1] = (double)stt.all_nan;
+        a.out[HC + 2] = (double)stt.early;
+        a.out[HC + 3] = (double)err;
+        a.out[HC + 4] = stt.minimum;
+        a.out[HC + 5] = stt.maximum;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Launch wrappers (host).
 // ---------------------------------------------------------------------------------------------
@@ -1226,9 +1526,16 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s)
 {
     const dim3 grid((unsigned)a.H, GRAD_SPLIT);
-    if (a.C == FR_C) hipLaunchKernelGGL(weights_gradient_kernel<FR_C>, grid, dim3(256), 0, s, a);
-    else if (a.C == 3) hipLaunchKernelGGL(weights_gradient_kernel<3>, grid, dim3(256), 0, s, a);
-    else return hipErrorInvalidValue;
+    if (a.C != FR_C && a.C != 3) return hipErrorInvalidValue;
+    if (a.R > SM_LARGE_R) {
+        hipLaunchKernelGGL(softmin_minmax_kernel, dim3(SM_NB), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(softmin_exp_kernel, dim3(SM_NB), dim3(256), 0, s, a);
+        if (a.C == FR_C) hipLaunchKernelGGL((weights_gradient_kernel<FR_C, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((weights_gradient_kernel<3, true>), grid, dim3(256), 0, s, a);
+    } else {
+        if (a.C == FR_C) hipLaunchKernelGGL((weights_gradient_kernel<FR_C, false>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((weights_gradient_kernel<3, false>), grid, dim3(256), 0, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !sum_splits) return e;   // unsharded: the finish kernel adds the splits itself
     const int HC = a.H * a.C;
@@ -1239,8 +1546,15 @@ hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_s
 
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s)
 {
-    if (a.sg_window > 0) hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(finish_flat_kernel, dim3(1), dim3(1024), 0, s, a);
+    const int W = a.H + 2 * a.sg_window + 1;
+    const size_t lds = ((size_t)a.C * (2 * W + a.H) + 2 * a.sg_window + 1) * sizeof(double);
+    if (a.sg_window > 0 && W <= SGK_MAXW && a.C <= 16 && lds <= 65536) {
+        hipLaunchKernelGGL(sg_finish_kernel, dim3(1), dim3(64 * (a.C > 4 ? a.C : 4)), lds, s, a);
+    } else if (a.sg_window > 0) {
+        hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(finish_flat_kernel, dim3(1), dim3(1024), 0, s, a);
+    }
     return hipGetLastError();
 }
 

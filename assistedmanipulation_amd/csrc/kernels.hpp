@@ -206,6 +206,8 @@ struct WGradArgs {
     int64_t begin, count, Rpad;
     int H, C;
     double *gsplit;        // [GRAD_SPLIT][H][C]
+    double *wexp;          // [R] scratch: unnormalised weights (R > SM_LARGE_R)
+    double *wpart;         // [4 * 64] scratch: per-chunk min / max / count / sum (R > SM_LARGE_R)
 };
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
@@ -214,10 +216,8 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // The update's rollouts (fr_coop_x_kernel): one workgroup per CU of four one-SIMD waves of rollouts
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
-// The update's rollouts (fr_coop.hip): fuse_cost = evaluate the step costs in the launch when there is
-// no energy tank (*costs_done); e0 / e1 = optional timing events around the launch.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, bool fuse_cost, hipEvent_t e0, hipEvent_t e1,
-                                 bool *folded, bool *costs_done);
+// The update's rollouts (fr_coop.hip): e0 / e1 = optional timing events around the launch.
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
 

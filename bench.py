@@ -32,8 +32,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; t
 # Algorithmic FLOPs of one rollout-step of the minimal arithmetic the device executes
 # (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
 # FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins these values):
-# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel (with the A/B
-# switch MPPI_COST_KERNEL=fused both run in the rollout launch, fr_coop_xc_kernel).
+# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel.
 FLOPS_PER_ROLLOUT_STEP = 6518.0
 FLOPS_COST_PER_ROLLOUT_STEP = 690.0
 FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STEP
@@ -53,6 +52,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--samples-per-gpu", type=int, default=SAMPLES_PER_GPU)
+    p.add_argument("--horizon-steps", type=int, default=int(round(HORISON / 0.01)),
+                   help="H (dt = 0.01); 64 = configs[2]/[3], 128 = configs[4]")
+    p.add_argument("--smoothing", type=int, default=0,
+                   help="Savitzky-Golay window (order 1); 10 = configs[4]")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     return p.parse_args()
@@ -101,7 +104,11 @@ def main():
         import torch.distributed as dist  # bootstrap + barrier / max-over-ranks only (gloo)
         dist.init_process_group("gloo")
     S_total = args.samples_per_gpu * world
-    conf = am.frankaridgeback_configuration(rollouts=S_total, horison=HORISON, keep_best_rollouts=KEEP_BEST)
+    horison = args.horizon_steps * 0.01
+    sg = am.Smoothing(args.smoothing, 1) if args.smoothing > 0 else None
+    default_workload = args.samples_per_gpu == SAMPLES_PER_GPU and args.horizon_steps == 64 and sg is None
+    conf = am.frankaridgeback_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST,
+                                            smoothing=sg)
     traj = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
     if traj is None:
         raise SystemExit("engine create failed")
@@ -147,10 +154,10 @@ def main():
     value = S_total * traj.H / (elapsed / args.steps)
     lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
     dyn_ms = dyn / args.steps                             # the rollout (dynamics) kernel alone, timed loop
-    records = not lane and os.environ.get("MPPI_COST_KERNEL") != "fused"   # A/B: costs in the rollout launch
+    records = not lane   # the coop kernel writes step records; fr_step_cost_kernel evaluates them
     cost_ms = float(kt[1] - kt[5]) if records else 0.0      # fr_step_cost_kernel (breakdown pass)
     traffic = None
-    if os.path.exists(PMC_JSON) and world == 1 and args.samples_per_gpu == SAMPLES_PER_GPU:
+    if os.path.exists(PMC_JSON) and world == 1 and default_workload:
         with open(PMC_JSON) as f:
             traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
@@ -175,14 +182,19 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (HUDDLED state, constant forecast wrench (20,0,0) N, Philox noise)",
-        "config": {"workload": "BASELINE configs[%d]: %d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, "
-                               "full AssistedManipulation cost stack%s" % (2 if world == 1 else 3, S_total, traj.H,
-                                                                          ", sample-sharded over RCCL" if world > 1 else ""),
+        "config": {"workload": "%s%d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, "
+                               "full AssistedManipulation cost stack%s%s" % (
+                                   ("BASELINE configs[%d]: " % (2 if world == 1 else 3)) if default_workload else "",
+                                   S_total, traj.H, ", Savitzky-Golay window %d order 1" % args.smoothing if sg else "",
+                                   ", sample-sharded over RCCL" if world > 1 else ""),
                    "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
         "kernel_ms": {"rollout_dynamics": dyn_ms, "rollout_cost": cost_ms, "breakdown_untimed": {
                       "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]}},
-        "roofline": {"bound": "mfma", "compute": "fp64 VALU (MI355X fp64 vector peak = fp64 matrix peak)",
-                     "kernel": "fr_rollout_kernel" if lane else ("fr_coop_x_kernel" if records else "fr_coop_xc_kernel"), "achieved": achieved_tflops,
+        # The rollout kernel runs fp64 VALU work (no MFMA: the 12-body chain has no dense contraction)
+        # at one wave per SIMD, so it is bound by issue slots and dependency chains, not by a
+        # datapath peak; the fraction is reported against the fp64 vector peak.
+        "roofline": {"bound": "valu", "compute": "fp64 VALU, latency/issue-bound at one wave per SIMD",
+                     "kernel": "fr_rollout_kernel" if lane else "fr_coop_x_kernel", "achieved": achieved_tflops,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
                      "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
@@ -193,7 +205,9 @@ def main():
                 "peak_GBs": HBM_PEAK_GBS},
     }
     if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.samples_per_gpu, HORISON)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.samples_per_gpu, horison)
+        # not vs_baseline (no published number): the GPU / CPU-port ratio, same workload
+        line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line))
     if dist:
         dist.destroy_process_group()

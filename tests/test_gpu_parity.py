@@ -154,9 +154,11 @@ def test_all_nan_raises():
         dev.update(x, 0.0)
 
 
-def test_flat_costs_early_return():
-    """All costs equal -> difference < 1e-6 -> weights / gradient left stale (mppi.cpp:373-375)."""
-    conf, dev, orc, sd = fr_pair(S=32, horison=0.08, K=4)
+@pytest.mark.parametrize("S", [32, 20000])
+def test_flat_costs_early_return(S):
+    """All costs equal -> difference < 1e-6 -> weights / gradient left stale (mppi.cpp:373-375).
+    S = 20000 takes the large-R softmin path (three launches, kernels.hip SM_LARGE_R)."""
+    conf, dev, orc, sd = fr_pair(S=S, horison=0.08, K=4, threads=16)
     x = am.huddled_state()
     n = orc.noise_draws(0.0)
     dev.inject_noise(np.zeros((n, 12)))
@@ -174,10 +176,11 @@ def _hip():
     return L
 
 
-def test_two_shards_on_one_device_equal_unsharded():
+@pytest.mark.parametrize("S,hor", [(256, 0.32), (20000, 0.08)])
+def test_two_shards_on_one_device_equal_unsharded(S, hor):
     """Sample sharding through the phase-split ABI: two handles on one GPU each
-    own half the rollouts; the two all-reduces are done on the host.  Must equal one handle."""
-    S, hor = 256, 0.32
+    own half the rollouts; the two all-reduces are done on the host.  Must equal one handle.
+    S = 20000: every shard weighs all R global costs through the large-R softmin path."""
     conf, single, orc, sd = fr_pair(S=S, horison=hor)
     shards = []
     for r in range(2):
