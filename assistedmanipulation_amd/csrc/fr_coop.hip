@@ -323,26 +323,39 @@ __device__ __forceinline__ int opaque_mask(bool c)
     return m;
 }
 
+// fdlibm's __kernel_sin / __kernel_cos coefficients, held in SGPRs for the horizon loop: built once
+// and made opaque, so the loop's FMAs read them as scalar operands instead of rematerialising each
+// as two v_mov_b32 per step (machine LICM stays off for this file, see the Makefile)
+struct SinCosK {
+    double s[6], c[6];
+};
+__device__ __forceinline__ SinCosK sincos_constants()
+{
+    SinCosK k{{-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
+               2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10},
+              {4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+               -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11}};
+#pragma unroll
+    for (int i = 0; i < 6; i++) asm volatile("" : "+s"(k.s[i]), "+s"(k.c[i]));
+    return k;
+}
+
 // sin and cos of a joint angle, branch-free (the library sincos branches to a Payne-Hanek
 // reduction for |x| >= 2^30, which ended the step's last scheduling region).  Valid for
 // |x| < 2^26: k = rint(2x / pi), r = x - k pi/2 with pi/2 in two parts (the first FMA is exact
 // for these k), fdlibm's __kernel_sin / __kernel_cos polynomials on [-pi/4, pi/4] (< 1 ulp), and
 // the quadrant by selects and a sign flip.  Joint angles are O(10); inf / NaN give NaN as sin does.
-__device__ __forceinline__ void fsincos(double x, double *sp, double *cp)
+__device__ __forceinline__ void fsincos(double x, double *sp, double *cp, const SinCosK &K)
 {
     const double k = __builtin_rint(x * 0.63661977236758134308);
     double r = __builtin_fma(-k, 1.5707963267948966, x);
     r = __builtin_fma(-k, 6.123233995736766e-17, r);
     const double z = r * r;
     const double ps = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
-                      __builtin_fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                      2.75573137070700676789e-06), -1.98412698298579493134e-04), 8.33333333332248946124e-03),
-                      -1.66666666666666324348e-01);
+                      __builtin_fma(z, K.s[5], K.s[4]), K.s[3]), K.s[2]), K.s[1]), K.s[0]);
     const double s = __builtin_fma(r * z, ps, r);
     const double pc = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
-                      __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                      -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
-                      4.16666666666666019037e-02);
+                      __builtin_fma(z, K.c[5], K.c[4]), K.c[3]), K.c[2]), K.c[1]), K.c[0]);
     const double hz = 0.5 * z, w = 1.0 - hz;
     const double c = w + (((1.0 - w) - hz) + (z * z) * pc);
     const int n = (int)k;
@@ -432,9 +445,9 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
 __device__ __forceinline__ void gj_pivot_0(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[0]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[0]));
     const double nt = -(Mc[0] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
@@ -453,9 +466,9 @@ __device__ __forceinline__ void gj_pivot_0(double *Mc)
 __device__ __forceinline__ void gj_pivot_1(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[1]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[1]));
     const double nt = -(Mc[1] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -474,9 +487,9 @@ __device__ __forceinline__ void gj_pivot_1(double *Mc)
 __device__ __forceinline__ void gj_pivot_2(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
     const double nt = -(Mc[2] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
@@ -495,9 +508,9 @@ __device__ __forceinline__ void gj_pivot_2(double *Mc)
 __device__ __forceinline__ void gj_pivot_3(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
     const double nt = -(Mc[3] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
@@ -516,9 +529,9 @@ __device__ __forceinline__ void gj_pivot_3(double *Mc)
 __device__ __forceinline__ void gj_pivot_4(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
     const double nt = -(Mc[4] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
@@ -537,9 +550,9 @@ __device__ __forceinline__ void gj_pivot_4(double *Mc)
 __device__ __forceinline__ void gj_pivot_5(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
     const double nt = -(Mc[5] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
@@ -558,9 +571,9 @@ __device__ __forceinline__ void gj_pivot_5(double *Mc)
 __device__ __forceinline__ void gj_pivot_6(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
     const double nt = -(Mc[6] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
@@ -579,9 +592,9 @@ __device__ __forceinline__ void gj_pivot_6(double *Mc)
 __device__ __forceinline__ void gj_pivot_7(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
     const double nt = -(Mc[7] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
@@ -600,9 +613,9 @@ __device__ __forceinline__ void gj_pivot_7(double *Mc)
 __device__ __forceinline__ void gj_pivot_8(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
     const double nt = -(Mc[8] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
@@ -621,9 +634,9 @@ __device__ __forceinline__ void gj_pivot_8(double *Mc)
 __device__ __forceinline__ void gj_pivot_9(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
     const double nt = -(Mc[9] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
@@ -642,9 +655,9 @@ __device__ __forceinline__ void gj_pivot_9(double *Mc)
 __device__ __forceinline__ void gj_pivot_10(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
     const double nt = -(Mc[10] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
@@ -663,9 +676,9 @@ __device__ __forceinline__ void gj_pivot_10(double *Mc)
 __device__ __forceinline__ void gj_pivot_11(double *Mc)
 {
     double d;
-    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
     const double nt = -(Mc[11] * frcp(d));
-    asm("s_nop 1\n\t"
+    asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
@@ -1283,7 +1296,8 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     double E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
     const double *grav = a.model->gravity;
     double sq, cq;
-    fsincos(q, &sq, &cq);   // one sincos per lane and step: FK and base yaw
+    const SinCosK scK = sincos_constants();
+    fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
     coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
@@ -1378,7 +1392,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         sq = q - q * q * q * (1.0 / 6.0);
         cq = 1.0 - q * q * 0.5;
 #else
-        fsincos(q, &sq, &cq);
+        fsincos(q, &sq, &cq, scK);
 #endif
 #ifdef PHASE_TRACE
         const uint64_t t_end = stamp(sq);
@@ -1444,6 +1458,9 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
     if (wv < 4) {
         const int wblk = blockIdx.x * 4 + wv;
+#ifdef MAIN_PRIO
+        __builtin_amdgcn_s_setprio(MAIN_PRIO);
+#endif
         coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel);
     } else if ((int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
@@ -1523,7 +1540,11 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.xrows = xrows;
     *folded = frow;
     if (e0) (void)hipEventRecord(e0, s);
+#ifdef FORCE_X
+    if (false) {}
+#else
     if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
+#endif
     else if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, (unsigned)groups, s);
     else if (a.energy) launch_x<CK_ASSISTED_MANIPULATION, true>(a, (unsigned)groups, s);
     else launch_x<CK_ASSISTED_MANIPULATION, false>(a, (unsigned)groups, s);

@@ -34,9 +34,12 @@ using namespace mppi_cost;
 // Records of one rollout are contiguous ([R][H][FR_NREC]): a wave stages up to 64 of them into LDS
 // with 1 KiB-contiguous loads, then each lane reads its step's record back.  The LDS record stride
 // is 42 doubles (84 dwords), so the 16-byte reads of eight consecutive lanes hit distinct banks.
+#ifdef COST_LDS_STAGE
 constexpr int LREC2 = 21;   // LDS record stride in double2
+#endif
 constexpr int NREC2 = FR_NREC / 2;
 
+#ifdef COST_LDS_STAGE
 template <int CK, bool EN>
 __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
 {
@@ -88,6 +91,45 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
     else if (a.optimal) *a.cost_out = J;
     else a.cost_out[a.begin + row] = J;
 }
+#else
+// Lane k loads its step's record straight into registers (21 16-byte loads, 336 B apart across the
+// lanes: every byte of the rollout's records is used once, through L2).  Staging through LDS took
+// 21.5 KB per wave and held a CU to seven waves, too few to hide the loads; without it the kernel
+// is bounded by registers (four waves per SIMD).
+template <int CK, bool EN>
+__global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
+{
+    const int lane = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    const bool frow = a.fcost != nullptr && row == a.count;
+    // no filter() when the update threw (mppi.cpp:170-176)
+    if ((frow || a.optimal) && (a.status->all_nan || a.status->sg_error)) return;
+    const int H = a.H;
+    const double2 *rec = reinterpret_cast<const double2 *>(frow ? a.frec : a.rec + row * H * FR_NREC);
+    const StepConst *stp = frow ? a.fsteps : a.steps;
+    const DevCost &Cs = *a.cost;
+    double J = 0.0;
+    for (int base = 0; base < H; base += 64) {
+        const int n = (H - base < 64) ? H - base : 64;
+        const int k = base + (lane < n ? lane : 0);
+        double r[FR_NREC];
+        const double2 *src = rec + (int64_t)k * NREC2;
+#pragma unroll
+        for (int i = 0; i < NREC2; i++) {
+            const double2 v = src[i];
+            r[2 * i] = v.x;
+            r[2 * i + 1] = v.y;
+        }
+        const double c = step_cost<CK, EN>(Cs, stp[k], r);
+        for (int i = 0; i < n; i++) J += readlane_f64(c, i);
+    }
+    if (lane != 0) return;
+    J = isnan(J) ? (double)NAN : J;
+    if (frow) *a.fcost = J;
+    else if (a.optimal) *a.cost_out = J;
+    else a.cost_out[a.begin + row] = J;
+}
+#endif
 
 }  // namespace
 

@@ -1,0 +1,61 @@
+"""Check the gfx9 DPP read-after-VALU-write hazard in a kernel's ISA: a DPP instruction may not read
+(as its DPP source, src0) a VGPR that a VALU instruction wrote fewer than two wait states before
+(instructions in between, or s_nop N = N + 1).  The rollout kernel's hand-written DPP blocks drop the
+defensive s_nop where the generated order already leaves the distance; this verifies it on the
+compiled code (straight-line: the horizon loop is one basic block).
+
+usage: dpp_hazard_check.py file.s [kernel_symbol_prefix]   (default: every kernel in the file)"""
+import re
+import sys
+
+
+def regs(tok):
+    """VGPR numbers named by an operand token (v5, v[4:5])."""
+    tok = tok.strip().lstrip("-|").rstrip("|")
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def check(path, prefix=""):
+    bad = 0
+    inside = False
+    recent = []   # (wait states since the write, registers)
+    for l in open(path):
+        l = l.rstrip("\n")
+        if not inside:
+            m = re.match(r"^(_Z\w+):", l)
+            if m and m.group(1).startswith(prefix or "_Z"):
+                inside, recent = True, []
+            continue
+        if l.startswith(".Lfunc_end"):
+            inside = False
+            continue
+        s = l.strip()
+        if not s or s.startswith((".", ";")) or s.endswith(":"):
+            if s.endswith(":"):
+                recent = []   # a branch target: the distance is only tracked in straight-line code
+            continue
+        op = s.split()[0]
+        ws = int(s.split()[1], 0) + 1 if op == "s_nop" else 1
+        if "_dpp" in op or " row_" in s or "quad_perm" in s:
+            ops = s[len(op):].split(",")
+            src0 = regs(ops[1]) if len(ops) > 1 else set()
+            for dist, w in recent:
+                if dist < 2 and (w & src0):
+                    print("hazard (%d wait states): %s" % (dist, s))
+                    bad += 1
+        recent = [(d + ws, w) for d, w in recent if d + ws < 2]
+        if op.startswith("v_") and op != "v_nop":
+            dst = regs(s[len(op):].split(",")[0])
+            if dst:
+                recent.append((0, dst))
+    return bad
+
+
+if __name__ == "__main__":
+    n = check(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
+    print("dpp_hazard_check: %d DPP read-after-write hazards in %s" % (n, sys.argv[1]))
+    sys.exit(1 if n else 0)
