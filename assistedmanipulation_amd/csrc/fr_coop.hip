@@ -1425,8 +1425,8 @@ template <int CK, bool EN, int WPB, bool FROW>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
 {
     constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
-    __shared__ double lds_kin[WPB * ROWS_PER_WAVE * KS];
-    __shared__ double lds_scr[WPB * ROWS_PER_WAVE * LDS_SCR];
+    __shared__ __attribute__((aligned(16))) double lds_kin[WPB * ROWS_PER_WAVE * KS];
+    __shared__ __attribute__((aligned(16))) double lds_scr[WPB * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;   // no filter() (mppi.cpp:170-176)
     const int wv = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
@@ -1446,8 +1446,8 @@ template <int CK, bool EN>
 __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
 {
     constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
-    __shared__ double lds_kin[5 * ROWS_PER_WAVE * KS];
-    __shared__ double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
+    __shared__ __attribute__((aligned(16))) double lds_kin[5 * ROWS_PER_WAVE * KS];
+    __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;

@@ -8,7 +8,7 @@ import numpy as np
 path, nb = sys.argv[1], int(sys.argv[2])
 raw = np.fromfile(path, dtype=np.uint32)
 rec = raw.reshape(-1, nb, 4)[-1].astype(np.int64)   # last update
-rec = rec[:nb - 2] if nb > 2 else rec
+rec = rec[:nb]
 st, en, hw, xcc = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3] & 0xF
 ok = en != 0
 st, en, hw, xcc = st[ok], en[ok], hw[ok], xcc[ok]
@@ -37,3 +37,7 @@ for n in sorted(set(share)):
     m = share == n
     print("  blocks on SIMDs holding %d waves: %4d  dur p50 %.1f us" % (n, m.sum(), np.median(dur[m])))
 print("per-XCC blocks:", sorted(collections.Counter(xcc).items()))
+order = np.argsort(-dur)[:6]
+idx = np.nonzero(ok)[0]
+for i in order:
+    print("  longest: wave %5d dur %.1f us start %.1f end %.1f  SIMD %s (waves there %d)" % (idx[i], dur[i], s_us[i], e_us[i], key[i], cnt[key[i]]))
