@@ -43,7 +43,7 @@ BYTES_REC_PER_ROLLOUT_STEP = 336.0
 BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
 # HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
 # tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
-PMC_JSON = os.path.join(HERE, "profiles", "r01_pmc_rollout.json")
+PMC_JSON = os.path.join(HERE, "profiles", "r02_pmc_rollout.json")
 
 
 def parse():
