@@ -102,8 +102,8 @@ static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16,
 // velocity weight of the cost, and the lane masks of the kinematic sums.  Row 12 serves lanes
 // 12..15: body 0's geometry with every mask and weight zero.
 constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 25, T_AX = 28, T_ROT = 31, T_NROT = 32;
-constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42;
-constexpr int MB = 43;   // odd: lanes reading their own body's entry hit distinct banks
+constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42, T_MC = 43;
+constexpr int MB = 45;   // odd: lanes reading their own body's entry hit distinct banks
 constexpr int LDS_MODEL = (FR_NB + 1) * MB;
 
 // ---- DPP helpers (fp64 as two dwords) ------------------------------------------------------
@@ -695,28 +695,44 @@ __device__ __forceinline__ void gj_pivot_11(double *Mc)
 }
 // ---- END generated by tools/gen_gj.py ----
 
+// The third column of a rotation in delta form (D = R - I, row-major) from its first two, r2 = r0 x r1:
+// d2 = e0 x d1 + d0 x e1 + d0 x d1 (the zero delta gives zero).
+__device__ __forceinline__ void delta_col2(double *D)
+{
+    D[2] = __builtin_fma(D[3], D[7], __builtin_fma(-D[6], D[4], -D[6]));
+    D[5] = __builtin_fma(D[6], D[1], __builtin_fma(-D[0], D[7], -D[7]));
+    D[8] = __builtin_fma(D[0], D[4], __builtin_fma(-D[3], D[1], D[4] + D[0]));
+}
+
 // One level of the delta-form prefix scan: (I + Da)(I + D) = I + Da + D + Da D,
-// pa + (I + Da) p = pa + p + Da p.
+// pa + (I + Da) p = pa + p + Da p - with the rotations' first two columns only: 9 doubles shifted
+// (18 moves) instead of 12, the partner's third column rebuilt by delta_col2 (7 ops), and only
+// columns 0 and 1 formed (1150 -> 1105 loop instructions).
 template <int S>
-__device__ __forceinline__ void scan_level(double *D, double *p)
+__device__ __forceinline__ void scan_level2(double *D, double *p)
 {
     double Da[9], pa[3];
 #pragma unroll
-    for (int k = 0; k < 9; k++) Da[k] = shr<S>(D[k]);
-#pragma unroll
-    for (int k = 0; k < 3; k++) pa[k] = shr<S>(p[k]);
+    for (int r = 0; r < 3; r++) {
+        Da[3 * r] = shr<S>(D[3 * r]);
+        Da[3 * r + 1] = shr<S>(D[3 * r + 1]);
+        pa[r] = shr<S>(p[r]);
+    }
+    delta_col2(Da);
     double Dn[9], pn[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
 #pragma unroll
-        for (int c = 0; c < 3; c++)
+        for (int c = 0; c < 2; c++)
             Dn[3 * r + c] = Da[3 * r] * D[c] + (Da[3 * r + 1] * D[3 + c] + (Da[3 * r + 2] * D[6 + c] + (Da[3 * r + c] + D[3 * r + c])));
         pn[r] = Da[3 * r] * p[0] + (Da[3 * r + 1] * p[1] + (Da[3 * r + 2] * p[2] + (pa[r] + p[r])));
     }
 #pragma unroll
-    for (int k = 0; k < 9; k++) D[k] = Dn[k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) p[k] = pn[k];
+    for (int r = 0; r < 3; r++) {
+        D[3 * r] = Dn[3 * r];
+        D[3 * r + 1] = Dn[3 * r + 1];
+        p[r] = pn[r];
+    }
 }
 
 // Packed upper-triangle index of a symmetric 6x6.
@@ -827,6 +843,7 @@ struct LaneConst {
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
     int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
+    double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
@@ -856,10 +873,11 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     D[4] -= 1.0;
     D[8] -= 1.0;
     FKSTAMP(0, D[8])
-    scan_level<1>(D, p);
-    scan_level<2>(D, p);
-    scan_level<4>(D, p);
-    scan_level<8>(D, p);
+    scan_level2<1>(D, p);
+    scan_level2<2>(D, p);
+    scan_level2<4>(D, p);
+    scan_level2<8>(D, p);
+    delta_col2(D);
     FKSTAMP(1, p[2])
     double R[9];
 #pragma unroll
@@ -1094,24 +1112,25 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const CoopBody &bd, double tau_l, double *Lk,
                                              uint64_t &t_mid)
 {
-    double v[10] = {bd.m, bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
-    double own[10];
+    // (h, Ib) scanned; the subtree's mass is a per-lane constant of the body table (T_MC)
+    double v[9] = {bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
+    double own[9];
 #pragma unroll
-    for (int k = 0; k < 10; k++) own[k] = v[k];
+    for (int k = 0; k < 9; k++) own[k] = v[k];
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] += shl<1>(v[k]);
+    for (int k = 0; k < 9; k++) v[k] += shl<1>(v[k]);
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] += shl<2>(v[k]);
+    for (int k = 0; k < 9; k++) v[k] += shl<2>(v[k]);
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] += shl<4>(v[k]);
+    for (int k = 0; k < 9; k++) v[k] += shl<4>(v[k]);
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] += shl<8>(v[k]);
+    for (int k = 0; k < 9; k++) v[k] += shl<8>(v[k]);
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] = msel(L.m_j10, v[k], own[k]);
+    for (int k = 0; k < 9; k++) v[k] = msel(L.m_j10, v[k], own[k]);
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
-    const double m = v[0], h0 = v[1], h1 = v[2], h2 = v[3];
-    const double I00 = v[4], I01 = v[5], I02 = v[6], I11 = v[7], I12 = v[8], I22 = v[9];
+    const double m = L.mc, h0 = v[0], h1 = v[1], h2 = v[2];
+    const double I00 = v[3], I01 = v[4], I02 = v[5], I11 = v[6], I12 = v[7], I22 = v[8];
     double F[6];
     F[0] = m * S[0] - (h1 * S[5] - h2 * S[4]);
     F[1] = m * S[1] - (h2 * S[3] - h0 * S[5]);
@@ -1197,7 +1216,12 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
         else if (f == T_VW) v = live * dc.vel_q[b];
         else if (f == T_WV) v = (!dummy && b <= FR_EE_PARENT) ? 1.0 : 0.0;
         else if (f == T_WA) v = (!dummy && b >= FR_ARM0 && b < FR_ARM1) ? 1.0 : 0.0;
-        else v = (!dummy && b == 11) ? -1.0 : 0.0;   // T_FIX
+        else if (f == T_FIX) v = (!dummy && b == 11) ? -1.0 : 0.0;
+        else if (f == T_MC) {   // the composite mass of the body's subtree (a constant: no scan)
+            v = 0.0;
+            for (int i = b; i < FR_NB && !dummy; i++)
+                if (b <= FR_EE_PARENT || i == b) v += dm.b[i].mass;
+        } else v = 0.0;
         Lmodel[t] = v;
     }
 }
@@ -1290,6 +1314,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         asm volatile("" : "+v"(anc));
         L.anc = anc;
     }
+    L.mc = M[T_MC];
 
     double q = jl ? x0p[jb] : 0.0;
     double qd = jl ? x0p[FR_NB + jb] : 0.0;
