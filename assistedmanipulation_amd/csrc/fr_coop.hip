@@ -304,6 +304,17 @@ __device__ __forceinline__ double frcp(double d)
     return __builtin_fma(r, __builtin_fma(e, e, e), r);
 }
 
+// -x / d for the Gauss-Jordan pivots: v_rcp_f64 and one Newton correction applied to the product,
+// t = -x r, e = 1 - d r, -x / d ~ t + t e (four ops, three deep; the rcp's 2.8e-8 relative error
+// squares to ~1e-15).  frcp's exact reciprocal needs one more dependent FMA per pivot.
+__device__ __forceinline__ double neg_quot(double x, double d)
+{
+    const double r = __builtin_amdgcn_rcp(d);
+    const double t = -x * r;
+    const double e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(t, e, t);
+}
+
 // b on the lanes whose mask m is all ones, a on the lanes where it is zero (m: a loop-invariant
 // per-lane mask in a VGPR, made opaque where it is built).  One v_bfi_b32 per dword and no compare:
 // C++ selects on the row index were compares per use, and LLVM turns a select whose operand is a
@@ -446,7 +457,7 @@ __device__ __forceinline__ void gj_pivot_0(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[0]));
-    const double nt = -(Mc[0] * frcp(d));
+    const double nt = neg_quot(Mc[0], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
@@ -467,7 +478,7 @@ __device__ __forceinline__ void gj_pivot_1(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[1]));
-    const double nt = -(Mc[1] * frcp(d));
+    const double nt = neg_quot(Mc[1], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -488,7 +499,7 @@ __device__ __forceinline__ void gj_pivot_2(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
-    const double nt = -(Mc[2] * frcp(d));
+    const double nt = neg_quot(Mc[2], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
@@ -509,7 +520,7 @@ __device__ __forceinline__ void gj_pivot_3(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
-    const double nt = -(Mc[3] * frcp(d));
+    const double nt = neg_quot(Mc[3], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
@@ -530,7 +541,7 @@ __device__ __forceinline__ void gj_pivot_4(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
-    const double nt = -(Mc[4] * frcp(d));
+    const double nt = neg_quot(Mc[4], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
@@ -551,7 +562,7 @@ __device__ __forceinline__ void gj_pivot_5(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
-    const double nt = -(Mc[5] * frcp(d));
+    const double nt = neg_quot(Mc[5], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
@@ -572,7 +583,7 @@ __device__ __forceinline__ void gj_pivot_6(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
-    const double nt = -(Mc[6] * frcp(d));
+    const double nt = neg_quot(Mc[6], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
@@ -593,7 +604,7 @@ __device__ __forceinline__ void gj_pivot_7(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
-    const double nt = -(Mc[7] * frcp(d));
+    const double nt = neg_quot(Mc[7], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
@@ -614,7 +625,7 @@ __device__ __forceinline__ void gj_pivot_8(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
-    const double nt = -(Mc[8] * frcp(d));
+    const double nt = neg_quot(Mc[8], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
@@ -635,7 +646,7 @@ __device__ __forceinline__ void gj_pivot_9(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
-    const double nt = -(Mc[9] * frcp(d));
+    const double nt = neg_quot(Mc[9], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
@@ -656,7 +667,7 @@ __device__ __forceinline__ void gj_pivot_10(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
-    const double nt = -(Mc[10] * frcp(d));
+    const double nt = neg_quot(Mc[10], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
@@ -677,7 +688,7 @@ __device__ __forceinline__ void gj_pivot_11(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
-    const double nt = -(Mc[11] * frcp(d));
+    const double nt = neg_quot(Mc[11], d);
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
