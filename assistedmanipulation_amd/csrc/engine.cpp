@@ -104,6 +104,7 @@ struct mppi_handle {
     // device buffers
     DevModel *d_model = nullptr;
     DevCost *d_cost = nullptr;
+    double *d_table = nullptr;   // cooperative kernels' body table (built from d_model, d_cost)
     DevPointMass *d_pm = nullptr;
     StepConst *d_steps = nullptr;
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
@@ -333,6 +334,18 @@ void dfree(mppi_handle *h, T *&p)
 bool use_coop(const mppi_handle *h)
 {
     return h->coop || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || h->am.enable_energy_limit;
+}
+
+// Sampling inside the cooperative update launch (fr_coop.hip fused_sample): FrankaRidgeback rows
+// in one round of four-wave workgroups.  MPPI_FUSE_SAMPLE=0 keeps the separate sample_kernel (A/B).
+bool fuse_sampling(const mppi_handle *h)
+{
+    static const bool off = [] {
+        const char *e = std::getenv("MPPI_FUSE_SAMPLE");
+        return e && e[0] == '0';
+    }();
+    return !off && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
+           fr_coop_update_fusable(h->count);
 }
 
 mppi_status alloc_shard_buffers(mppi_handle *h)
@@ -617,6 +630,9 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         }
         CREATE_TRY(dalloc(h, &h->d_cost, 1));
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
+        CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
+        CREATE_TRY(launch_fr_body_table(h->d_model, h->d_cost, h->d_table, nullptr));
+        CREATE_TRY(hipDeviceSynchronize());
     } else {
         DevPointMass p{};
         p.inv_mass = 1.0 / dyn->point_mass.mass;
@@ -992,6 +1008,7 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         FrRolloutArgs a{};
         a.model = h->d_model;
         a.cost = h->d_cost;
+        a.table = h->d_table;
         a.steps = h->opt_steps;
         a.x0 = h->d_x0_opt;
         a.Ushift = h->d_U;
@@ -1074,9 +1091,11 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     }
     // the stable order of the previous costs was ranked behind the previous publish (phase 3)
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
+    // the cooperative update launch samples its own rows when it runs one round of workgroups
+    const bool fuse = fuse_sampling(h);
+    SampleArgs sa{};
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
-        SampleArgs sa{};
         sa.rank = h->d_rank;
         sa.Uprev = h->d_U;
         sa.inj = h->d_inj;
@@ -1095,7 +1114,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         sa.X = (int)h->X;
         if (h->tdiag)
             for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
-        HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
+        if (!fuse) HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
     }
     // timing level 1 with the cooperative kernel: the rollout launch records its own events
     const bool ev_in_launch = h->timing == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
@@ -1104,6 +1123,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         FrRolloutArgs a{};
         a.model = h->d_model;
         a.cost = h->d_cost;
+        a.table = h->d_table;
         a.steps = h->d_steps;
         a.x0 = h->d_x0;
         a.Ushift = h->d_Us;
@@ -1120,6 +1140,12 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
         a.rec = h->d_rec;
+        if (fuse) {   // U*_shifted read from U* with the shift; the state from the launch
+            a.fuse_sample = 1;
+            a.samp = sa;
+            a.Ushift = sp.shift_by > 0 ? h->d_U : h->d_Us;
+            a.ush = sp.shift_by > 0 ? (int)std::min<int64_t>(sp.shift_by, h->H) : 0;
+        }
         // a pending filter() not folded here stays pending: this update's phase 3 supersedes it,
         // and only the latest one is observable (mppi_optimal_cost / logger)
         const bool fold = use_coop(h) && h->opt_state == mppi_handle::OPT_PENDING;

@@ -41,6 +41,7 @@
 #include "engine_types.hpp"
 #include "kernels.hpp"
 #include "fr_cost_terms.hpp"
+#include "sample_device.hpp"
 #include <hip/hip_ext.h>
 
 using namespace mppi_eng;
@@ -105,6 +106,7 @@ constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 2
 constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42, T_MC = 43;
 constexpr int MB = 45;   // odd: lanes reading their own body's entry hit distinct banks
 constexpr int LDS_MODEL = (FR_NB + 1) * MB;
+static_assert(LDS_MODEL <= FR_BODY_TABLE, "body table buffer");
 
 // ---- DPP helpers (fp64 as two dwords) ------------------------------------------------------
 // mov_dpp with bound_ctrl: lanes whose source lies outside the row read 0.
@@ -1189,12 +1191,15 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// Stage the per-body table (geometry, inertia, axes, cost weights, lane masks) in LDS.
-__device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double *Lmodel, int nt)
+// The per-body table (geometry, inertia, axes, cost weights, lane masks), built once per handle
+// (launch_fr_body_table, at create: the model and cost are constants of the handle).  Built in the
+// rollout kernels themselves, its chain of dependent, divergent loads of the model held every
+// workgroup for ~7 us before its first step (PRO_TRACE); a copy of the table is one load.
+__global__ void fr_body_table_kernel(const DevModel *model, const DevCost *cost, double *table)
 {
-    const DevModel &dm = *a.model;
-    const DevCost &dc = *a.cost;
-    for (int t = threadIdx.x; t < LDS_MODEL; t += nt) {
+    const DevModel &dm = *model;
+    const DevCost &dc = *cost;
+    for (int t = threadIdx.x; t < LDS_MODEL; t += blockDim.x) {
         const int row = t / MB, f = t % MB;
         const bool dummy = row == FR_NB;
         const int b = dummy ? 0 : row;
@@ -1233,8 +1238,14 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
             for (int i = b; i < FR_NB && !dummy; i++)
                 if (b <= FR_EE_PARENT || i == b) v += dm.b[i].mass;
         } else v = 0.0;
-        Lmodel[t] = v;
+        table[t] = v;
     }
+}
+
+// Stage the body table in LDS.
+__device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double *Lmodel, int nt)
+{
+    for (int t = threadIdx.x; t < LDS_MODEL; t += nt) Lmodel[t] = a.table[t];
 }
 
 // Step record store (layout: kernels.hpp FR_NREC), the whole row active (no branch splits the
@@ -1273,7 +1284,7 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // repeating its row-uniform terms.
 template <int CK, bool EN, bool FROW>
 __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
-                                          const double *Lmodel)
+                                          const double *Lmodel, const double *Lx0)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1283,7 +1294,9 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         a.trace[4 * wblk + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         a.trace[4 * wblk + 2] = hw;
+#ifndef PRO_TRACE
         a.trace[4 * wblk + 3] = xcc;
+#endif
     }
 #endif
     // FROW: the row after the last rollout is the previous update's filter() (optimal rollout)
@@ -1292,8 +1305,11 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     if (!live) return;   // row-uniform: the row's lanes leave together (no DPP partner is lost)
     const int H = a.H;
     const bool opt_row = a.optimal || frow;   // no noise (mppi.cpp:450-479)
-    const double *x0p = FROW && frow ? a.fx0 : a.x0;
+    // U*_shifted row k is Up row min(k + ush, H - 1): with fused sampling (a.fuse_sample) the
+    // shift reads U* itself (mppi.cpp:197-207); the state staged in LDS (stage_x0)
+    const double *x0p = FROW && frow ? a.fx0 : Lx0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
+    const int ush = FROW && frow ? 0 : a.ush;
     double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_NREC;   // [rollout][step][FR_NREC]
     auto recp = [&](int k) -> double * { return rp + (int64_t)k * FR_NREC; };
     const bool jl = j < FR_NB;   // lane owns a body / control component
@@ -1349,13 +1365,13 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     store_record(recp(0), j, L, q, qd, kin, E);
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[(int64_t)k * nstride];
-        const double ub_l = Up[k * FR_C + jb];
+        const double ub_l = Up[min(k + ush, H - 1) * FR_C + jb];
 #else
     // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
     // whose latency a single wave per SIMD cannot hide within one step
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
-    double eps_n = np[0], ub_n = Up[jb];
+    double eps_n = np[0], ub_n = Up[min(ush, H - 1) * FR_C + jb];
     store_record(recp(0), j, L, q, qd, kin, E);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
@@ -1367,7 +1383,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
-        ub_n = Up[(k + 1) * FR_C + jb];
+        ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
 #endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
         // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
@@ -1450,6 +1466,76 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #endif
 }
 
+// The update's state into LDS: from the launch's arguments with fused sampling, else from x0
+__device__ __forceinline__ void stage_x0(const FrRolloutArgs &a, double *Lx0)
+{
+    if ((int)threadIdx.x < MAX_X) Lx0[threadIdx.x] = a.fuse_sample ? a.samp.x0v[threadIdx.x] : a.x0[threadIdx.x < FR_X ? threadIdx.x : 0];
+}
+
+// Trajectory::sample for the workgroup's own rows, ahead of its horizon loop (a.fuse_sample): the
+// eps pieces of rows [r0, r0 + n1) and [x0r, x0r + n2) for every step (sample_device.hpp).  A
+// thread keeps one (row, piece) and walks the steps k0, k0 + kstep, ... four at a time, computing
+// the four pieces (their loads issued together) before storing them: with five waves on the CU
+// the prologue is latency-bound, not issue-bound.  The rows read U*_shifted from U*
+// (FrRolloutArgs::ush); block 0 writes U*_shifted and x0 back for the kernels that follow (finish,
+// filter()).  This replaces the sample_kernel launch ahead of the rollouts.  The caller's
+// __syncthreads makes the eps stores visible to the workgroup's rows.
+template <int NT, bool DIAG>
+__device__ __forceinline__ void fused_sample_rows(const SampleArgs &sa, int64_t r0, int n1, int64_t x0r, int n2)
+{
+    constexpr int NB = DIAG ? (FR_C + 3) / 4 : 1;
+    constexpr int CW = DIAG ? 4 : FR_C;
+    constexpr int UN = 4;
+    const int per = (n1 + n2) * NB;   // (row, piece) pairs: <= 20 * 3 <= NT
+    const int kstep = NT / per;
+    const int t = (int)threadIdx.x;
+#ifdef FUSE_NOSAMPLE
+    return;   // timing diagnostics only: the eps tensor is left as it was
+#endif
+    if (per == 0 || t >= per * kstep) return;
+    const int rp = t % per, r = rp / NB, blk = rp - r * NB, k0 = t / per;
+    const int64_t lr = r < n1 ? r0 + r : x0r + (r - n1);
+    const int64_t g = sa.begin + lr;
+    const int rank = g >= 2 ? sa.rank[g] : 0;
+    const int H = sa.H;
+    for (int k = k0; k < H; k += UN * kstep) {
+        double e[UN][CW];
+        if constexpr (DIAG) {   // plans, then every piece's loads, then the draws: one wait per pass
+            mppi_sample::EpsPlan pl[UN];
+            double v[UN][4];
+#pragma unroll
+            for (int u = 0; u < UN; u++) {
+                pl[u] = mppi_sample::eps_plan<FR_C>(sa, k + u * kstep < H ? k + u * kstep : k, lr, g, rank, blk);
+                const double2 *p2 = reinterpret_cast<const double2 *>(pl[u].p);
+                const double2 lo = p2[0], hi = p2[1];
+                v[u][0] = lo.x; v[u][1] = lo.y; v[u][2] = hi.x; v[u][3] = hi.y;
+            }
+#pragma unroll
+            for (int u = 0; u < UN; u++) mppi_sample::eps_finish(sa, pl[u], blk, v[u], e[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < UN; u++)
+                if (k + u * kstep < H) mppi_sample::sample_eps<FR_C, false>(sa, k + u * kstep, lr, g, rank, blk, e[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UN; u++)
+            if (k + u * kstep < H) mppi_sample::store_eps<FR_C, DIAG>(sa, k + u * kstep, lr, blk, e[u]);
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void fused_sample(const FrRolloutArgs &a, int64_t r0, int n1, int64_t x0r, int n2)
+{
+    const SampleArgs &sa = a.samp;
+    if (blockIdx.x == 0) {
+        if (sa.sp.shift_by > 0)
+            for (int i = threadIdx.x; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
+        if ((int)threadIdx.x < sa.X) sa.x0_out[threadIdx.x] = sa.x0v[threadIdx.x];
+    }
+    if (sa.sp.tdiag) fused_sample_rows<NT, true>(sa, r0, n1, x0r, n2);
+    else fused_sample_rows<NT, false>(sa, r0, n1, x0r, n2);
+}
+
 // WPB waves per workgroup.  The update's launch uses WPB = 5 with > 80 KB of LDS per workgroup, so a
 // CU holds one workgroup: waves 0..3 take one SIMD each, and wave 4 runs the rows left over when
 // the rollouts do not fill four-wave groups (rollouts 0 and 1 of the reference's R = S + 2, plus the
@@ -1464,6 +1550,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     __shared__ __attribute__((aligned(16))) double lds_kin[WPB * ROWS_PER_WAVE * KS];
     __shared__ __attribute__((aligned(16))) double lds_scr[WPB * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
+    __shared__ double Lx0[MAX_X];
     if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;   // no filter() (mppi.cpp:170-176)
     const int wv = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -1471,9 +1558,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int wrow = wv * ROWS_PER_WAVE + rowi;   // row within the workgroup
     const int wblk = blockIdx.x * WPB + wv;        // wave index in the launch
     stage_body_table(a, Lmodel, 64 * WPB);
+    stage_x0(a, Lx0);
+    if constexpr (WPB == 4) {
+        if (a.fuse_sample) {
+            const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE;
+            fused_sample<64 * WPB>(a, r0, (int)(r0 + 4 * ROWS_PER_WAVE < a.count ? 4 * ROWS_PER_WAVE : a.count - r0), 0, 0);
+        }
+    }
     __syncthreads();
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
-                            Lmodel);
+                            Lmodel, Lx0);
 }
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and a fifth wave
@@ -1485,11 +1579,21 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ __attribute__((aligned(16))) double lds_kin[5 * ROWS_PER_WAVE * KS];
     __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
+    __shared__ double Lx0[MAX_X];
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
     const int wrow = wv * ROWS_PER_WAVE + rowi;
+#ifdef PRO_TRACE   // kernel entry per main wave (slot 3; coop_rows records the loop's start and end)
+    if (a.trace && lane == 0 && wv < 4) a.trace[4 * (blockIdx.x * 4 + wv) + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
     stage_body_table(a, Lmodel, 320);
+    stage_x0(a, Lx0);
+    if (a.fuse_sample) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
+        const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
+        const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
+        fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
+    }
     __syncthreads();
     double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
     if (wv < 4) {
@@ -1497,10 +1601,10 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #ifdef MAIN_PRIO
         __builtin_amdgcn_s_setprio(MAIN_PRIO);
 #endif
-        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel);
+        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
     } else if ((int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
-        coop_rows<CK, EN, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel);
+        coop_rows<CK, EN, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
     }
 }
 
@@ -1553,6 +1657,21 @@ hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
+hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s)
+{
+    hipLaunchKernelGGL(fr_body_table_kernel, dim3(1), dim3(640), 0, s, model, cost, table);
+    return hipGetLastError();
+}
+
+// Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample
+// their own rows, a.fuse_sample) for `count` rows.
+bool fr_coop_update_fusable(int64_t count)
+{
+    constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
+    const int64_t groups = count / WG_ROWS, xrows = count - groups * WG_ROWS + 1;   // + a folded filter() row
+    return groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE;
+}
+
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded)
 {
@@ -1565,6 +1684,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     const int64_t xrows = extra + (frow ? 1 : 0);
     FrRolloutArgs a = a0;
     if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
+        if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         if (e0) (void)hipEventRecord(e0, s);
         const hipError_t e = launch_fr_coop(a, s);

@@ -30,6 +30,7 @@
 #include "device_common.hpp"
 #include "engine_types.hpp"
 #include "kernels.hpp"
+#include "sample_device.hpp"
 
 using namespace mppi_eng;
 using mppi_dev::smax;
@@ -439,61 +440,6 @@ __device__ __forceinline__ double fr_cost(const DevCost &Csref, const StepConst 
     return cost;
 }
 
-// eps = T z for one draw.  z from the Philox stream keyed by (seed, update, draw).
-__device__ __forceinline__ void philox_draw(const SampleParams &P, int64_t draw, const double *T, int C, double *eps)
-{
-    float z[16];
-#pragma unroll
-    for (int blk = 0; blk < 4; blk++) {
-        if (4 * blk >= C) break;
-        mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};
-        mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
-        mppi_dev::box_muller(r.x, r.y, z[4 * blk + 0], z[4 * blk + 1]);
-        mppi_dev::box_muller(r.z, r.w, z[4 * blk + 2], z[4 * blk + 3]);
-    }
-    if (P.tdiag) {
-        for (int c = 0; c < C; c++) eps[c] = T[c * C + c] * (double)z[c];
-    } else {
-        for (int i = 0; i < C; i++) {
-            double s = 0.0;
-            for (int j = 0; j < C; j++) s += T[i * C + j] * (double)z[j];
-            eps[i] = s;
-        }
-    }
-}
-
-// The eps column (k) of rollout g as Trajectory::sample leaves it (mppi.cpp:242-269).
-// `col` holds the previous contents of the column on entry.
-__device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, int rank, int64_t k, int H, int C,
-                                              const double *Uprev, const double *inj, const double *T,
-                                              const double *noise, int64_t Rpad, int64_t lr, double *eps)
-{
-    if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
-        for (int c = 0; c < C; c++) eps[c] = -Uprev[k * C + c];
-        return;
-    }
-    int64_t draw = -1;
-    if (rank < P.keep) {
-        if (P.shift_by > 0) {
-            if (k < P.shifted) {
-                for (int c = 0; c < C; c++) eps[c] = noise[((k + P.shift_by) * Rpad + lr) * C + c];
-                return;
-            }
-            draw = (int64_t)rank * (H - P.shifted) + (k - P.shifted);
-        } else {
-            for (int c = 0; c < C; c++) eps[c] = noise[(k * Rpad + lr) * C + c];
-            return;
-        }
-    } else {
-        draw = P.keep_draws + (int64_t)(rank - P.keep) * H + k;
-    }
-    if (P.injected) {
-        for (int c = 0; c < C; c++) eps[c] = inj[draw * C + c];
-    } else {
-        philox_draw(P, draw, T, C, eps);
-    }
-}
-
 // t0 + k dt exactly as the reference's double expression (mppi.cpp:430, 437): window times are
 // compared with ==/< (filter.cpp:94-106), so no FMA contraction here.
 __device__ __forceinline__ double step_time(double t0, int k, double dt)
@@ -639,72 +585,12 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
     if (blockIdx.x == 0 && k == 0 && (int)threadIdx.x < a.X) a.x0_out[threadIdx.x] = a.x0v[threadIdx.x];
     if (blockIdx.x == 0 && a.sp.shift_by > 0 && (int)threadIdx.x < C) {
         const int c = threadIdx.x;
-        const int64_t sh = a.sp.shift_by, kept = a.sp.shifted;
-        a.Us[k * C + c] = (k < kept) ? a.Uprev[(k + sh) * C + c] : a.Uprev[(a.H - 1) * C + c];
+        a.Us[k * C + c] = mppi_sample::shifted_u(a, k, c);
     }
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t lr = tid / NB;
     if (lr >= a.count) return;
-    const int blk = (int)(tid - lr * NB);
-    const int c0 = DIAG ? 4 * blk : 0;
-    constexpr int CW = DIAG ? (C < 4 ? C : 4) : C;
-    const int cw = DIAG ? ((C - c0) < 4 ? (C - c0) : 4) : C;
-    const int64_t g = a.begin + lr;
-    double eps[CW];
-    if (g == 0) {
-#pragma unroll
-        for (int c = 0; c < CW; c++) eps[c] = 0.0;
-    } else if (!DIAG) {
-        const int rank = (g >= 2) ? a.rank[g] : 0;
-        sample_column(a.sp, g, rank, k, a.H, C, a.Uprev, a.inj, a.T, a.prev, a.Rpad, lr, eps);
-    } else {
-        const SampleParams &P = a.sp;
-        int64_t draw = -1;
-        const double *src = nullptr;
-        double sgn = 1.0;
-        if (g == 1) {
-            src = a.Uprev + (int64_t)k * C + c0;
-            sgn = -1.0;
-        } else {
-            const int rank = a.rank[g];
-            if (rank < P.keep) {
-                if (P.shift_by > 0) {
-                    if (k < P.shifted) src = a.prev + (((int64_t)k + P.shift_by) * a.Rpad + lr) * C + c0;
-                    else draw = (int64_t)rank * (a.H - P.shifted) + (k - P.shifted);
-                } else {
-                    src = a.prev + ((int64_t)k * a.Rpad + lr) * C + c0;
-                }
-            } else {
-                draw = P.keep_draws + (int64_t)(rank - P.keep) * a.H + k;
-            }
-        }
-        if (src) {
-#pragma unroll
-            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? sgn * src[c] : 0.0;
-        } else if (P.injected) {
-#pragma unroll
-            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.inj[draw * C + c0 + c] : 0.0;
-        } else {
-            mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};
-            mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
-            float z[4];
-            mppi_dev::box_muller(r.x, r.y, z[0], z[1]);
-            mppi_dev::box_muller(r.z, r.w, z[2], z[3]);
-#pragma unroll
-            for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.tdv[c0 + c] * (double)z[c] : 0.0;
-        }
-    }
-    double *o = a.noise + ((int64_t)k * a.Rpad + lr) * C + c0;
-    if constexpr (CW == 4) {   // a full piece: two 16-byte stores (C = 12: c0 = 0, 4, 8 doubles, 32-B aligned)
-        if (cw == 4) {
-            reinterpret_cast<double2 *>(o)[0] = double2{eps[0], eps[1]};
-            reinterpret_cast<double2 *>(o)[1] = double2{eps[2], eps[3]};
-            return;
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < CW; c++)
-        if (c < cw) o[c] = eps[c];
+    mppi_sample::sample_item<C, DIAG>(a, k, lr, (int)(tid - lr * NB));
 }
 
 // ---------------------------------------------------------------------------------------------

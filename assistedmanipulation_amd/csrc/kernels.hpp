@@ -17,9 +17,33 @@ struct Status {
     double minimum, maximum, total;
 };
 
+constexpr int MAX_X = 32;   // state dimension bound of the by-value state (FrankaRidgeback 31)
+static_assert(FR_X <= MAX_X, "state dimension");
+
+// sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
+struct SampleArgs {
+    const int *rank;          // [R] stable-order rank of rollouts 2..R-1
+    const double *Uprev;      // [H][C]  U* of the previous update (rollout 1 = -U*)
+    const double *inj;        // injected eps stream [draws][C]
+    const double *T;          // [C][C] noise transform (row-major)
+    const double *prev;       // [H][Rpad][C] eps of the previous update (kept rollouts shift it)
+    double *noise;            // [H][Rpad][C] eps of this update
+    double *Us;               // [H][C] U*_shifted, written when shift_by > 0
+    SampleParams sp;
+    int64_t begin, count, Rpad;
+    int H, C;
+    // the update's state, passed by value (no host-to-device copy on the update path): block
+    // (0, 0) writes it to x0_out for the rollout kernels
+    double x0v[MAX_X];
+    double *x0_out;
+    int X;
+    double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
+};
+
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;
+    const double *table;      // cooperative kernels: the per-body table (launch_fr_body_table)
     const StepConst *steps;   // [H]
     const double *x0;         // [X]
     const double *Ushift;     // [H][C]  U* shifted to this update
@@ -42,6 +66,14 @@ struct FrRolloutArgs {
     // cooperative kernel: per-step records for the cost kernel, [count][H][FR_NREC] (rollout-major:
     // one rollout's records are contiguous), and the folded / standalone filter() row's [H][FR_NREC]
     double *rec, *frec;
+    // U*_shifted row k is Ushift row min(k + ush, H - 1): ush = 0 with U*_shifted itself, the
+    // update's shift with U* (fused sampling)
+    int ush;
+    // fuse_sample: the launch samples its own rows' eps (samp, sample_device.hpp) before the
+    // horizon loop instead of a sample_kernel launch ahead of it; x0 comes from samp.x0v.  Block 0
+    // writes U*_shifted and x0 back for the kernels after it.
+    int fuse_sample;
+    SampleArgs samp;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -71,29 +103,6 @@ struct FrCostArgs {
     const double *frec;
     const StepConst *fsteps;
     double *fcost;
-};
-
-constexpr int MAX_X = 32;   // state dimension bound of the by-value state (FrankaRidgeback 31)
-static_assert(FR_X <= MAX_X, "state dimension");
-
-// sample(): the eps tensor of this update (mppi.cpp:242-269), one thread per (step, local rollout).
-struct SampleArgs {
-    const int *rank;          // [R] stable-order rank of rollouts 2..R-1
-    const double *Uprev;      // [H][C]  U* of the previous update (rollout 1 = -U*)
-    const double *inj;        // injected eps stream [draws][C]
-    const double *T;          // [C][C] noise transform (row-major)
-    const double *prev;       // [H][Rpad][C] eps of the previous update (kept rollouts shift it)
-    double *noise;            // [H][Rpad][C] eps of this update
-    double *Us;               // [H][C] U*_shifted, written when shift_by > 0
-    SampleParams sp;
-    int64_t begin, count, Rpad;
-    int H, C;
-    // the update's state, passed by value (no host-to-device copy on the update path): block
-    // (0, 0) writes it to x0_out for the rollout kernels
-    double x0v[MAX_X];
-    double *x0_out;
-    int X;
-    double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
 };
 
 struct PmRolloutArgs {
@@ -218,6 +227,9 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
 // The update's rollouts (fr_coop.hip): e0 / e1 = optional timing events around the launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded);
+bool fr_coop_update_fusable(int64_t count);
+constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
+hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
 
