@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -107,10 +108,10 @@ struct mppi_handle {
     double *d_table = nullptr;   // cooperative kernels' body table (built from d_model, d_cost)
     DevPointMass *d_pm = nullptr;
     StepConst *d_steps = nullptr;
-    double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr, *d_weights = nullptr;
+    double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
-    double *d_wexp = nullptr, *d_wpart = nullptr;   // large-R softmin scratch (kernels.hip SM_LARGE_R)
+    double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
     bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
@@ -337,14 +338,13 @@ bool use_coop(const mppi_handle *h)
 }
 
 // Sampling inside the cooperative update launch (fr_coop.hip fused_sample): FrankaRidgeback rows
-// in one round of four-wave workgroups.  MPPI_FUSE_SAMPLE=0 keeps the separate sample_kernel (A/B).
+// in one round of four-wave workgroups, opt-in (MPPI_FUSE_SAMPLE=1).  Measured even with the
+// separate sample_kernel (0.3604-0.3622 vs 0.3610-0.3629 ms/update at 4096 x 64): the prologue
+// delays the critical workgroup (the one whose fifth wave doubles a SIMD) by what the launch saves.
 bool fuse_sampling(const mppi_handle *h)
 {
-    static const bool off = [] {
-        const char *e = std::getenv("MPPI_FUSE_SAMPLE");
-        return e && e[0] == '0';
-    }();
-    return !off && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
+    const char *e = std::getenv("MPPI_FUSE_SAMPLE");   // per update: tests switch it in-process
+    return e && e[0] == '1' && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
            fr_coop_update_fusable(h->count);
 }
 
@@ -494,18 +494,19 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     }
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
-    for (auto &e : h->ev) CREATE_TRY(hipEventCreate(&e));
+    // timing-only events without the system-scope fence: with it each record held the next kernel
+    // on the stream back by ~6 us (cache write-back and invalidate); the host reads nothing they guard
+    for (auto &e : h->ev) CREATE_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_pub, hipEventDisableTiming));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
-    CREATE_TRY(hipEventCreate(&h->ev_opt_end));
-    CREATE_TRY(hipEventCreate(&h->ev_dyn));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_end, hipEventDisableSystemFence));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_dyn, hipEventDisableSystemFence));
     const size_t HC = (size_t)(h->H * h->C);
     CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_U, HC));
     CREATE_TRY(dalloc(h, &h->d_Us, HC));
     CREATE_TRY(dalloc(h, &h->d_costs, (size_t)h->R));
-    CREATE_TRY(dalloc(h, &h->d_weights, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
@@ -531,6 +532,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     }
     CREATE_TRY(hipHostMalloc((void **)&h->h_out, (HC + 8) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     CREATE_TRY(hipHostGetDevicePointer((void **)&h->h_out_dev, h->h_out, 0));
+    std::memset(h->h_out, 0, (HC + 8) * sizeof(double));   // the publish flag starts below every sequence
     CREATE_TRY(hipHostMalloc((void **)&h->h_opt, 8 * sizeof(double), hipHostMallocDefault));
     h->h_opt[0] = 0.0;
     CREATE_TRY(hipMemcpy(h->d_T, h->T.data(), h->T.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -1222,6 +1224,7 @@ static FinishArgs finish_args(mppi_handle *h)
     f.U = h->d_U;
     f.opt_cost = h->d_opt;
     f.out = h->h_out_dev;   // the host block, written in place (no copy launch behind the finish)
+    f.seq = (double)(h->update_count + 1);   // != 0: the block's flag starts at 0
     f.x0 = h->d_x0;
     f.x0_opt = h->d_x0_opt;
     f.X = (int)h->X;
@@ -1238,7 +1241,6 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.cost = h->d_costs;
     w.R = h->R;
     w.cost_scale = h->cost_scale;
-    w.weights = h->d_weights;
     w.status = h->d_status;
     w.noise = h->d_noise;
     w.begin = h->begin;
@@ -1263,13 +1265,14 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     HIP_TRY(launch_finish(finish_args(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
-    HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
+    const bool standalone_filter = !(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h));
+    if (standalone_filter) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));   // the side stream waits on it
     // filter(): cost of the published U* (mppi.cpp:450-479).  With the cooperative kernel it rides
     // in the next update's remainder launch (it then shares a SIMD with rollouts 0 and 1 instead of
     // doubling up a SIMD of the next update's main launch); otherwise it runs now on the side stream.
     h->opt_steps = h->d_steps;
     h->opt_state = mppi_handle::OPT_PENDING;
-    if (!(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h))) {
+    if (standalone_filter) {
         mppi_status st = launch_filter_standalone(h);
         if (st != MPPI_OK) return st;
     }
@@ -1278,11 +1281,23 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     // the next update.  On the engine stream behind the published block, it runs while the host
     // takes the result and comes back with the next state.
     HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
-    // wait for the published block by polling its event: a blocking synchronize sleeps the thread
-    // and the wake-up sat on the update's critical path (the GPU idles until the next update)
-    hipError_t q;
-    while ((q = hipEventQuery(h->timing >= 2 ? h->ev[5] : h->ev_pub)) == hipErrorNotReady) {}
-    HIP_TRY(q);
+    // wait for the published block by polling its sequence flag (finish kernels, publish_block): a
+    // blocking synchronize sleeps the thread and the wake-up sat on the update's critical path, and
+    // an event behind the finish kernel delayed the stream.  The stream is queried now and then so
+    // that a failed launch ends the wait with its error.
+    {
+        const double seq = (double)(h->update_count + 1);
+        volatile double *flag = h->h_out + HC + 6;
+        for (uint64_t spin = 1; *flag != seq; spin++) {
+            if ((spin & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(h->stream);
+                if (q != hipErrorNotReady && q != hipSuccess) HIP_TRY(q);
+                if (q == hipSuccess && *flag != seq) return fail(h, MPPI_ERR_DEVICE, "finish kernel did not publish");
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (h->timing >= 2) HIP_TRY(hipEventSynchronize(h->ev[5]));
     h->phase_open = false;
     if (h->timing >= 2) {
         for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
@@ -1360,7 +1375,13 @@ mppi_status mppi_weights(mppi_handle *h, double *out)
 {
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipMemcpy(out, h->d_weights, (size_t)h->R * sizeof(double), hipMemcpyDeviceToHost));
+    // the device keeps e_r and the normaliser (weights_gradient_kernel, finish): w_r = e_r / total,
+    // IEEE division as on the device.  Before the first update that got past optimise() the
+    // weights are the zeros they were created as.
+    Status st{};
+    HIP_TRY(hipMemcpy(&st, h->d_status, sizeof(Status), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, h->d_wexp, (size_t)h->R * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < h->R; r++) out[r] = st.total != 0.0 ? out[r] / st.total : 0.0;
     return MPPI_OK;
 }
 

@@ -723,19 +723,22 @@ __device__ __forceinline__ double wave_sum(double v)
 }
 
 // optimise() and the partial gradient in one launch (mppi.cpp:344-418), grid (H, GRAD_SPLIT).
-// Block (k, s) sums w_r eps_r over a contiguous eighth of the local rollouts of step k, one
-// rollout's C contiguous components per thread, then its 256 partials in a fixed tree into
-// gsplit[s][k] (deterministic, no atomics); the finish kernel adds the GRAD_SPLIT partials in a
-// fixed order.  The weights need min / max / count of the costs and the softmin normaliser: every
-// block computes them itself from the costs (out of L2) instead of waiting for another block, in
-// the order of one 1024-thread block - each real wave carries four of its sixteen waves lane for
-// lane, so the butterflies pair the same values and every block holds the same bits.  The block's
-// eps loads are issued first and land during the reductions.  Each block writes the weights of its
-// slice of [0, R), block (0, 0) the status words.
+// Block (k, s) sums e_r eps_r (e_r the unnormalised softmin weight) over a contiguous eighth of the
+// local rollouts of step k, one rollout's C contiguous components per thread, then its 256 partials
+// in a fixed tree into gsplit[s][k] (deterministic, no atomics); the finish kernel adds the
+// GRAD_SPLIT partials in a fixed order and divides by the normaliser total = sum_r e_r:
+// (sum_r e_r eps_r) / total for the reference's sum_r (e_r / total) eps_r, a rounding difference.
+// e_r needs min / max / count of the costs: every block computes them itself from the costs (out of
+// L2) instead of waiting for another block, in the order of one 1024-thread block - each real wave
+// carries four of its sixteen waves lane for lane, so the butterflies pair the same values and
+// every block holds the same bits.  The normaliser is not needed here: blocks (0, s) write e_r of
+// slice s of all R rollouts to wexp and its sum to Status::tsplit[s] (the finish kernel adds them,
+// the host divides for get_weights), so no block evaluates all R exponentials.  The block's eps
+// loads are issued first and land during the reductions.  Block (0, 0) writes the status words.
 constexpr int WV = 16;       // waves of the 1024-thread reduction order
 constexpr int WU = 8;        // costs per (virtual) thread and pass
 constexpr int NV = WV / 4;   // virtual waves per real wave
-constexpr int GR = 2;        // rollouts per thread whose eps is loaded up front
+constexpr int GR = 3;        // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
 
 // Large R (R > SM_LARGE_R, configs 4 / 5: every rank weighs all R global costs): recomputing
 // min / max / normaliser over all R in each of the H x GRAD_SPLIT blocks costs O(H R) exps, so
@@ -747,7 +750,10 @@ constexpr int GR = 2;        // rollouts per thread whose eps is loaded up front
 // and weights_gradient_kernel<C, true> folds the NB sums the same way for the normaliser and
 // reads e_r instead of recomputing it.
 constexpr int SM_NB = 64;
-constexpr int64_t SM_LARGE_R = 16384;
+#ifndef SM_LARGE_R_DEF
+#define SM_LARGE_R_DEF 16384
+#endif
+constexpr int64_t SM_LARGE_R = SM_LARGE_R_DEF;
 
 __device__ __forceinline__ void sm_chunk(int64_t R, int b, int64_t &r0, int64_t &r1)
 {
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
 template <int C, bool LARGE>
 __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
-    __shared__ double red[256 * C];
+    __shared__ double red[4 * C];
     __shared__ double smn[WV], smx[WV], ssum[WV];
     const int t = threadIdx.x, rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
@@ -916,43 +922,23 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
     // e_r of global rollout i: recomputed, or (LARGE) written by softmin_exp_kernel
     auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
-    if constexpr (!LARGE) {
-    double tot[NV];
-#pragma unroll
-    for (int v = 0; v < NV; v++) tot[v] = 0.0;
-    for (int64_t base = 0; base < R; base += WV * 64 * WU) {
-        double cv[WU][NV];
-#pragma unroll
-        for (int u = 0; u < WU; u++)
-#pragma unroll
-            for (int v = 0; v < NV; v++) {
-                const int64_t i = base + (int64_t)u * (WV * 64) + (NV * rw + v) * 64 + l;
-                cv[u][v] = (i < R) ? a.cost[i] : (double)NAN;
-            }
-#pragma unroll
-        for (int u = 0; u < WU; u++)
-#pragma unroll
-            for (int v = 0; v < NV; v++) {
-                const int64_t i = base + (int64_t)u * (WV * 64) + (NV * rw + v) * 64 + l;
-                if (i < R) tot[v] += expw(cv[u][v]);   // past R the one-block sum added +0.0
-            }
+    if constexpr (LARGE) {   // the normaliser is known: one partial carries it
+        if (k == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
+    } else if (k == 0) {   // slice s of [0, R): e_r and its sum
+        const int64_t wc = (R + ns - 1) / ns, w0 = (int64_t)s * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
+        double part = 0.0;
+        for (int64_t i = w0 + t; i < w1; i += 256) {
+            const double e = expw(a.cost[i]);
+            a.wexp[i] = e;
+            part += e;
+        }
+        part = wave_sum(part);
+        __syncthreads();   // smn / smx / ssum reads above are done
+        if (l == 0) ssum[rw] = part;
+        __syncthreads();
+        if (t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
     }
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
-        const double sv = wave_sum(tot[v]);
-        if (l == 0) ssum[NV * rw + v] = sv;
-    }
-    __syncthreads();
-    total = ssum[0];
-#pragma unroll
-    for (int i = 1; i < WV; i++) total += ssum[i];
-    }
-    {   // this block's slice of the weights
-        const int64_t nb = (int64_t)gridDim.x * ns, b = (int64_t)s * gridDim.x + k;
-        const int64_t wc = (R + nb - 1) / nb, w0 = b * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
-        for (int64_t i = w0 + t; i < w1; i += 256) a.weights[i] = wexp(i) / total;
-    }
-    if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; st->total = total; }
+    if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; }
     double acc[C];
 #pragma unroll
     for (int c = 0; c < C; c++) acc[c] = 0.0;
@@ -960,27 +946,25 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
         if (r < r1) {
-            const double wr = wexp(a.begin + r) / total;
+            const double wr = wexp(a.begin + r);
 #pragma unroll
             for (int c = 0; c < C; c++) acc[c] += wr * ne[m][c];
         }
     }
     for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
-        const double wr = wexp(a.begin + r) / total;
+        const double wr = wexp(a.begin + r);
         const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] += wr * n[c];
     }
+    // the block's 256 partials: butterflies within each wave, then the four wave sums in order
 #pragma unroll
-    for (int c = 0; c < C; c++) red[c * 256 + t] = acc[c];
+    for (int c = 0; c < C; c++) acc[c] = wave_sum(acc[c]);
+    if (l == 0)
+#pragma unroll
+        for (int c = 0; c < C; c++) red[rw * C + c] = acc[c];
     __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-        if (t < h)
-#pragma unroll
-            for (int c = 0; c < C; c++) red[c * 256 + t] += red[c * 256 + t + h];
-        __syncthreads();
-    }
-    if (t < C) a.gsplit[((int64_t)s * a.H + k) * C + t] = red[t * 256];
+    if (t < C) a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[C + t]) + (red[2 * C + t] + red[3 * C + t]);
 }
 
 __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
@@ -994,6 +978,27 @@ __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, i
     gpart[t] = s;
 }
 
+// The host block is complete: after every thread's stores, one system-scope release store of the
+// update's sequence number, which the host polls (no event behind the finish kernel: an event
+// record delayed the next kernel on the stream by ~6 us).  Call from every thread of the block.
+__device__ __forceinline__ void publish_block(const FinishArgs &a)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The softmin normaliser sum_r e_r from weights_gradient_kernel's GRAD_SPLIT partials, fixed order.
+__device__ __forceinline__ double softmin_total(const Status &st)
+{
+    double t = st.tsplit[0];
+#pragma unroll
+    for (int i = 1; i < GRAD_SPLIT; i++) t += st.tsplit[i];
+    return t;
+}
+
 // U* += step * gradient; Savitzky-Golay; clamp (mppi.cpp:421-447).  One workgroup.
 // SG: one thread per control dimension runs its MovingExtendedWindow (filter.cpp:19-116).
 __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
@@ -1003,6 +1008,8 @@ __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
     if (threadIdx.x == 0) sg_err = 0;
     __syncthreads();
     if (!stt.early) {
+    const double total = softmin_total(stt);
+    if (threadIdx.x == 0) a.status_w->total = total;
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
         double g;
         if (a.ns > 0) {   // stage 2 of the gradient, fixed order
@@ -1011,6 +1018,7 @@ __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
         } else {
             g = a.gpart[t];
         }
+        g /= total;   // sum_r e_r eps_r / sum_r e_r
         a.gradient[t] = g;
         a.Ushift[t] += g * a.gradient_step;
     }
@@ -1109,6 +1117,7 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 {
     __shared__ int sg_err;
     finish_block(a, sg_err);
+    publish_block(a);
 }
 
 // finish() without the Savitzky-Golay filter, one U* element per thread: every load is issued
@@ -1123,10 +1132,12 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
     const double *__restrict__ gs = a.ns > 0 ? a.gsplit : a.gpart;
     double *__restrict__ Us = a.Ushift;
     double *__restrict__ U = a.U;
+    const double total = softmin_total(*a.status);
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
         const int c = t % a.C;
         double g = gs[t];
         for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
+        g /= total;   // sum_r e_r eps_r / sum_r e_r
         double u = Us[t];
         const double uo = U[t];
         const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
@@ -1148,6 +1159,7 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
     if (threadIdx.x == 0) {
         const Status stt = *a.status;
         a.status_w->sg_error = 0;
+        if (upd) a.status_w->total = total;
         a.out[HC + 0] = oc;
         a.out[HC + 1] = (double)stt.all_nan;
         a.out[HC + 2] = (double)stt.early;
@@ -1155,6 +1167,7 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
     }
+    publish_block(a);
 }
 
 
@@ -1205,6 +1218,8 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
     if (t == 0) sg_err = 0;
     if (t < nw) wl[t] = a.sg_weights[t];
     if (upd) {
+        const double total = softmin_total(stt);
+        if (t == 0) a.status_w->total = total;
         for (int i = t; i < HC; i += blockDim.x) {
             double g;
             if (a.ns > 0) {   // stage 2 of the gradient, fixed order
@@ -1213,6 +1228,7 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
             } else {
                 g = a.gpart[i];
             }
+            g /= total;   // sum_r e_r eps_r / sum_r e_r
             a.gradient[i] = g;
             a.Ushift[i] += g * a.gradient_step;
         }
@@ -1352,6 +1368,7 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
     }
+    publish_block(a);
 }
 
 // ---------------------------------------------------------------------------------------------

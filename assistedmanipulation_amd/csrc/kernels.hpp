@@ -14,7 +14,8 @@ struct Status {
     int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
     int pad;
-    double minimum, maximum, total;
+    double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
+    double tsplit[8];                 // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };
 
 constexpr int MAX_X = 32;   // state dimension bound of the by-value state (FrankaRidgeback 31)
@@ -141,7 +142,8 @@ struct FinishArgs {
     // publish: U* <- U*_shifted and the host-visible block [U (H*C), optimal cost, status]
     double *U;
     const double *opt_cost;
-    double *out;
+    double *out;                // host block [HC + 8]: U*, then status words, then the sequence flag
+    double seq;                 // written to out[HC + 6] last, system-scope release (host polls it)
     // filter()'s state: the update's x0 copied for the optimal rollout that runs after it
     const double *x0;
     double *x0_opt;
@@ -204,18 +206,18 @@ hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
+static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser partials");
 // optimise() and the partial gradient in one launch (kernels.hip weights_gradient_kernel)
 struct WGradArgs {
     const double *cost;    // [R], global rollout index
     int64_t R;
     double cost_scale;
-    double *weights;       // [R]
     Status *status;
     const double *noise;   // [H][Rpad][C]
     int64_t begin, count, Rpad;
     int H, C;
     double *gsplit;        // [GRAD_SPLIT][H][C]
-    double *wexp;          // [R] scratch: unnormalised weights (R > SM_LARGE_R)
+    double *wexp;          // [R] unnormalised weights e_r (weights = e_r / Status::total)
     double *wpart;         // [4 * 64] scratch: per-chunk min / max / count / sum (R > SM_LARGE_R)
 };
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce

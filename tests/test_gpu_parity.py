@@ -356,3 +356,33 @@ def test_device_against_golden_fixtures(fixture):
         np.testing.assert_allclose(dev.get_gradient(), g["gradient"][j], rtol=0, atol=1e-8)
         np.testing.assert_allclose(dev.get_optimal_rollout(), g["U"][j], rtol=0, atol=1e-8)
         assert abs(dev.get_optimal_total_cost() - g["opt_cost"][j]) <= 1e-11 * abs(g["opt_cost"][j])
+
+
+@pytest.mark.parametrize("rollouts,injected", [(2046, False), (1000, False), (2046, True)])
+def test_fused_sampling_matches_sample_kernel(rollouts, injected, monkeypatch):
+    """The update launch's own sampling (MPPI_FUSE_SAMPLE=1: eps drawn in the rollout kernel's
+    prologue, U*_shifted read from U* with the shift) gives the same bits as the separate
+    sample_kernel over several shifted updates with kept rollouts (R = 2048: the fifth-wave rows
+    and the folded filter() row; R = 1002: leftover rows in several workgroups)."""
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.32, keep_best_rollouts=20, threads=8)
+    out = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("MPPI_FUSE_SAMPLE", fuse)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        rng = np.random.default_rng(11)
+        if injected:
+            t.set_noise_source(abi.MPPI_NOISE_HOST_INJECTED)
+        else:
+            t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for j in range(4):
+            if injected:
+                t.inject_noise(rng.standard_normal((t.noise_draws(0.05 * j), t.C)) * 0.1)
+            t.update(x, 0.05 * j)
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[fuse] = rec
+    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
