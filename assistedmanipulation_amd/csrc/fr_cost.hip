@@ -80,7 +80,7 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
                 r[2 * i] = v.x;
                 r[2 * i + 1] = v.y;
             }
-            c = step_cost<CK, EN>(Cs, stp[base + lane], r);
+            c = step_cost<CK, EN>(Cs, stp[base + lane], r, nullptr, nullptr);
         }
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
         __syncthreads();
@@ -97,8 +97,9 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
 // 21.5 KB per wave and held a CU to seven waves, too few to hide the loads; without it the kernel
 // is bounded by registers (four waves per SIMD).
 template <int CK, bool EN>
-__global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fr_step_cost_kernel(FrCostArgs a)
 {
+    __shared__ double Lj[FR_NB * JT_STRIDE];
     const int lane = threadIdx.x;
     const int64_t row = blockIdx.x;
     const bool frow = a.fcost != nullptr && row == a.count;
@@ -108,19 +109,27 @@ __global__ __launch_bounds__(64) void fr_step_cost_kernel(FrCostArgs a)
     const double2 *rec = reinterpret_cast<const double2 *>(frow ? a.frec : a.rec + row * H * FR_NREC);
     const StepConst *stp = frow ? a.fsteps : a.steps;
     const DevCost &Cs = *a.cost;
+    if (CK != CK_TRACK_POINT)   // per-joint parameters (84 of them for 64 lanes)
+        for (int i = lane; i < FR_NB * JT_STRIDE; i += 64) {
+            const int j = i / JT_STRIDE, f = i - j * JT_STRIDE;
+            const double *src = f < 3 ? &Cs.lower[j].bound + f : (f < 6 ? &Cs.upper[j].bound + (f - 3) : &Cs.vel_q[j]);
+            Lj[i] = *src;
+        }
+    __syncthreads();
     double J = 0.0;
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
         double r[FR_NREC];
         const double2 *src = rec + (int64_t)k * NREC2;
+        constexpr int NLOAD = CK == CK_TRACK_POINT ? NREC2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
 #pragma unroll
-        for (int i = 0; i < NREC2; i++) {
+        for (int i = 0; i < NLOAD; i++) {
             const double2 v = src[i];
             r[2 * i] = v.x;
             r[2 * i + 1] = v.y;
         }
-        const double c = step_cost<CK, EN>(Cs, stp[k], r);
+        const double c = step_cost<CK, EN>(Cs, stp[k], r, Lj, src);
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
     }
     if (lane != 0) return;

@@ -13,6 +13,7 @@
 #include "device_common.hpp"
 #include "engine_types.hpp"
 #include "kernels.hpp"
+#include "fsincos.hpp"
 
 namespace mppi_cost {
 
@@ -21,21 +22,39 @@ using mppi_dev::smin;
 
 constexpr int CK_ASSISTED_MANIPULATION = 1, CK_TRACK_POINT = 3;   // mppi_cost_kind
 
+// x / d from v_rcp_f64 and one Newton correction applied to the product (four ops; the rcp's
+// 2.8e-8 relative error squares to ~1e-15, against the IEEE quotient's ten-op sequence).  Only
+// for barrier quotients: d = 0 (v on the bound) gives NaN, and there the barrier selects `over`.
+__device__ __forceinline__ double fquot(double x, double d)
+{
+    const double r = __builtin_amdgcn_rcp(d);
+    const double t = x * r;
+    const double e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(t, e, t);
+}
+
 // AssistedManipulation barriers (assisted_manipulation.cpp), written as selects
-__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v)
+__device__ __forceinline__ double right_barrier(double bound, double scale, double mx, double v)
 {
-    const double d = v - b.bound;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (b.bound - v), b.max);
-    return (v >= b.bound) ? over : under;
+    const double d = v - bound;
+    const double over = mx + scale * (d * d);
+    const double under = smin(fquot(scale, bound - v), mx);
+    return (v >= bound) ? over : under;
 }
-__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v)
+__device__ __forceinline__ double left_barrier(double bound, double scale, double mx, double v)
 {
-    const double d = b.bound - v;
-    const double over = b.max + b.scale * (d * d);
-    const double under = smin(b.scale / (v - b.bound), b.max);
-    return (v <= b.bound) ? over : under;
+    const double d = bound - v;
+    const double over = mx + scale * (d * d);
+    const double under = smin(fquot(scale, v - bound), mx);
+    return (v <= bound) ? over : under;
 }
+__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v) { return right_barrier(b.bound, b.scale, b.max, v); }
+__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v) { return left_barrier(b.bound, b.scale, b.max, v); }
+
+// Per-joint parameters of the objective staged in LDS by the kernel (fr_cost.hip): lower barrier
+// (bound, scale, max), upper barrier, velocity weight - uniform loads next to their use instead of
+// 84 scalar registers the compiler loaded up front and spilled.
+constexpr int JT_STRIDE = 7;
 
 // trajectory_cost's velocity part on the EE frame velocity (assisted_manipulation.cpp:237-290)
 __device__ __forceinline__ double trajectory_term(const DevCost &Cs, const StepConst &sc, const double *vl)
@@ -61,20 +80,41 @@ __device__ __forceinline__ double manipulability_term(const DevCost &Cs, const d
 
 // AssistedManipulation::get_cost at the record's state with its kinematics
 template <bool EN>
-__device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r)
+__device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
+                                                             const double *Lj, const double2 *src)
 {
     double j0 = 0.0, j1 = 0.0, v0 = 0.0, v1 = 0.0;
+    int off = 0;
 #pragma unroll
     for (int j = 0; j < FR_NB; j++) {
+        // joint j's parameters are read after joint j - 1's terms: left to itself the compiler
+        // hoisted all 84 LDS reads to the top (168 registers live, two waves per SIMD)
+        asm volatile("" : "+v"(off) : "v"(j < 6 ? j0 : j1));
+        const double *P = Lj + off;
+        off += JT_STRIDE;
         const double q = r[REC_QQD + 2 * j], vq = fabs(r[REC_QQD + 2 * j + 1]);
-        const double lj = left_barrier(Cs.lower[j], q) + right_barrier(Cs.upper[j], q);
-        const double lv = Cs.vel_q[j] * (vq * vq);
+        const double lj = left_barrier(P[0], P[1], P[2], q) + right_barrier(P[3], P[4], P[5], q);
+        const double lv = P[6] * (vq * vq);
         if (j < 6) { j0 += lj; v0 += lv; }
         else { j1 += lj; v1 += lv; }
     }
     const double joint = j0 + j1, vel = v0 + v1;
+    // the rest of the record (r holds the (q, qd) pairs only) is loaded through a pointer that
+    // waits for the joint sums: the remaining terms start after them instead of interleaving with
+    // them and holding their values live (two waves per SIMD instead of four)
+    static_assert(REC_EE == 2 * FR_NB && FR_NREC - REC_EE == 18, "record tail");
+    double rest[FR_NREC - REC_EE], yaw = r[REC_QQD + 4];
+    const double2 *tp = src + REC_EE / 2;
+    asm volatile("" : "+v"(tp), "+v"(yaw) : "v"(joint), "v"(vel));
+#pragma unroll
+    for (int i = 0; i < (FR_NREC - REC_EE) / 2; i++) {
+        const double2 v = tp[i];
+        rest[2 * i] = v.x;
+        rest[2 * i + 1] = v.y;
+    }
+    r = rest - REC_EE;   // r[REC_EE ..] from here on
     double s, c;
-    sincos(r[REC_QQD + 4], &s, &c);   // base yaw q_2
+    fsincos(yaw, &s, &c, sincos_constants());   // base yaw q_2
     const double *ee = r + REC_EE, *am = r + REC_AM;
     double wc = 0.0;
     {
@@ -127,7 +167,7 @@ __device__ __forceinline__ double track_point_cost(const DevCost &Cs, const doub
         joint += below + above;
     }
     double s, c;
-    sincos(r[REC_QQD + 4], &s, &c);
+    fsincos(r[REC_QQD + 4], &s, &c, sincos_constants());
     const double r22 = (1.0 - c) + c;
     const double off0 = (0.3 * c + (-s) * 0.0) + 0.0 * 0.15;
     const double off1 = (0.3 * s + c * 0.0) + 0.0 * 0.15;
@@ -149,10 +189,13 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
 
 // gamma_k times the objective at step record r
 template <int CK, bool EN>
-__device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r)
+// (AssistedManipulation: r holds the record's (q, qd) pairs, the rest is read from src; TrackPoint:
+// r holds the whole record)
+__device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
+                                           const double2 *src)
 {
     if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r);
-    else return sc.gamma_k * assisted_manipulation_cost<EN>(Cs, sc, r);
+    else return sc.gamma_k * assisted_manipulation_cost<EN>(Cs, sc, r, Lj, src);
 }
 
 }  // namespace mppi_cost
