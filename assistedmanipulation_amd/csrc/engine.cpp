@@ -111,6 +111,7 @@ struct mppi_handle {
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
+    CostStats *d_cstats = nullptr;   // the update's cost min / max / count (cost kernel atomics)
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
@@ -511,6 +512,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_cstats, 1));
     CREATE_TRY(dalloc(h, &h->d_wpart, 4 * 64));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
@@ -980,6 +982,13 @@ void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 // ---- update ---------------------------------------------------------------------------------
 
 // The cost kernel's view of a cooperative rollout launch (same rows, records and outputs).
+// Unsharded cooperative FrankaRidgeback updates take the costs' min / max / count from the cost
+// kernel (CostStats); sharded ones see only their own costs there and reduce after the all-reduce.
+static bool cost_stats_used(const mppi_handle *h)
+{
+    return h->world == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
+}
+
 static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
 {
     FrCostArgs c{};
@@ -997,7 +1006,7 @@ static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
     c.frec = a.frec;
     c.fsteps = a.fsteps;
     c.fcost = a.fcost;
-    (void)h;
+    c.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     return c;
 }
 
@@ -1114,6 +1123,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         std::memcpy(sa.x0v, state, (size_t)h->X * sizeof(double));   // the state rides in the launch
         sa.x0_out = h->d_x0;
         sa.X = (int)h->X;
+        sa.stats = h->d_cstats;
         if (h->tdiag)
             for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
         if (!fuse) HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
@@ -1158,13 +1168,14 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.fcost = h->d_opt;
             a.frec = h->d_rec_opt;
         }
-        bool folded = false;
+        bool folded = false, costs_done = false;
+        a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? h->ev[1] : nullptr,
-                                          ev_in_launch ? h->ev_dyn : nullptr, &folded));
+                                          ev_in_launch ? h->ev_dyn : nullptr, &folded, &costs_done));
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
-            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+            if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
             if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
@@ -1251,6 +1262,7 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.gsplit = h->d_gsplit;
     w.wexp = h->d_wexp;
     w.wpart = h->d_wpart;
+    w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_weights_gradient(w, h->d_gpart, h->world > 1, h->stream));
     return MPPI_OK;

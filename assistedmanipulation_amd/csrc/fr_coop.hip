@@ -1425,6 +1425,70 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #endif
 }
 
+// ---- the objective inside the launch (a.costs_in_launch) ----------------------------------------
+// With R + 1 = S + 3 rows on 4S / 16 SIMDs one SIMD runs the fifth wave beside a main wave, and
+// every other SIMD idles for the last third of the launch while those two finish.  The objective
+// of the rows (fr_cost_terms.hpp rollout_cost: a pass per rollout, lane = step) runs there: each
+// main wave evaluates its own rows after its horizon loop, except the fifth wave's SIMD-mate, whose
+// rows - and then the fifth wave's - waves 1..3 of the workgroup evaluate once those waves signal
+// their records stored (an LDS flag each), so nothing is added to the doubled SIMD.  The per-joint
+// parameters are the body table's T_LO .. T_VW fields (stride MB).
+
+// J of local rollout lr (or the folded filter() row) from its records, written out
+template <int CK, bool EN>
+__device__ __forceinline__ void launch_row_cost(const FrRolloutArgs &a, int64_t lr, int lane, const double *Lmodel)
+{
+    const bool frow = a.fcost != nullptr && lr == a.count;
+    if (!(lr < a.count || frow)) return;
+    if (frow && (a.status->all_nan || a.status->sg_error)) return;   // no filter() when the update threw
+    const double J = mppi_cost::rollout_cost<CK, EN, MB>(*a.cost, frow ? a.fsteps : a.steps,
+                                                          frow ? a.frec : a.rec + lr * a.H * FR_NREC, a.H, lane,
+                                                          Lmodel + T_LO);
+    if (lane == 0) {
+        if (frow) *a.fcost = J;
+        else {
+            a.cost_out[a.begin + lr] = J;
+            mppi_cost::fold_cost_stats(a.stats, J, lr);
+        }
+    }
+}
+
+// This wave's record stores are complete and visible to the workgroup; then raise the flag
+__device__ __forceinline__ void signal_records(int *flag)
+{
+    __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wait_records(int *flag)
+{
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(8);
+}
+
+// Main wave wv (0..3) of the workgroup after its horizon loop.  xr: the workgroup's fifth wave has
+// rows (its SIMD-mate, wave 0, then only signals).
+template <int CK, bool EN>
+__device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
+                                             bool xr)
+{
+    if (xr && wv == 0) {
+        signal_records(Lflag);
+        return;
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
+#pragma unroll 1
+    for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
+    if (!xr) return;
+    wait_records(Lflag);
+#pragma unroll 1
+    for (int i = wv - 1; i < ROWS_PER_WAVE; i += 3) launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + i, lane, Lmodel);
+    wait_records(Lflag + 1);
+#pragma unroll 1
+    for (int i = wv - 1; i < ROWS_PER_WAVE; i += 3)
+        launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
+}
+
 // The update's state into LDS: from the launch's arguments with fused sampling, else from x0
 __device__ __forceinline__ void stage_x0(const FrRolloutArgs &a, double *Lx0)
 {
@@ -1487,6 +1551,7 @@ __device__ __forceinline__ void fused_sample(const FrRolloutArgs &a, int64_t r0,
 {
     const SampleArgs &sa = a.samp;
     if (blockIdx.x == 0) {
+        if (sa.stats) mppi_sample::reset_cost_stats(sa.stats, threadIdx.x);
         if (sa.sp.shift_by > 0)
             for (int i = threadIdx.x; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
         if ((int)threadIdx.x < sa.X) sa.x0_out[threadIdx.x] = sa.x0v[threadIdx.x];
@@ -1527,6 +1592,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     __syncthreads();
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
+    if constexpr (WPB == 4) {
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, false);
+    }
 }
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and a fifth wave
@@ -1539,6 +1607,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
+    __shared__ int Lflag[2];   // launch_costs: wave 0's and the fifth wave's records are stored
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
@@ -1548,6 +1617,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
     stage_body_table(a, Lmodel, 320);
     stage_x0(a, Lx0);
+    if (threadIdx.x < 2) Lflag[threadIdx.x] = 0;
     if (a.fuse_sample) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
@@ -1555,15 +1625,18 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     __syncthreads();
     double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
+    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the fifth wave has rows
     if (wv < 4) {
         const int wblk = blockIdx.x * 4 + wv;
 #ifdef MAIN_PRIO
         __builtin_amdgcn_s_setprio(MAIN_PRIO);
 #endif
         coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
-    } else if ((int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows) {
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, xr);
+    } else if (xr) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
         coop_rows<CK, EN, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
+        if (a.costs_in_launch) signal_records(Lflag + 1);
     }
 }
 
@@ -1622,6 +1695,14 @@ hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, doub
     return hipGetLastError();
 }
 
+// The objective inside the update launch (launch_costs); MPPI_COSTS_IN_LAUNCH=0 keeps the
+// separate fr_step_cost_kernel (A/B)
+static bool costs_in_launch_enabled()
+{
+    const char *e = getenv("MPPI_COSTS_IN_LAUNCH");
+    return !(e && e[0] == '0');
+}
+
 // Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample
 // their own rows, a.fuse_sample) for `count` rows.
 bool fr_coop_update_fusable(int64_t count)
@@ -1632,8 +1713,10 @@ bool fr_coop_update_fusable(int64_t count)
 }
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded)
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
+                                 bool *costs_done)
 {
+    *costs_done = false;
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     *folded = false;
@@ -1654,6 +1737,8 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.xbase = groups * WG_ROWS;
     a.xrows = xrows;
     *folded = frow;
+    a.costs_in_launch = costs_in_launch_enabled() ? 1 : 0;
+    *costs_done = a.costs_in_launch != 0;
     if (e0) (void)hipEventRecord(e0, s);
 #ifdef FORCE_X
     if (false) {}

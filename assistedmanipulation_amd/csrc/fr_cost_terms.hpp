@@ -51,9 +51,10 @@ __device__ __forceinline__ double left_barrier(double bound, double scale, doubl
 __device__ __forceinline__ double right_barrier(const DevBarrier &b, double v) { return right_barrier(b.bound, b.scale, b.max, v); }
 __device__ __forceinline__ double left_barrier(const DevBarrier &b, double v) { return left_barrier(b.bound, b.scale, b.max, v); }
 
-// Per-joint parameters of the objective staged in LDS by the kernel (fr_cost.hip): lower barrier
-// (bound, scale, max), upper barrier, velocity weight - uniform loads next to their use instead of
-// 84 scalar registers the compiler loaded up front and spilled.
+// Per-joint parameters of the objective in LDS, joint j at Lj[j JS ..]: lower barrier (bound,
+// scale, max), upper barrier, velocity weight - uniform loads next to their use instead of 84
+// scalar registers the compiler loaded up front and spilled.  fr_cost.hip stages them with stride
+// JT_STRIDE; the rollout kernel reads them from its body table.
 constexpr int JT_STRIDE = 7;
 
 // trajectory_cost's velocity part on the EE frame velocity (assisted_manipulation.cpp:237-290)
@@ -79,7 +80,7 @@ __device__ __forceinline__ double manipulability_term(const DevCost &Cs, const d
 }
 
 // AssistedManipulation::get_cost at the record's state with its kinematics
-template <bool EN>
+template <bool EN, int JS>
 __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
                                                              const double *Lj, const double2 *src)
 {
@@ -91,7 +92,7 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
         // hoisted all 84 LDS reads to the top (168 registers live, two waves per SIMD)
         asm volatile("" : "+v"(off) : "v"(j < 6 ? j0 : j1));
         const double *P = Lj + off;
-        off += JT_STRIDE;
+        off += JS;
         const double q = r[REC_QQD + 2 * j], vq = fabs(r[REC_QQD + 2 * j + 1]);
         const double lj = left_barrier(P[0], P[1], P[2], q) + right_barrier(P[3], P[4], P[5], q);
         const double lv = P[6] * (vq * vq);
@@ -187,15 +188,54 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
     return __hiloint2double(hi, lo);
 }
 
-// gamma_k times the objective at step record r
-template <int CK, bool EN>
-// (AssistedManipulation: r holds the record's (q, qd) pairs, the rest is read from src; TrackPoint:
-// r holds the whole record)
+// gamma_k times the objective at step record r (AssistedManipulation: r holds the record's (q, qd)
+// pairs, the rest is read from src; TrackPoint: r holds the whole record)
+template <int CK, bool EN, int JS = JT_STRIDE>
 __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
                                            const double2 *src)
 {
     if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r);
-    else return sc.gamma_k * assisted_manipulation_cost<EN>(Cs, sc, r, Lj, src);
+    else return sc.gamma_k * assisted_manipulation_cost<EN, JS>(Cs, sc, r, Lj, src);
+}
+
+// J of one rollout from its H step records (rollout-major, FR_NREC doubles each) by one wave:
+// lane k evaluates step k (64 steps a pass) and the wave sums the step costs in step order, as the
+// reference accumulates J += cost (mppi.cpp:322-337); a NaN step makes the sum NaN (the reference's
+// early stop), canonicalised to the quiet NaN it stores.  The same value on every lane.
+template <int CK, bool EN, int JS = JT_STRIDE>
+__device__ __forceinline__ double rollout_cost(const DevCost &Cs, const StepConst *stp, const double *rec, int H, int lane,
+                                               const double *Lj)
+{
+    constexpr int NREC2 = FR_NREC / 2;
+    double J = 0.0;
+    for (int base = 0; base < H; base += 64) {
+        const int n = (H - base < 64) ? H - base : 64;
+        const int k = base + (lane < n ? lane : 0);
+        double r[FR_NREC];
+        const double2 *src = reinterpret_cast<const double2 *>(rec) + (int64_t)k * NREC2;
+        constexpr int NLOAD = CK == CK_TRACK_POINT ? NREC2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
+#pragma unroll
+        for (int i = 0; i < NLOAD; i++) {
+            const double2 v = src[i];
+            r[2 * i] = v.x;
+            r[2 * i + 1] = v.y;
+        }
+        const double c = step_cost<CK, EN, JS>(Cs, stp[k], r, Lj, src);
+        for (int i = 0; i < n; i++) J += readlane_f64(c, i);
+    }
+    return isnan(J) ? (double)NAN : J;
+}
+
+// The costs' min / max / count (CostStats) gain one cost (NaN ones are not counted), in the slot
+// of its rollout index
+__device__ __forceinline__ void fold_cost_stats(CostStats *st, double J, int64_t r)
+{
+    if (!st || isnan(J)) return;
+    const unsigned long long key = mppi_dev::cost_order_key(J);
+    const int i = (int)(r & (CS_SLOTS - 1));
+    atomicMin(&st->kmin[16 * i], key);
+    atomicMax(&st->kmax[16 * i], key);
+    atomicAdd(&st->count[32 * i], 1u);
 }
 
 }  // namespace mppi_cost

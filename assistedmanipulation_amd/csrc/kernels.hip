@@ -583,6 +583,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
     constexpr int NB = DIAG ? (C + 3) / 4 : 1;   // thread pieces per (step, rollout)
     const int k = blockIdx.y;
     if (blockIdx.x == 0 && k == 0 && (int)threadIdx.x < a.X) a.x0_out[threadIdx.x] = a.x0v[threadIdx.x];
+    if (blockIdx.x == 0 && k == 0 && a.stats) mppi_sample::reset_cost_stats(a.stats, threadIdx.x);
     if (blockIdx.x == 0 && a.sp.shift_by > 0 && (int)threadIdx.x < C) {
         const int c = threadIdx.x;
         a.Us[k * C + c] = mppi_sample::shifted_u(a, k, c);
@@ -857,6 +858,21 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         maximum = smx[0];
         valid = ssum[0];
         total = ssum[1];
+    } else if (a.stats) {   // from the objective's atomics (exact: the same values as the pass)
+        static_assert(CS_SLOTS == 64, "one slot per lane");
+        unsigned long long kn = a.stats->kmin[16 * l], kx = a.stats->kmax[16 * l];
+        unsigned int n = a.stats->count[32 * l];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long on = __shfl_xor(kn, o, 64), ox = __shfl_xor(kx, o, 64);
+            kn = on < kn ? on : kn;
+            kx = ox > kx ? ox : kx;
+            n += __shfl_xor(n, o, 64);
+        }
+        minimum = n ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
+        maximum = n ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
+        valid = (double)n;
+        total = 0.0;
     } else {
     // min / max / count over the non-NaN costs
     double mn[NV], mx[NV], cn[NV];
@@ -905,6 +921,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         maximum = smax(maximum, smx[i]);
         valid += ssum[i];
     }
+
     __syncthreads();
     total = 0.0;
     }
@@ -1378,6 +1395,9 @@ namespace mppi_eng {
 
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s)
 {
+#ifdef DIAG_SKIP_RANK   // timing diagnostics only: the kept rollouts are then not the best ones
+    return hipSuccess;
+#endif
     if (S <= 0) return hipSuccess;
     if (S <= RANK_TILED_MAX) {   // rank[] zeroed by the finish kernel (or at create)
         const unsigned nb = (unsigned)((S + RANK_T - 1) / RANK_T);

@@ -18,6 +18,18 @@ struct Status {
     double tsplit[8];                 // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };
 
+// min / max / count of the update's non-NaN costs, accumulated with order-independent atomics on
+// order-preserving keys (exact, so deterministic) by whoever evaluates the objective (the rollout
+// launch or fr_step_cost_kernel), and read by weights_gradient_kernel instead of a pass over all R
+// costs in each of its blocks.  CS_SLOTS slots, one 128-byte line each, spread the atomics: on one
+// address 4099 x 3 of them cost ~40 us.  Reset by the update's sampling launch.
+constexpr int CS_SLOTS = 64;
+struct CostStats {
+    unsigned long long kmin[CS_SLOTS * 16];
+    unsigned long long kmax[CS_SLOTS * 16];
+    unsigned int count[CS_SLOTS * 32];
+};
+
 constexpr int MAX_X = 32;   // state dimension bound of the by-value state (FrankaRidgeback 31)
 static_assert(FR_X <= MAX_X, "state dimension");
 
@@ -39,6 +51,7 @@ struct SampleArgs {
     double *x0_out;
     int X;
     double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
+    CostStats *stats;   // reset by block (0, 0) for this update's costs (may be null)
 };
 
 struct FrRolloutArgs {
@@ -75,6 +88,11 @@ struct FrRolloutArgs {
     // writes U*_shifted and x0 back for the kernels after it.
     int fuse_sample;
     SampleArgs samp;
+    // costs_in_launch (set by launch_fr_coop_update): the waves evaluate the objective of the rows
+    // after their horizon loops (fr_coop.hip launch_costs) instead of fr_step_cost_kernel; stats as
+    // in FrCostArgs
+    int costs_in_launch;
+    CostStats *stats;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -104,6 +122,7 @@ struct FrCostArgs {
     const double *frec;
     const StepConst *fsteps;
     double *fcost;
+    CostStats *stats;         // the update's rollout costs (not filter()'s) folded in, or null
 };
 
 struct PmRolloutArgs {
@@ -219,6 +238,7 @@ struct WGradArgs {
     double *gsplit;        // [GRAD_SPLIT][H][C]
     double *wexp;          // [R] unnormalised weights e_r (weights = e_r / Status::total)
     double *wpart;         // [4 * 64] scratch: per-chunk min / max / count / sum (R > SM_LARGE_R)
+    const CostStats *stats;   // min / max / count from the cost kernel (unsharded), or null: a pass
 };
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
@@ -228,7 +248,8 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
 // The update's rollouts (fr_coop.hip): e0 / e1 = optional timing events around the launch.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded);
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
+                                 bool *costs_done);
 bool fr_coop_update_fusable(int64_t count);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed

@@ -69,6 +69,18 @@ __device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, 
     }
 }
 
+// The cost statistics before this update's costs are folded in: slot i by thread i (< CS_SLOTS).
+// Device-scope atomic exchanges, performed where the folds' atomics are: with fused sampling the
+// reset and the folds share a launch, and a plain store would wait in this XCD's L2 while the
+// other XCDs' atomics read the previous update's values.
+__device__ __forceinline__ void reset_cost_stats(CostStats *st, int i)
+{
+    if (i >= CS_SLOTS) return;
+    atomicExch(&st->kmin[16 * i], ~0ull);
+    atomicExch(&st->kmax[16 * i], 0ull);
+    atomicExch(&st->count[32 * i], 0u);
+}
+
 // U*_shifted row k, component c (mppi.cpp:197-207): U* shifted left by shift_by, the last column
 // repeated; only meaningful when shift_by > 0 (otherwise U*_shifted keeps its contents)
 __device__ __forceinline__ double shifted_u(const SampleArgs &a, int k, int c)

@@ -163,15 +163,21 @@ def main():
     value = S_total * traj.H / (elapsed / args.steps)
     lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
     dyn_ms = dyn / nd                                     # the rollout (dynamics) kernel alone, timed loop
-    records = not lane   # the coop kernel writes step records; fr_step_cost_kernel evaluates them
-    cost_ms = float(kt[1] - kt[5]) if records else 0.0      # fr_step_cost_kernel (breakdown pass)
+    records = not lane   # the coop kernel writes step records; the objective reads them back
+    # one round of four-wave workgroups (fr_coop.hip fr_coop_update_fusable): the launch evaluates
+    # the objective itself in the SIMDs' idle tail (MPPI_COSTS_IN_LAUNCH=0: fr_step_cost_kernel)
+    count_all = traj.R // world + (1 if rank < traj.R % world else 0)
+    groups = count_all // 16
+    xrows = count_all - 16 * groups + (1 if count_all - 16 * groups > 0 else 0)
+    in_launch = records and os.environ.get("MPPI_COSTS_IN_LAUNCH") != "0" and 0 < groups <= 256 and xrows <= 4 * groups
+    cost_ms = float(kt[1] - kt[5]) if records and not in_launch else 0.0   # fr_step_cost_kernel (breakdown pass)
     traffic = None
     if os.path.exists(PMC_JSON) and world == 1 and default_workload:
         with open(PMC_JSON) as f:
             traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
     units = count_local * traj.H
-    flops_unit = FLOPS_DYN_PER_ROLLOUT_STEP if records else FLOPS_PER_ROLLOUT_STEP
+    flops_unit = FLOPS_DYN_PER_ROLLOUT_STEP if records and not in_launch else FLOPS_PER_ROLLOUT_STEP
     flops = flops_unit * units
     achieved_tflops = flops / (dyn_ms * 1e-3) / 1e12
     if rank != 0:
@@ -203,13 +209,15 @@ def main():
         # at one wave per SIMD, so it is bound by issue slots and dependency chains, not by a
         # datapath peak; the fraction is reported against the fp64 vector peak.
         "roofline": {"bound": "valu", "compute": "fp64 VALU, latency/issue-bound at one wave per SIMD",
-                     "kernel": "fr_rollout_kernel" if lane else "fr_coop_x_kernel", "achieved": achieved_tflops,
+                     "kernel": "fr_rollout_kernel" if lane else ("fr_coop_x_kernel (dynamics + objective)" if in_launch else "fr_coop_x_kernel"),
+                     "achieved": achieved_tflops,
                      "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
                      "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
                      "flops_per_rollout_step": flops_unit},
-        "hbm": {"rollout_algorithmic_GBs": (BYTES_PER_ROLLOUT_STEP if records else BYTES_EPS_PER_ROLLOUT_STEP) * units
-                / (dyn_ms * 1e-3) / 1e9,
+        "hbm": {"rollout_algorithmic_GBs": ((BYTES_PER_ROLLOUT_STEP + (BYTES_REC_PER_ROLLOUT_STEP if in_launch else 0.0))
+                                            if records else BYTES_EPS_PER_ROLLOUT_STEP) * units / (dyn_ms * 1e-3) / 1e9,
+                "objective_in_rollout_launch": in_launch,
                 "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if records and cost_ms > 0 else None,
                 "peak_GBs": HBM_PEAK_GBS},
     }
