@@ -74,6 +74,12 @@ struct mppi_handle {
     // reference scalar state (mppi.hpp:545-657)
     double last_shift_time = 0, rollout_time = 0, last_rollout_time = 0, update_last = 0, update_duration = 0;
     uint64_t update_count = 0;
+    // draws ahead (launch_draw_ahead behind phase 3): valid for the update whose inputs match
+    struct AheadSig {
+        uint64_t update_index, seed;
+        int64_t begin, count, H, C;
+    } ahead{};
+    bool ahead_valid = false;
     int64_t shift_by = 0, shifted = 0;
     int compat_uint8 = 0;
     int noise_source = MPPI_NOISE_DEVICE_PHILOX;
@@ -342,6 +348,18 @@ bool use_coop(const mppi_handle *h)
 // in one round of four-wave workgroups, opt-in (MPPI_FUSE_SAMPLE=1).  Measured even with the
 // separate sample_kernel (0.3604-0.3622 vs 0.3610-0.3629 ms/update at 4096 x 64): the prologue
 // delays the critical workgroup (the one whose fifth wave doubles a SIMD) by what the launch saves.
+// The next update's draws made behind the publish (phase 3) so that its sampling launch leaves
+// the critical path: device Philox, diagonal transform, an update whose rollout launch runs one
+// round of workgroups (it copies the kept columns in, fused_sample mode 2).  MPPI_DRAW_AHEAD=0
+// turns it off (A/B).
+static bool draw_ahead_possible(const mppi_handle *h)
+{
+    const char *e = std::getenv("MPPI_DRAW_AHEAD");
+    if (e && e[0] == '0') return false;
+    return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C && h->tdiag &&
+           h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count) && h->S <= RANK_TILED_MAX;
+}
+
 bool fuse_sampling(const mppi_handle *h)
 {
     const char *e = std::getenv("MPPI_FUSE_SAMPLE");   // per update: tests switch it in-process
@@ -351,6 +369,7 @@ bool fuse_sampling(const mppi_handle *h)
 
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
+    h->ahead_valid = false;   // the draws ahead live in the buffers freed here
     dfree(h, h->d_noise);
     dfree(h, h->d_noise_prev);
     h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
@@ -1102,8 +1121,13 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     }
     // the stable order of the previous costs was ranked behind the previous publish (phase 3)
     if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
-    // the cooperative update launch samples its own rows when it runs one round of workgroups
-    const bool fuse = fuse_sampling(h);
+    // this update's draws were made ahead (behind the previous publish) when nothing they depend
+    // on changed since; else the cooperative update launch may sample its own rows (opt-in)
+    const bool ahead = h->ahead_valid && draw_ahead_possible(h) && h->ahead.update_index == h->update_count &&
+                       h->ahead.seed == h->seed && h->ahead.begin == h->begin && h->ahead.count == h->count &&
+                       h->ahead.H == h->H && h->ahead.C == h->C;
+    h->ahead_valid = false;
+    const bool fuse = ahead || fuse_sampling(h);
     SampleArgs sa{};
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
@@ -1153,7 +1177,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.trace = h->d_trace;
         a.rec = h->d_rec;
         if (fuse) {   // U*_shifted read from U* with the shift; the state from the launch
-            a.fuse_sample = 1;
+            a.fuse_sample = ahead ? 2 : 1;
             a.samp = sa;
             a.Ushift = sp.shift_by > 0 ? h->d_U : h->d_Us;
             a.ush = sp.shift_by > 0 ? (int)std::min<int64_t>(sp.shift_by, h->H) : 0;
@@ -1292,7 +1316,23 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     // sample()'s stable order of this update's costs (final here: all-reduced when sharded), for
     // the next update.  On the engine stream behind the published block, it runs while the host
     // takes the result and comes back with the next state.
-    HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
+    if (!draw_ahead_possible(h)) HIP_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
+    else {   // the next update's draws, into the buffer it will write, with the rank in one launch
+        SampleArgs sa{};
+        sa.Uprev = h->d_U;
+        sa.noise = h->d_noise_prev;
+        sa.sp.update_index = h->update_count + 1;
+        sa.sp.seed = h->seed;
+        sa.begin = h->begin;
+        sa.count = h->count;
+        sa.Rpad = h->Rpad;
+        sa.H = (int)h->H;
+        sa.C = (int)h->C;
+        for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
+        HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->stream));
+        h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
+        h->ahead_valid = true;
+    }
     // wait for the published block by polling its sequence flag (finish kernels, publish_block): a
     // blocking synchronize sleeps the thread and the wake-up sat on the update's critical path, and
     // an event behind the finish kernel delayed the stream.  The stream is queried now and then so

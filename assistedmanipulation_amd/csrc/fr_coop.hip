@@ -1546,16 +1546,67 @@ __device__ __forceinline__ void fused_sample_rows(const SampleArgs &sa, int64_t 
     }
 }
 
+// Draws ahead (a.fuse_sample == 2): the eps tensor already holds this update's draws, made by
+// draw_ahead_kernel behind the previous update; only the kept rollouts' columns from the previous
+// eps remain (rank < keep: steps k < shifted, or every step when nothing shifted).  A wave copies
+// its own kept rows before its horizon loop (rk: the row's rank, loaded at kernel entry so the load
+// overlaps the table staging), lanes 0..11 of a row = 3 pieces x 4 step phases, loads of UN steps
+// in flight before their stores.  Waves without a kept row start at once.
+__device__ __forceinline__ int kept_rank(const FrRolloutArgs &a, int64_t lr)
+{
+    const int64_t g = a.samp.begin + lr;
+    return (a.fuse_sample == 2 && lr < a.count && g >= 2) ? a.samp.rank[g] : 0x7FFFFFFF;
+}
+__device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t lr, int lane, int rk)
+{
+    const SampleArgs &sa = a.samp;
+    const bool kept = rk < sa.sp.keep;
+    if (__ballot(kept) == 0) return;
+    const int j = lane & 15;
+    if (kept && j < 12) {
+        const int blk = j % 3, ph = j / 3;
+        const int kend = sa.sp.shift_by > 0 ? (int)sa.sp.shifted : sa.H;
+        const int64_t sh = sa.sp.shift_by > 0 ? sa.sp.shift_by : 0;
+        constexpr int UN = 8;
+        for (int k0 = ph; k0 < kend; k0 += 4 * UN) {
+            double2 v[UN][2];
+#pragma unroll
+            for (int u = 0; u < UN; u++) {
+                const int k = k0 + 4 * u < kend ? k0 + 4 * u : ph;
+                const double2 *src = reinterpret_cast<const double2 *>(sa.prev + (((int64_t)k + sh) * sa.Rpad + lr) * FR_C + 4 * blk);
+                v[u][0] = src[0];
+                v[u][1] = src[1];
+            }
+#pragma unroll
+            for (int u = 0; u < UN; u++) {
+                if (k0 + 4 * u >= kend) break;
+                double2 *dst = reinterpret_cast<double2 *>(sa.noise + ((int64_t)(k0 + 4 * u) * sa.Rpad + lr) * FR_C + 4 * blk);
+                dst[0] = v[u][0];
+                dst[1] = v[u][1];
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // the copies land before the row's lanes read them
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+// Block 0's share of sampling in fused / draws-ahead launches: U*_shifted and x0 written back for
+// the kernels after the launch, the cost statistics reset (before any row's objective folds in).
+template <int NT>
+__device__ __forceinline__ void block0_sample_writes(const FrRolloutArgs &a, int t)
+{
+    const SampleArgs &sa = a.samp;
+    if (sa.stats) mppi_sample::reset_cost_stats(sa.stats, t);
+    if (sa.sp.shift_by > 0)
+        for (int i = t; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
+    if (t < sa.X) sa.x0_out[t] = sa.x0v[t];
+}
+
 template <int NT>
 __device__ __forceinline__ void fused_sample(const FrRolloutArgs &a, int64_t r0, int n1, int64_t x0r, int n2)
 {
     const SampleArgs &sa = a.samp;
-    if (blockIdx.x == 0) {
-        if (sa.stats) mppi_sample::reset_cost_stats(sa.stats, threadIdx.x);
-        if (sa.sp.shift_by > 0)
-            for (int i = threadIdx.x; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
-        if ((int)threadIdx.x < sa.X) sa.x0_out[threadIdx.x] = sa.x0v[threadIdx.x];
-    }
+    if (blockIdx.x == 0) block0_sample_writes<NT>(a, threadIdx.x);
     if (sa.sp.tdiag) fused_sample_rows<NT, true>(sa, r0, n1, x0r, n2);
     else fused_sample_rows<NT, false>(sa, r0, n1, x0r, n2);
 }
@@ -1581,15 +1632,23 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int rowi = lane >> 4;
     const int wrow = wv * ROWS_PER_WAVE + rowi;   // row within the workgroup
     const int wblk = blockIdx.x * WPB + wv;        // wave index in the launch
+    int rk = 0x7FFFFFFF;
+    if constexpr (WPB == 4) rk = kept_rank(a, (int64_t)wblk * ROWS_PER_WAVE + rowi);
     stage_body_table(a, Lmodel, 64 * WPB);
     stage_x0(a, Lx0);
     if constexpr (WPB == 4) {
-        if (a.fuse_sample) {
+        if (a.fuse_sample == 1) {
             const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE;
             fused_sample<64 * WPB>(a, r0, (int)(r0 + 4 * ROWS_PER_WAVE < a.count ? 4 * ROWS_PER_WAVE : a.count - r0), 0, 0);
         }
     }
     __syncthreads();
+    if constexpr (WPB == 4) {
+        if (a.fuse_sample == 2) {
+            if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);
+            kept_rows_wave(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, rk);
+        }
+    }
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
@@ -1615,10 +1674,13 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #ifdef PRO_TRACE   // kernel entry per main wave (slot 3; coop_rows records the loop's start and end)
     if (a.trace && lane == 0 && wv < 4) a.trace[4 * (blockIdx.x * 4 + wv) + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
+    const int64_t lr = wv < 4 ? (int64_t)(blockIdx.x * 4 + wv) * ROWS_PER_WAVE + rowi
+                              : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row
+    const int rk = kept_rank(a, lr);
     stage_body_table(a, Lmodel, 320);
     stage_x0(a, Lx0);
     if (threadIdx.x < 2) Lflag[threadIdx.x] = 0;
-    if (a.fuse_sample) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
+    if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
         fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
@@ -1626,6 +1688,10 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __syncthreads();
     double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
     const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the fifth wave has rows
+    if (a.fuse_sample == 2) {
+        if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the doubled SIMD
+        if (wv < 4 || xr) kept_rows_wave(a, lr, lane, rk);
+    }
     if (wv < 4) {
         const int wblk = blockIdx.x * 4 + wv;
 #ifdef MAIN_PRIO

@@ -546,11 +546,20 @@ __global__ __launch_bounds__(RANK_T) void rank_merge_kernel(const double *__rest
 // block (x, y) ranks its 256 rollouts against the 256 of tile y staged in LDS; off the diagonal
 // tile the index tie-break is block-uniform, so one compare per pair.  rank[] is zeroed by the
 // finish kernel that precedes this launch on the engine stream.
+__device__ __forceinline__ void rank_tile(const double *__restrict__ cost, int64_t S, int *__restrict__ rank, unsigned bx,
+                                          unsigned by, uint64_t *kj);
+
 __global__ __launch_bounds__(RANK_T) void rank_tiled_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
 {
     __shared__ uint64_t kj[RANK_T];
-    const int64_t i = (int64_t)blockIdx.x * RANK_T + threadIdx.x;
-    const int64_t j0 = (int64_t)blockIdx.y * RANK_T;
+    rank_tile(cost, S, rank, blockIdx.x, blockIdx.y, kj);
+}
+
+__device__ __forceinline__ void rank_tile(const double *__restrict__ cost, int64_t S, int *__restrict__ rank, unsigned bx,
+                                          unsigned by, uint64_t *kj)
+{
+    const int64_t i = (int64_t)bx * RANK_T + threadIdx.x;
+    const int64_t j0 = (int64_t)by * RANK_T;
     const int64_t jl = j0 + threadIdx.x;
     kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
     __syncthreads();
@@ -558,10 +567,10 @@ __global__ __launch_bounds__(RANK_T) void rank_tiled_kernel(const double *__rest
     const uint64_t ki = cost_key(cost[2 + i]);
     const int jn = (int)((S - j0) < RANK_T ? (S - j0) : RANK_T);
     int cnt = 0;
-    if (blockIdx.y < blockIdx.x) {          // every j < i: equal keys count
+    if (by < bx) {          // every j < i: equal keys count
 #pragma unroll 8
         for (int t = 0; t < jn; t++) cnt += (kj[t] <= ki) ? 1 : 0;
-    } else if (blockIdx.y > blockIdx.x) {   // every j > i
+    } else if (by > bx) {   // every j > i
 #pragma unroll 8
         for (int t = 0; t < jn; t++) cnt += (kj[t] < ki) ? 1 : 0;
     } else {
@@ -592,6 +601,63 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
     const int64_t lr = tid / NB;
     if (lr >= a.count) return;
     mppi_sample::sample_item<C, DIAG>(a, k, lr, (int)(tid - lr * NB));
+}
+
+// The next update's draws, ahead (engine.cpp): every local rollout's eps for every step as if
+// nothing were kept.  Rollout 0 zero, rollout 1 = -U* (the U* just published), the rest Philox by
+// (rollout, step) (sample_device.hpp philox_index).  The update's rollout launch copies the kept
+// rollouts' shifted columns over these once the shift is known (fr_coop.hip kept_columns).
+template <int C>
+__device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned bx, int k)
+{
+    static_assert(C % 4 == 0, "full pieces");
+    constexpr int NB = C / 4;
+    const int64_t tid = (int64_t)bx * 256 + threadIdx.x;
+    const int64_t lr = tid / NB;
+    if (lr >= a.count) return;
+    const int blk = (int)(tid - lr * NB);
+    const int64_t g = a.begin + lr;
+    mppi_sample::EpsPlan e{a.Uprev, 0.0, 0, true};   // rollout 0: zeros
+    if (g == 1) {
+        e.p = a.Uprev + (int64_t)k * C + 4 * blk;
+        e.sgn = -1.0;
+    } else if (g >= 2) {
+        e.draw = mppi_sample::philox_index(g, k, a.H);
+        e.use_p = false;
+    }
+    double v[4] = {0.0, 0.0, 0.0, 0.0}, eps[4];
+    if (e.use_p) {
+        const double2 *p2 = reinterpret_cast<const double2 *>(e.p);
+        const double2 lo = p2[0], hi = p2[1];
+        v[0] = lo.x; v[1] = lo.y; v[2] = hi.x; v[3] = hi.y;
+    }
+    mppi_sample::eps_finish(a, e, blk, v, eps);
+    mppi_sample::store_eps<C, true>(a, k, lr, blk, eps);
+}
+
+// The draws ahead and the stable rank of this update's costs in one launch (neither reads the
+// other's output): blocks [0, nr^2) rank tiles, the rest draw (grid nx x H flattened)
+template <int C>
+__global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank,
+                                                        unsigned nr, SampleArgs a, unsigned nx)
+{
+    __shared__ uint64_t kj[RANK_T];
+    static_assert(RANK_T == 256, "one block size");
+    const unsigned b = blockIdx.x;
+    if (b < nr * nr) rank_tile(cost, S, rank, b % nr, b / nr, kj);
+    else {
+        const unsigned d = b - nr * nr;
+        draw_ahead_block<C>(a, d % nx, (int)(d / nx));
+    }
+}
+
+hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, hipStream_t s)
+{
+    if (a.C != FR_C || a.count <= 0 || S > RANK_TILED_MAX) return hipErrorInvalidValue;
+    constexpr int NB = FR_C / 4;
+    const unsigned nx = (unsigned)((a.count * NB + 255) / 256), nr = (unsigned)((S + RANK_T - 1) / RANK_T);
+    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -84,8 +84,9 @@ struct FrRolloutArgs {
     // update's shift with U* (fused sampling)
     int ush;
     // fuse_sample: the launch samples its own rows' eps (samp, sample_device.hpp) before the
-    // horizon loop instead of a sample_kernel launch ahead of it; x0 comes from samp.x0v.  Block 0
-    // writes U*_shifted and x0 back for the kernels after it.
+    // horizon loop instead of a sample_kernel launch ahead of it (1), or only copies the kept
+    // rollouts' columns into draws made ahead (2, draw_ahead_kernel); x0 comes from samp.x0v.
+    // Block 0 writes U*_shifted and x0 back for the kernels after it and resets the cost stats.
     int fuse_sample;
     SampleArgs samp;
     // costs_in_launch (set by launch_fr_coop_update): the waves evaluate the objective of the rows
@@ -222,6 +223,10 @@ constexpr int64_t RANK_TILED_MAX = 8192;
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s);
 inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
+// The next update's draws before its state, time and stable order exist (FrankaRidgeback, diagonal
+// transform, device Philox): rollout 0 zero, rollout 1 = -U*, the rest Philox by (rollout, step);
+// in the same launch as the stable rank of this update's costs (S <= RANK_TILED_MAX; rank[] cleared)
+hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage

@@ -14,6 +14,13 @@ namespace mppi_sample {
 
 using namespace mppi_eng;
 
+// Device Philox mode: the counter of (global rollout g, step k).  A rollout's draws then do not
+// depend on its rank in the previous costs' stable order, so the next update's draws can be made
+// before that order and the next state and time exist (draws ahead, engine.cpp); the kept
+// rollouts' shifted columns are copied in afterwards.  The injected stream is consumed in the
+// reference's draw order (mppi.cpp:242-262), so host-driven parity runs see the reference's noise.
+__device__ __forceinline__ int64_t philox_index(int64_t g, int k, int H) { return g * H + k; }
+
 // eps = T z for one draw.  z from the Philox stream keyed by (seed, update, draw).
 __device__ __forceinline__ void philox_draw(const SampleParams &P, int64_t draw, const double *T, int C, double *eps)
 {
@@ -65,7 +72,7 @@ __device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, 
     if (P.injected) {
         for (int c = 0; c < C; c++) eps[c] = inj[draw * C + c];
     } else {
-        philox_draw(P, draw, T, C, eps);
+        philox_draw(P, philox_index(g, (int)k, H), T, C, eps);
     }
 }
 
@@ -92,7 +99,7 @@ __device__ __forceinline__ double shifted_u(const SampleArgs &a, int k, int c)
 // eps of step k, rollout g (local lr, stable-order rank `rank`, 0 for g < 2), piece blk (DIAG:
 // components 4 blk .. 4 blk + 3, zero past C; else all C): rollout 0 is the zero-noise rollout;
 // rollout 1 carries -U*; kept rollouts shift the previous update's eps; the rest draw
-// (Philox4x32-10, counter = global draw index in the reference's draw order, or the injected stream).
+// (Philox4x32-10 by philox_index, or the injected stream in the reference's draw order).
 template <int C, bool DIAG>
 __device__ __forceinline__ void sample_eps(const SampleArgs &a, int k, int64_t lr, int64_t g, int rank, int blk,
                                            double *eps)
@@ -130,6 +137,7 @@ __device__ __forceinline__ void sample_eps(const SampleArgs &a, int k, int64_t l
 #pragma unroll
             for (int c = 0; c < CW; c++) eps[c] = (c < cw) ? a.inj[draw * C + c0 + c] : 0.0;
         } else {
+            draw = philox_index(g, k, a.H);
             mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};
             mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, (uint32_t)P.seed, (uint32_t)(P.seed >> 32));
             float z[4];
@@ -167,10 +175,14 @@ __device__ __forceinline__ EpsPlan eps_plan(const SampleArgs &a, int k, int64_t 
     } else if (rank < P.keep && (P.shift_by <= 0 || k < P.shifted)) {
         e.p = a.prev + (((int64_t)k + (P.shift_by > 0 ? P.shift_by : 0)) * a.Rpad + lr) * C + c0;
     } else {
-        e.draw = rank < P.keep ? (int64_t)rank * (a.H - P.shifted) + (k - P.shifted)
-                               : P.keep_draws + (int64_t)(rank - P.keep) * a.H + k;
-        if (P.injected) e.p = a.inj + e.draw * C + c0;
-        else e.use_p = false;
+        if (P.injected) {
+            e.draw = rank < P.keep ? (int64_t)rank * (a.H - P.shifted) + (k - P.shifted)
+                                   : P.keep_draws + (int64_t)(rank - P.keep) * a.H + k;
+            e.p = a.inj + e.draw * C + c0;
+        } else {
+            e.draw = philox_index(g, k, a.H);
+            e.use_p = false;
+        }
     }
     return e;
 }

@@ -386,3 +386,27 @@ def test_fused_sampling_matches_sample_kernel(rollouts, injected, monkeypatch):
     for j, (a, b) in enumerate(zip(out["0"], out["1"])):
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+
+
+@pytest.mark.parametrize("rollouts", [2046, 1000])
+def test_draws_ahead_match_sampling_at_update(rollouts, monkeypatch):
+    """Draws made behind the previous publish (MPPI_DRAW_AHEAD, the default for device Philox) with
+    the kept rollouts' columns copied in by the rollout launch equal the sampling launch at update
+    time, bit for bit, over updates whose shift varies (5, 2, 5, 0 steps) with kept rollouts."""
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.32, keep_best_rollouts=20, threads=8)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
+    out = {}
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("MPPI_DRAW_AHEAD", ahead)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for tm in times:
+            t.update(x, tm)
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[ahead] = rec
+    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
