@@ -184,6 +184,8 @@ class Trajectory:
         self.R, self.H, self.C, self.X = R.value, H.value, Cc.value, X.value
         self._rolled_out_state = np.asarray(configuration.initial_state, dtype=np.float64).copy()
         self._rolled_out_state[:] = 0.0   # m_rollout_state.setZero() (mppi.cpp:121)
+        self._state_buf = np.zeros(self._rolled_out_state.size, dtype=np.float64)
+        self._state_ptr = _p(self._state_buf)
         self._update_last = 0.0
         self._update_count = 0
 
@@ -279,10 +281,12 @@ class Trajectory:
     # -- the hot path ------------------------------------------------------------------------
     def update(self, state, time):
         """Trajectory::update (mppi.cpp:154-187)."""
-        s = np.ascontiguousarray(state, dtype=np.float64)
-        assert s.size == self.X
-        self._check(self._L.mppi_update(self._h, _p(s), float(time)))
-        self._rolled_out_state = s.copy()
+        buf = self._state_buf   # one contiguous buffer and its pointer, built once: the update
+        np.copyto(buf, np.reshape(state, -1))   # path is latency-bound (microseconds per call)
+        st = self._L.mppi_update(self._h, self._state_ptr, float(time))
+        if st != abi.MPPI_OK:
+            self._check(st)
+        self._rolled_out_state = buf   # copied when queried (get_rolled_out_state)
         self._update_last = float(time)
         self._update_count += 1
 
@@ -345,7 +349,7 @@ class Trajectory:
         return self.R
 
     def get_rolled_out_state(self):
-        return self._rolled_out_state
+        return self._rolled_out_state.copy()
 
     def _vec(self, fn, n):
         out = np.zeros(n)
