@@ -357,7 +357,7 @@ static bool draw_ahead_possible(const mppi_handle *h)
     const char *e = std::getenv("MPPI_DRAW_AHEAD");
     if (e && e[0] == '0') return false;
     return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C && h->tdiag &&
-           h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count) && h->S <= RANK_TILED_MAX;
+           h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count);
 }
 
 bool fuse_sampling(const mppi_handle *h)
@@ -1329,7 +1329,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         sa.H = (int)h->H;
         sa.C = (int)h->C;
         for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
-        HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->stream));
+        HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
         h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
         h->ahead_valid = true;
     }

@@ -651,11 +651,18 @@ __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict
     }
 }
 
-hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, hipStream_t s)
+hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
+                                       hipStream_t s)
 {
-    if (a.C != FR_C || a.count <= 0 || S > RANK_TILED_MAX) return hipErrorInvalidValue;
+    if (a.C != FR_C || a.count <= 0) return hipErrorInvalidValue;
     constexpr int NB = FR_C / 4;
-    const unsigned nx = (unsigned)((a.count * NB + 255) / 256), nr = (unsigned)((S + RANK_T - 1) / RANK_T);
+    const unsigned nx = (unsigned)((a.count * NB + 255) / 256);
+    unsigned nr = (unsigned)((S + RANK_T - 1) / RANK_T);
+    if (S > RANK_TILED_MAX) {   // O(S log S) rank in its own launches, then the draws alone
+        const hipError_t e = launch_rank(cost, S, rank, sorted, s);
+        if (e != hipSuccess) return e;
+        nr = 0;
+    }
     hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx);
     return hipGetLastError();
 }

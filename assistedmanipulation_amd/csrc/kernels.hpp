@@ -225,8 +225,9 @@ inline int64_t rank_scratch(int64_t S) { return ((S + 255) / 256) * 256; }
 hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 // The next update's draws before its state, time and stable order exist (FrankaRidgeback, diagonal
 // transform, device Philox): rollout 0 zero, rollout 1 = -U*, the rest Philox by (rollout, step);
-// in the same launch as the stable rank of this update's costs (S <= RANK_TILED_MAX; rank[] cleared)
-hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, hipStream_t s);
+// with the stable rank of this update's costs (one launch when S <= RANK_TILED_MAX; rank[] cleared)
+hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
+                             hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage

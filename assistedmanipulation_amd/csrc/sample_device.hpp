@@ -192,7 +192,7 @@ __device__ __forceinline__ void eps_finish(const SampleArgs &a, const EpsPlan &e
 {
     if (e.use_p) {
 #pragma unroll
-        for (int c = 0; c < 4; c++) eps[c] = e.sgn * v[c];
+        for (int c = 0; c < 4; c++) eps[c] = e.sgn == 0.0 ? 0.0 : e.sgn * v[c];   // rollout 0: +0, as sampled
     } else {
         const SampleParams &P = a.sp;
         mppi_dev::u32x4 ctr{(uint32_t)e.draw, (uint32_t)((uint64_t)e.draw >> 32), (uint32_t)P.update_index, (uint32_t)blk};

@@ -410,3 +410,55 @@ def test_draws_ahead_match_sampling_at_update(rollouts, monkeypatch):
     for j, (a, b) in enumerate(zip(out["0"], out["1"])):
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+
+
+def test_two_philox_shards_draw_ahead_equal_unsharded():
+    """Device Philox across two shards on one GPU (phase-split ABI, host all-reduces): each shard
+    holds 4098 rollouts, so its rollout launch runs one round of workgroups and its draws are made
+    ahead; S = 8194 > RANK_TILED_MAX, so the rank takes the chunk + merge path before those draws.
+    The unsharded handle (8196 rollouts) samples at update time.  Draws are indexed by (rollout,
+    step): the noise is identical, the costs too, U* to the gradient's summation order."""
+    conf = am.frankaridgeback_configuration(rollouts=8194, horison=0.08, keep_best_rollouts=20, threads=8)
+    mk = lambda: am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    single, shards = mk(), [mk(), mk()]
+    for r, t in enumerate([single] + shards):
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        if t is not single:
+            t.set_shard(2, r - 1)
+    hip = _hip()
+    R, HC = single.R, single.H * single.C
+    x = am.huddled_state()
+
+    def allreduce(ptrs, n):
+        bufs = [np.zeros(n) for _ in ptrs]
+        for p, b in zip(ptrs, bufs):
+            assert hip.hipMemcpy(b.ctypes.data, p, n * 8, 2) == 0   # D2H
+        s = bufs[0] + bufs[1]
+        for p in ptrs:
+            assert hip.hipMemcpy(p, s.ctypes.data, n * 8, 1) == 0   # H2D
+
+    for j in range(4):
+        t = 0.05 * j
+        single.update(x, t)
+        for sh in shards:
+            sh.update_phase1(x, t)
+        hip.hipDeviceSynchronize()
+        allreduce([sh.device_costs_ptr() for sh in shards], R)
+        for sh in shards:
+            sh.update_phase2()
+        hip.hipDeviceSynchronize()
+        allreduce([sh.device_gradient_ptr() for sh in shards], HC)
+        for sh in shards:
+            sh.update_phase3(t)
+        full = single.noise()
+        for r, sh in enumerate(shards):   # a shard's noise() holds its rows at their global indices
+            b, e = am.shard_range(R, 2, r)
+            mine, ref = sh.noise()[b:e], full[b:e]
+            d = max(2 - b, 0)   # rollout 1 carries -U*, which differs in the last bits (gradient order)
+            np.testing.assert_array_equal(mine[d:], ref[d:], err_msg="update %d shard %d noise" % (j, r))
+            np.testing.assert_allclose(mine[:d], ref[:d], rtol=0, atol=1e-12)
+        for sh in shards:
+            np.testing.assert_allclose(sh.costs(), single.costs(), rtol=1e-13, atol=0)
+            np.testing.assert_allclose(sh.get_optimal_rollout(), single.get_optimal_rollout(), rtol=0, atol=1e-12)
+            assert sh.argmin() == single.argmin()
