@@ -777,24 +777,9 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
 // One workgroup of 1024 threads.
 // ---------------------------------------------------------------------------------------------
 // Block-wide reductions for one 1024-thread workgroup: wave butterflies, then 16 wave partials.
-__device__ __forceinline__ double wave_min(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = smin(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_max(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = smax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_sum(double v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ double wave_min(double v) { return mppi_dev::wave_min_dpp(v); }
+__device__ __forceinline__ double wave_max(double v) { return mppi_dev::wave_max_dpp(v); }
+__device__ __forceinline__ double wave_sum(double v) { return mppi_dev::wave_sum_dpp(v); }
 
 // optimise() and the partial gradient in one launch (mppi.cpp:344-418), grid (H, GRAD_SPLIT).
 // Block (k, s) sums e_r eps_r (e_r the unnormalised softmin weight) over a contiguous eighth of the
@@ -933,15 +918,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         total = ssum[1];
     } else if (a.stats) {   // from the objective's atomics (exact: the same values as the pass)
         static_assert(CS_SLOTS == 64, "one slot per lane");
-        unsigned long long kn = a.stats->kmin[16 * l], kx = a.stats->kmax[16 * l];
-        unsigned int n = a.stats->count[32 * l];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long on = __shfl_xor(kn, o, 64), ox = __shfl_xor(kx, o, 64);
-            kn = on < kn ? on : kn;
-            kx = ox > kx ? ox : kx;
-            n += __shfl_xor(n, o, 64);
-        }
+        const unsigned long long kn = mppi_dev::wave_umin64_dpp(a.stats->kmin[16 * l]);
+        const unsigned long long kx = mppi_dev::wave_umax64_dpp(a.stats->kmax[16 * l]);
+        const unsigned int n = (unsigned int)mppi_dev::wave_sum_dpp((double)a.stats->count[32 * l]);
         minimum = n ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
         maximum = n ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
         valid = (double)n;
