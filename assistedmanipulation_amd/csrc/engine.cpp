@@ -117,7 +117,11 @@ struct mppi_handle {
     double *d_x0 = nullptr, *d_U = nullptr, *d_Us = nullptr, *d_noise = nullptr, *d_noise_prev = nullptr, *d_costs = nullptr;
     double *d_gpart = nullptr, *d_grad = nullptr, *d_T = nullptr, *d_inj = nullptr, *d_opt = nullptr;
     double *d_cmin = nullptr, *d_cmax = nullptr, *d_x0_opt = nullptr, *d_gsplit = nullptr;
-    CostStats *d_cstats = nullptr;   // the update's cost min / max / count (cost kernel atomics)
+    CostStats *d_cstats = nullptr;
+    // sharded with an engine-owned communicator: the rank's costs at their global slots, zero
+    // elsewhere for good (nothing writes those), all-reduced out of place into d_costs - no clear
+    // per update (a fill launch and its gap)
+    double *d_costs_local = nullptr;   // the update's cost min / max / count (cost kernel atomics)
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
@@ -370,6 +374,7 @@ bool fuse_sampling(const mppi_handle *h)
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
     h->ahead_valid = false;   // the draws ahead live in the buffers freed here
+    if (h->d_costs_local) HIP_TRY(hipMemset(h->d_costs_local, 0, (size_t)h->R * sizeof(double)));   // a new range
     dfree(h, h->d_noise);
     dfree(h, h->d_noise_prev);
     h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
@@ -754,6 +759,7 @@ mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char uniqu
     std::memcpy(&id, unique_id, 128);
     HIP_TRY(hipSetDevice(h->device));
     NCCL_TRY(ncclCommInitRank(&h->comm, world, id, rank));
+    if (!h->d_costs_local) HIP_TRY(dalloc(h, &h->d_costs_local, (size_t)h->R));
     return MPPI_OK;
 }
 
@@ -1008,6 +1014,13 @@ static bool cost_stats_used(const mppi_handle *h)
     return h->world == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
 }
 
+// Where an update's rollout costs go: d_costs, or the rank's zero-padded local vector that the
+// engine's own all-reduce sums into d_costs
+static double *rollout_costs_out(const mppi_handle *h)
+{
+    return (h->world > 1 && h->comm) ? h->d_costs_local : h->d_costs;
+}
+
 static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
 {
     FrCostArgs c{};
@@ -1120,7 +1133,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         h->inj_pending.erase(h->inj_pending.begin(), h->inj_pending.begin() + (long)need);
     }
     // the stable order of the previous costs was ranked behind the previous publish (phase 3)
-    if (h->world > 1) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
+    // phase-split callers all-reduce d_costs in place: clear the other ranks' slots first
+    if (h->world > 1 && !h->comm) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
     // this update's draws were made ahead (behind the previous publish) when nothing they depend
     // on changed since; else the cooperative update launch may sample its own rows (opt-in)
     const bool ahead = h->ahead_valid && draw_ahead_possible(h) && h->ahead.update_index == h->update_count &&
@@ -1164,7 +1178,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.x0 = h->d_x0;
         a.Ushift = h->d_Us;
         a.noise = h->d_noise;
-        a.cost_out = h->d_costs;
+        a.cost_out = rollout_costs_out(h);
         a.begin = h->begin;
         a.count = h->count;
         a.Rpad = h->Rpad;
@@ -1216,7 +1230,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.x0 = h->d_x0;
         a.Ushift = h->d_Us;
         a.noise = h->d_noise;
-        a.cost_out = h->d_costs;
+        a.cost_out = rollout_costs_out(h);
         a.begin = h->begin;
         a.count = h->count;
         a.Rpad = h->Rpad;
@@ -1385,7 +1399,7 @@ mppi_status mppi_update(mppi_handle *h, const double *state, double time)
     if (st != MPPI_OK) return st;
     if (h->world > 1) {
         if (!h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
-        NCCL_TRY(ncclAllReduce(h->d_costs, h->d_costs, (size_t)h->R, ncclDouble, ncclSum, h->comm, h->stream));
+        NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R, ncclDouble, ncclSum, h->comm, h->stream));
     }
     st = mppi_update_phase2(h);
     if (st != MPPI_OK) return st;
