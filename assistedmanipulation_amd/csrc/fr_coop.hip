@@ -413,12 +413,10 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
         : "+&v"(m[0]), "+&v"(m[1]), "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
         : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
 }
-// pivot 0
-__device__ __forceinline__ void gj_pivot_0(double *Mc)
+// pivot 0 (d = the composite mass of body 0; inv = 1 / d)
+__device__ __forceinline__ void gj_pivot_0(double *Mc, double inv)
 {
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[0]));
-    const double nt = neg_quot(Mc[0], d);
+    const double nt = -Mc[0] * inv;
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
@@ -434,12 +432,10 @@ __device__ __forceinline__ void gj_pivot_0(double *Mc)
         : "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
         : "v"(nt));
 }
-// pivot 1
-__device__ __forceinline__ void gj_pivot_1(double *Mc)
+// pivot 1 (d = the composite mass of body 1; inv = 1 / d)
+__device__ __forceinline__ void gj_pivot_1(double *Mc, double inv)
 {
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[1]));
-    const double nt = neg_quot(Mc[1], d);
+    const double nt = -Mc[1] * inv;
     asm(""
         "v_fmac_f64_dpp %0, %0, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
@@ -816,6 +812,7 @@ struct LaneConst {
     int m_live;     // j < 12: the lane owns a body
     int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
+    double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
@@ -1134,7 +1131,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 #ifdef PHASE_TRACE
     t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
 #endif
-    gj_pivot_0(Mc); gj_pivot_1(Mc); gj_pivot_2(Mc); gj_pivot_3(Mc); gj_pivot_4(Mc); gj_pivot_5(Mc);
+    gj_pivot_0(Mc, L.inv_m0); gj_pivot_1(Mc, L.inv_m1); gj_pivot_2(Mc); gj_pivot_3(Mc); gj_pivot_4(Mc); gj_pivot_5(Mc);
     gj_pivot_6(Mc); gj_pivot_7(Mc); gj_pivot_8(Mc); gj_pivot_9(Mc); gj_pivot_10(Mc); gj_pivot_11(Mc);
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
     // tau' at L_TP and every other lane its column in its own block row (read above, dead now), so
@@ -1301,6 +1298,8 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
         L.anc = anc;
     }
     L.mc = M[T_MC];
+    L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
+    L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
 
     double q = jl ? x0p[jb] : 0.0;
     double qd = jl ? x0p[FR_NB + jb] : 0.0;
