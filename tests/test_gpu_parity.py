@@ -388,17 +388,19 @@ def test_fused_sampling_matches_sample_kernel(rollouts, injected, monkeypatch):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
 
 
-@pytest.mark.parametrize("rollouts", [2046, 1000])
-def test_draws_ahead_match_sampling_at_update(rollouts, monkeypatch):
+@pytest.mark.parametrize("rollouts,objective", [(2046, "am"), (1000, "am"), (2046, "energy"), (1000, "track_point")])
+def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
     """Draws made behind the previous publish (MPPI_DRAW_AHEAD, the default for device Philox) with
     the kept rollouts' columns copied in by the rollout launch equal the sampling launch at update
-    time, bit for bit, over updates whose shift varies (5, 2, 5, 0 steps) with kept rollouts."""
+    time, bit for bit, over updates whose shift varies (5, 2, 5, 0 steps) with kept rollouts; for
+    the default objective, the energy-tank variant (articulated-body kernel) and TrackPoint."""
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.32, keep_best_rollouts=20, threads=8)
     times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
+    make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
     out = {}
     for ahead in ("0", "1"):
         monkeypatch.setenv("MPPI_DRAW_AHEAD", ahead)
-        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), make_cost())
         t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
         t.set_forecast(am.constant_forecast(t.H))
         x = am.huddled_state()
