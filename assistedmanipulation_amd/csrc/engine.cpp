@@ -325,6 +325,15 @@ mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
         }
         if (!ok) { why = "body " + std::to_string(i) + " joint type/axis does not match the FrankaRidgeback topology"; return MPPI_ERR_UNSUPPORTED; }
     }
+    // The planar base's x / y joints sit unrotated on the world (robot.urdf x_base_joint /
+    // y_base_joint, rpy 0 0 0): the solve takes their motion subspaces as the unit axes
+    // (column_dots, and the zero M_01 of gj_pivot_0).
+    for (int i = 0; i < 2; i++)
+        for (int k = 0; k < 9; k++)
+            if (d.bodies[i].rotation[k] != ((k % 4 == 0) ? 1.0 : 0.0)) {
+                why = "body " + std::to_string(i) + " (planar base joint) placement must be unrotated";
+                return MPPI_ERR_UNSUPPORTED;
+            }
     if (d.end_effector.parent != FR_EE_PARENT || d.arm_mount.parent != FR_AM_PARENT) {
         why = "end-effector / arm-mount frame parents do not match the FrankaRidgeback topology";
         return MPPI_ERR_UNSUPPORTED;

@@ -126,3 +126,6 @@ def test_create_rejects_unsupported_models():
     dyn = am.FrankaRidgebackDynamics()
     dyn.model.bodies[11].parent = 10
     assert _create(dyn=dyn) is None and "topology" in _err()
+    dyn = am.FrankaRidgebackDynamics()
+    dyn.model.bodies[1].rotation[1] = 1e-3   # the solve takes the base joints' axes as world x / y
+    assert _create(dyn=dyn) is None and "must be unrotated" in _err()
