@@ -65,6 +65,7 @@ PROTOTYPES = {
     "mppi_kernel_times_nowait": (C.c_int, [_h, C.POINTER(C.c_float)]),
     "mppi_kernel_times_detail": (C.c_int, [_h, C.POINTER(C.c_float), C.c_int]),
     "mppi_set_timing": (C.c_int, [_h, C.c_int]),
+    "mppi_rollout_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
 }
 
 _lib = None

@@ -59,6 +59,13 @@ struct mppi_handle {
     // HIP-event timing on the update path (mppi_set_timing): 0 none, 1 the rollout kernel alone
     // ([5]), 2 every phase.  Each event record costs the stream a few microseconds between kernels.
     int timing = 0;
+    // timing level 1 records the rollout launch's event pair into a ring; the elapsed times are
+    // read later (mppi_rollout_kernel_times), not in the update that recorded them: reading one
+    // right behind the publish held the host ~70 us before it returned
+    static constexpr int EV_RING = 64;
+    hipEvent_t ev_ring[2 * EV_RING] = {};
+    int ring_head = 0, ring_count = 0;   // next pair to record; recorded pairs not yet read
+    bool ring_unread = false;            // kernel_ms[5] not yet taken from the newest pair
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
     double dt = 0, gradient_step = 0, cost_scale = 0, gamma = 1;
@@ -731,6 +738,8 @@ void mppi_destroy(mppi_handle *h)
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : h->ev_ring)
+        if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1177,7 +1186,16 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     }
     // timing level 1 with the cooperative kernel: the rollout launch records its own events
     const bool ev_in_launch = h->timing == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
-    if (h->timing >= 1 && !ev_in_launch) HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    // the rollout launch's event pair: the ring's next pair at level 1, ev[1] / ev_dyn at level 2
+    hipEvent_t ev_r0 = h->ev[1], ev_r1 = h->ev_dyn;
+    if (h->timing == 1) {
+        ev_r0 = h->ev_ring[2 * h->ring_head];
+        ev_r1 = h->ev_ring[2 * h->ring_head + 1];
+        h->ring_head = (h->ring_head + 1) % mppi_handle::EV_RING;
+        h->ring_count = std::min(h->ring_count + 1, (int)mppi_handle::EV_RING);
+        h->ring_unread = true;
+    }
+    if (h->timing >= 1 && !ev_in_launch) HIP_TRY(hipEventRecord(ev_r0, h->stream));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         FrRolloutArgs a{};
         a.model = h->d_model;
@@ -1218,14 +1236,14 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         bool folded = false, costs_done = false;
         a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
         if (use_coop(h)) {
-            HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? h->ev[1] : nullptr,
-                                          ev_in_launch ? h->ev_dyn : nullptr, &folded, &costs_done));
+            HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
+                                          &folded, &costs_done));
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
             if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
-            if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+            if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
         }
         if (folded) {   // the optimal cost is ready with this update's rollouts; phase 3's host block
                         // carries it back (finish_kernel copies d_opt), on the same stream
@@ -1247,7 +1265,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.H = (int)h->H;
         a.optimal = 0;
         HIP_TRY(launch_pm_rollout(a, h->stream));
-        if (h->timing >= 1) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+        if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
     }
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     h->updated_once = true;
@@ -1378,7 +1396,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
         (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
     }
-    if (h->timing >= 1) (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
+    if (h->timing >= 2) (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
     if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
@@ -1589,6 +1607,10 @@ mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
 mppi_status mppi_set_timing(mppi_handle *h, int level)
 {
     if (!h || level < 0 || level > 2) return MPPI_ERR_INVALID;
+    if (level == 1 && !h->ev_ring[0]) {
+        HIP_TRY(hipSetDevice(h->device));
+        for (auto &e : h->ev_ring) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    }
     h->timing = level;
     for (float &m : h->kernel_ms) m = 0.0f;
     return MPPI_OK;
@@ -1599,7 +1621,28 @@ mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
     if (!h || !ms || n < 0 || n > 6) return MPPI_ERR_INVALID;
     if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
+    if (h->ring_unread) {   // level 1: the newest recorded pair
+        const int i = (h->ring_head + mppi_handle::EV_RING - 1) % mppi_handle::EV_RING;
+        HIP_TRY(hipEventSynchronize(h->ev_ring[2 * i + 1]));
+        (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev_ring[2 * i], h->ev_ring[2 * i + 1]);
+        h->ring_unread = false;
+    }
     std::memcpy(ms, h->kernel_ms, (size_t)n * sizeof(float));
+    return MPPI_OK;
+}
+
+mppi_status mppi_rollout_kernel_times(mppi_handle *h, float *ms, int capacity, int *count)
+{
+    if (!h || !count || capacity < 0 || (capacity > 0 && !ms)) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    const int n = std::min(h->ring_count, capacity);
+    for (int j = 0; j < n; j++) {   // oldest first
+        const int i = (h->ring_head + mppi_handle::EV_RING - h->ring_count + j) % mppi_handle::EV_RING;
+        HIP_TRY(hipEventSynchronize(h->ev_ring[2 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&ms[j], h->ev_ring[2 * i], h->ev_ring[2 * i + 1]));
+    }
+    *count = n;
+    h->ring_count = 0;
     return MPPI_OK;
 }
 

@@ -404,6 +404,14 @@ class Trajectory:
         2 every phase (mppi_set_timing)."""
         self._check(self._L.mppi_set_timing(self._h, int(level)))
 
+    def rollout_kernel_times(self):
+        """The rollout launch's HIP-event times (ms) of the updates run at timing level 1 since the
+        last call, oldest first (mppi_rollout_kernel_times)."""
+        out = (C.c_float * 64)()
+        n = C.c_int(0)
+        self._check(self._L.mppi_rollout_kernel_times(self._h, out, 64, C.byref(n)))
+        return list(out[:n.value])
+
     def kernel_times(self, wait=True, detail=False):
         """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
         wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's).

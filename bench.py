@@ -128,8 +128,9 @@ def main():
         dist.barrier()
     # HIP events around the rollout kernel on every EV_EVERY-th update of the timed region (each
     # event record delays the next kernel on the stream by ~4.5 us; the kernel's duration does not
-    # vary, so a sample of the launches gives its average)
-    dyn, nd = 0.0, 0
+    # vary, so a sample of the launches gives its average).  The engine keeps the event pairs and
+    # they are read after the timed region (mppi_rollout_kernel_times).
+    traj.rollout_kernel_times()    # clear the record
     t0 = time.perf_counter()
     for i in range(args.steps):
         sampled = i % EV_EVERY == 0
@@ -137,12 +138,12 @@ def main():
             traj.set_timing(1)
         traj.update(x, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
         if sampled:
-            dyn += traj.kernel_times(detail=True)[5]   # the rollout kernel's HIP-event time, this update
-            nd += 1
             traj.set_timing(0)
         j += 1
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
+    dyn_times = traj.rollout_kernel_times()   # the rollout kernel's HIP-event times, sampled updates
+    dyn, nd = sum(dyn_times), len(dyn_times)
     # the per-phase breakdown from a few further updates with every event recorded (untimed)
     traj.set_timing(2)
     kt = np.zeros(6)

@@ -373,6 +373,11 @@ mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5);
  * (dynamics) kernel alone: [1] spans it and the FrankaRidgeback cost kernel that sums the step
  * costs from its records. */
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n);
+/* The rollout launch's HIP-event times (ms) of every update run at timing level 1 since the last
+ * call, oldest first (at most the last 64): *count <- min(recorded, capacity), and the record is
+ * cleared.  Reading them after a timed loop keeps the event queries out of it (querying an event
+ * pair right behind the publish held the host ~70 us). */
+mppi_status mppi_rollout_kernel_times(mppi_handle *h, float *ms, int capacity, int *count);
 
 #ifdef __cplusplus
 }

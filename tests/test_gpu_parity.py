@@ -464,3 +464,32 @@ def test_two_philox_shards_draw_ahead_equal_unsharded():
             np.testing.assert_allclose(sh.costs(), single.costs(), rtol=1e-13, atol=0)
             np.testing.assert_allclose(sh.get_optimal_rollout(), single.get_optimal_rollout(), rtol=0, atol=1e-12)
             assert sh.argmin() == single.argmin()
+
+
+@pytest.mark.parametrize("S", [4096, 1000])
+def test_rollout_kernel_event_ring(S):
+    """Timing level 1 records the rollout launch's events into a ring read after the loop
+    (mppi_rollout_kernel_times): one positive time per timed update, oldest first, the record
+    cleared by the read; kernel_times(detail)[5] still gives the newest; timing leaves U* alone."""
+    def run(timed):
+        conf = am.frankaridgeback_configuration(rollouts=S, horison=0.64, keep_best_rollouts=20)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=11)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        assert t.rollout_kernel_times() == []
+        for j in range(7):
+            if timed and j % 2 == 1:
+                t.set_timing(1)
+            t.update(x, 0.05 * j)
+            t.set_timing(0)
+        t.synchronize()
+        return t, t.get_optimal_rollout()
+    t, u_timed = run(True)
+    newest = t.kernel_times(detail=True)[5]
+    times = t.rollout_kernel_times()
+    assert len(times) == 3 and all(0.0 < v < 100.0 for v in times)
+    assert newest == pytest.approx(times[-1])
+    assert t.rollout_kernel_times() == []
+    _, u_plain = run(False)
+    np.testing.assert_array_equal(u_timed, u_plain)
