@@ -66,6 +66,12 @@ struct mppi_handle {
     hipEvent_t ev_ring[2 * EV_RING] = {};
     int ring_head = 0, ring_count = 0;   // next pair to record; recorded pairs not yet read
     bool ring_unread = false;            // kernel_ms[5] not yet taken from the newest pair
+    // MPPI_HOST_TRACE=1: host-side turnaround stamps, averaged and printed by mppi_destroy:
+    // [0] flag seen -> phase 3 returns, [1] return -> next phase 1, [2] phase 1 -> rollout launched
+    bool host_trace = false;
+    std::chrono::steady_clock::time_point ht_flag, ht_ret;
+    double ht_sum[3] = {0, 0, 0};
+    int64_t ht_n[3] = {0, 0, 0};
     int dyn_kind = 0, cost_kind = 0;
     int64_t S = 0, K = 0, R = 0, H = 0, C = 0, X = 0;
     double dt = 0, gradient_step = 0, cost_scale = 0, gamma = 1;
@@ -481,6 +487,10 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     }
 
     h = new mppi_handle();
+    {
+        const char *e = getenv("MPPI_HOST_TRACE");
+        h->host_trace = e && e[0] == '1';
+    }
     h->device = device;
     h->dyn_kind = dyn->kind;
     h->cost_kind = cost->kind;
@@ -724,6 +734,10 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 void mppi_destroy(mppi_handle *h)
 {
     if (!h) return;
+    if (h->host_trace && h->ht_n[2] > 0)
+        std::fprintf(stderr, "mppi host turnaround (us): flag->return %.2f  return->phase1 %.2f  phase1->launched %.2f  (n=%lld)\n",
+                     h->ht_sum[0] / (double)std::max<int64_t>(1, h->ht_n[0]), h->ht_sum[1] / (double)std::max<int64_t>(1, h->ht_n[1]),
+                     h->ht_sum[2] / (double)h->ht_n[2], (long long)h->ht_n[2]);
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
@@ -1116,6 +1130,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     if (!h || !state) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
+    if (h->host_trace && h->ht_n[0] > h->ht_n[1]) {
+        h->ht_sum[1] += std::chrono::duration<double, std::micro>(h->t_start - h->ht_ret).count();
+        h->ht_n[1]++;
+    }
     h->rollout_time = time;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[0], h->stream));
     if (h->fc.type != FC_NONE) {   // this update's forecast samples, t0 + k dt (mppi.cpp:326)
@@ -1268,6 +1286,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
     }
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    if (h->host_trace) {
+        h->ht_sum[2] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h->t_start).count();
+        h->ht_n[2]++;
+    }
     h->updated_once = true;
     h->phase_open = true;
     return MPPI_OK;
@@ -1389,6 +1411,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        if (h->host_trace) h->ht_flag = std::chrono::steady_clock::now();
     }
     if (h->timing >= 2) HIP_TRY(hipEventSynchronize(h->ev[5]));
     h->phase_open = false;
@@ -1417,6 +1440,11 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     h->update_duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - h->t_start).count();
     h->update_last = h->rollout_time;
     ++h->update_count;
+    if (h->host_trace) {
+        h->ht_ret = std::chrono::steady_clock::now();
+        h->ht_sum[0] += std::chrono::duration<double, std::micro>(h->ht_ret - h->ht_flag).count();
+        h->ht_n[0]++;
+    }
     return MPPI_OK;
 }
 

@@ -1764,8 +1764,11 @@ hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, doub
 // separate fr_step_cost_kernel (A/B)
 static bool costs_in_launch_enabled()
 {
-    const char *e = getenv("MPPI_COSTS_IN_LAUNCH");
-    return !(e && e[0] == '0');
+    static const bool on = [] {   // read once: getenv scans the environment on every call
+        const char *e = getenv("MPPI_COSTS_IN_LAUNCH");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample

@@ -120,9 +120,16 @@ def main():
     traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
     traj.set_forecast(am.constant_forecast(traj.H))
     x = am.huddled_state()
+    traj.set_timing(1)   # creates the engine's timing-event ring outside the timed region
+    traj.set_timing(0)
     j = 0
-    for _ in range(args.warmup):
+    for i in range(args.warmup):   # the timed loop's pattern (first event records happen here)
+        sampled = i % EV_EVERY == 0
+        if sampled:
+            traj.set_timing(1)
         traj.update(x, 0.05 * j)
+        if sampled:
+            traj.set_timing(0)
         j += 1
     if dist:
         dist.barrier()
