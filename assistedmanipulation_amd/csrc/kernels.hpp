@@ -6,6 +6,10 @@
 
 #include "engine_types.hpp"
 
+#ifndef GRAD_SPLIT_DEF
+#define GRAD_SPLIT_DEF 8
+#endif
+
 namespace mppi_eng {
 
 // Device-side outcome of optimise() (mppi.cpp:344-375) and of the smoothing filter.
@@ -15,7 +19,7 @@ struct Status {
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
     int pad;
     double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
-    double tsplit[8];                 // its GRAD_SPLIT partial sums (weights_gradient_kernel)
+    double tsplit[GRAD_SPLIT_DEF];    // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };
 
 // min / max / count of the update's non-NaN costs, accumulated with order-independent atomics on
@@ -230,7 +234,7 @@ hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S,
                              hipStream_t s);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
-constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
+constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
 static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser partials");
 // optimise() and the partial gradient in one launch (kernels.hip weights_gradient_kernel)
 struct WGradArgs {
