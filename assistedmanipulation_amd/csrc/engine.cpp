@@ -66,6 +66,11 @@ struct mppi_handle {
     hipEvent_t ev_ring[2 * EV_RING] = {};
     int ring_head = 0, ring_count = 0;   // next pair to record; recorded pairs not yet read
     bool ring_unread = false;            // kernel_ms[5] not yet taken from the newest pair
+    // the update's rollout launch drew the next update's eps for its main waves' rows (tail_draws):
+    // phase 3 draws only the rows it left (launch_draw_ahead's subset)
+    bool tail_drawn = false;
+    int tail_nxb = 0;
+    int64_t tail_xbase = 0;
     // MPPI_HOST_TRACE=1: host-side turnaround stamps, averaged and printed by mppi_destroy:
     // [0] flag seen -> phase 3 returns, [1] return -> next phase 1, [2] phase 1 -> rollout launched
     bool host_trace = false;
@@ -384,6 +389,13 @@ static bool draw_ahead_possible(const mppi_handle *h)
     if (e && e[0] == '0') return false;
     return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C && h->tdiag &&
            h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count);
+}
+
+// MPPI_TAIL_DRAWS=0: the next update's draws all in rank_draw_kernel behind the publish (A/B)
+static bool tail_draws_disabled()
+{
+    const char *e = std::getenv("MPPI_TAIL_DRAWS");   // per update: tests switch it in-process
+    return e && e[0] == '0';
 }
 
 bool fuse_sampling(const mppi_handle *h)
@@ -1130,6 +1142,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     if (!h || !state) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
+    h->tail_drawn = false;
     if (h->host_trace && h->ht_n[0] > h->ht_n[1]) {
         h->ht_sum[1] += std::chrono::duration<double, std::micro>(h->t_start - h->ht_ret).count();
         h->ht_n[1]++;
@@ -1251,17 +1264,28 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.fcost = h->d_opt;
             a.frec = h->d_rec_opt;
         }
-        bool folded = false, costs_done = false;
+        bool folded = false, costs_done = false, tail = false;
         a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
+        // the next update's draws in the launch's tail, into the buffer it will write (phase 3 makes
+        // the rest with the rank); needs the sampling arguments (fused launch) and no tail switch-off
+        a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
-                                          &folded, &costs_done));
+                                          &folded, &costs_done, &tail));
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
             if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
             if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
+        }
+        h->tail_drawn = tail;
+        if (tail) {   // the rows the tail left: the fifth wave's and its SIMD-mate's (fr_coop.hip)
+            constexpr int64_t WG_ROWS = 16;
+            const int64_t groups = h->count / WG_ROWS;
+            const int64_t xrows = h->count - groups * WG_ROWS + (folded ? 1 : 0);
+            h->tail_xbase = groups * WG_ROWS;
+            h->tail_nxb = (int)((xrows + 3) / 4);
         }
         if (folded) {   // the optimal cost is ready with this update's rollouts; phase 3's host block
                         // carries it back (finish_kernel copies d_opt), on the same stream
@@ -1392,7 +1416,8 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         sa.H = (int)h->H;
         sa.C = (int)h->C;
         for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
-        HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
+        if (h->tail_drawn) HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, h->tail_nxb, h->tail_xbase));
+        else HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
         h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
         h->ahead_valid = true;
     }

@@ -1463,6 +1463,35 @@ __device__ __forceinline__ void wait_records(int *flag)
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(8);
 }
 
+// The next update's draws for the wave's own four rows (a.ahead_noise), made in the launch's idle
+// tail after the rows' objective: draw_ahead_block's values (Philox by (rollout, step) with the
+// next update's index, Box-Muller, the diagonal transform), rows of rollouts >= 2 only.  Lane
+// items run step-major over (row, piece), so twelve consecutive lanes store one step's 384
+// contiguous bytes.  The wave read its rows' previous eps (kept columns) at entry, so the buffer
+// is free; no other wave touches these rows.
+__device__ __forceinline__ void tail_draws(const FrRolloutArgs &a, int64_t lr0, int lane)
+{
+    const SampleArgs &sa = a.samp;
+    const int H = sa.H;
+    const uint32_t upd = (uint32_t)(sa.sp.update_index + 1);
+    const uint32_t s0 = (uint32_t)sa.sp.seed, s1 = (uint32_t)((uint64_t)sa.sp.seed >> 32);
+#pragma unroll 1
+    for (int it = lane; it < 12 * H; it += 64) {
+        const int blk = it % 3, i = (it / 3) % 4, k = it / 12;
+        const int64_t lr = lr0 + i, g = sa.begin + lr;
+        if (lr >= sa.count || g < 2) continue;
+        const int64_t draw = mppi_sample::philox_index(g, k, H);
+        const mppi_dev::u32x4 ctr{(uint32_t)draw, (uint32_t)((uint64_t)draw >> 32), upd, (uint32_t)blk};
+        const mppi_dev::u32x4 r = mppi_dev::philox4x32_10(ctr, s0, s1);
+        float z[4];
+        mppi_dev::box_muller(r.x, r.y, z[0], z[1]);
+        mppi_dev::box_muller(r.z, r.w, z[2], z[3]);
+        double2 *o = reinterpret_cast<double2 *>(a.ahead_noise + ((int64_t)k * sa.Rpad + lr) * FR_C + 4 * blk);
+        o[0] = double2{sa.tdv[4 * blk] * (double)z[0], sa.tdv[4 * blk + 1] * (double)z[1]};
+        o[1] = double2{sa.tdv[4 * blk + 2] * (double)z[2], sa.tdv[4 * blk + 3] * (double)z[3]};
+    }
+}
+
 // Main wave wv (0..3) of the workgroup after its horizon loop.  xr: the workgroup's fifth wave has
 // rows (its SIMD-mate, wave 0, then only signals).
 template <int CK, bool EN>
@@ -1478,6 +1507,7 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
 #pragma unroll 1
     for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
+    if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
     if (!xr) return;
     wait_records(Lflag);
 #pragma unroll 1
@@ -1782,9 +1812,10 @@ bool fr_coop_update_fusable(int64_t count)
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
-                                 bool *costs_done)
+                                 bool *costs_done, bool *tail_drawn)
 {
     *costs_done = false;
+    *tail_drawn = false;
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     *folded = false;
@@ -1796,6 +1827,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
         if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
+        a.ahead_noise = nullptr;
         if (e0) (void)hipEventRecord(e0, s);
         const hipError_t e = launch_fr_coop(a, s);
         if (e1) (void)hipEventRecord(e1, s);
@@ -1807,6 +1839,9 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     *folded = frow;
     a.costs_in_launch = costs_in_launch_enabled() ? 1 : 0;
     *costs_done = a.costs_in_launch != 0;
+    // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
+    if (xrows == 0 || !a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
+    *tail_drawn = a.ahead_noise != nullptr;
     if (e0) (void)hipEventRecord(e0, s);
 #ifdef FORCE_X
     if (false) {}

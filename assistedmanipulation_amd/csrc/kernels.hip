@@ -608,14 +608,18 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
 // (rollout, step) (sample_device.hpp philox_index).  The update's rollout launch copies the kept
 // rollouts' shifted columns over these once the shift is known (fr_coop.hip kept_columns).
 template <int C>
-__device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned bx, int k)
+__device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned bx, int k, int sub_nxb, int64_t sub_xbase)
 {
     static_assert(C % 4 == 0, "full pieces");
     constexpr int NB = C / 4;
     const int64_t tid = (int64_t)bx * 256 + threadIdx.x;
-    const int64_t lr = tid / NB;
-    if (lr >= a.count) return;
+    int64_t lr = tid / NB;
     const int blk = (int)(tid - lr * NB);
+    if (sub_nxb > 0) {   // only the rows the rollout launch's tail left (fr_coop.hip tail_draws)
+        const int64_t nm = 4 * (int64_t)sub_nxb;
+        lr = lr < nm ? 16 * (lr / 4) + (lr % 4) : sub_xbase + (lr - nm);
+    }
+    if (lr >= a.count) return;
     const int64_t g = a.begin + lr;
     mppi_sample::EpsPlan e{a.Uprev, 0.0, 0, true};   // rollout 0: zeros
     if (g == 1) {
@@ -639,7 +643,7 @@ __device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned b
 // other's output): blocks [0, nr^2) rank tiles, the rest draw (grid nx x H flattened)
 template <int C>
 __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank,
-                                                        unsigned nr, SampleArgs a, unsigned nx)
+                                                        unsigned nr, SampleArgs a, unsigned nx, int sub_nxb, int64_t sub_xbase)
 {
     __shared__ uint64_t kj[RANK_T];
     static_assert(RANK_T == 256, "one block size");
@@ -647,23 +651,26 @@ __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict
     if (b < nr * nr) rank_tile(cost, S, rank, b % nr, b / nr, kj);
     else {
         const unsigned d = b - nr * nr;
-        draw_ahead_block<C>(a, d % nx, (int)(d / nx));
+        draw_ahead_block<C>(a, d % nx, (int)(d / nx), sub_nxb, sub_xbase);
     }
 }
 
 hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                                       hipStream_t s)
+                                       hipStream_t s, int sub_nxb, int64_t sub_xbase)
 {
     if (a.C != FR_C || a.count <= 0) return hipErrorInvalidValue;
+    if (sub_nxb > 0 && (16 * (int64_t)sub_nxb > sub_xbase || sub_xbase > a.count)) return hipErrorInvalidValue;
     constexpr int NB = FR_C / 4;
-    const unsigned nx = (unsigned)((a.count * NB + 255) / 256);
+    const int64_t rows = sub_nxb > 0 ? 4 * (int64_t)sub_nxb + (a.count - sub_xbase) : a.count;
+    const unsigned nx = (unsigned)((rows * NB + 255) / 256);
     unsigned nr = (unsigned)((S + RANK_T - 1) / RANK_T);
     if (S > RANK_TILED_MAX) {   // O(S log S) rank in its own launches, then the draws alone
         const hipError_t e = launch_rank(cost, S, rank, sorted, s);
         if (e != hipSuccess) return e;
         nr = 0;
     }
-    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx);
+    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx,
+                       sub_nxb, sub_xbase);
     return hipGetLastError();
 }
 

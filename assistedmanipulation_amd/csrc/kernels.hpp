@@ -98,6 +98,9 @@ struct FrRolloutArgs {
     // in FrCostArgs
     int costs_in_launch;
     CostStats *stats;
+    // the next update's draws for the main waves' own rows, made in the launch's idle tail into
+    // this buffer (fr_coop.hip tail_draws; null: none): rank_draw_kernel then draws only the rest
+    double *ahead_noise;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -230,8 +233,10 @@ hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 // The next update's draws before its state, time and stable order exist (FrankaRidgeback, diagonal
 // transform, device Philox): rollout 0 zero, rollout 1 = -U*, the rest Philox by (rollout, step);
 // with the stable rank of this update's costs (one launch when S <= RANK_TILED_MAX; rank[] cleared)
+// sub_nxb > 0: the rollout launch's tail drew the rest, so only the rows it left are drawn - the
+// first wave's rows of its first sub_nxb workgroups (16 b + i, i < 4) and [sub_xbase, count).
 hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                             hipStream_t s);
+                             hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
@@ -258,8 +263,9 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
 // The update's rollouts (fr_coop.hip): e0 / e1 = optional timing events around the launch.
+// *tail_drawn: the launch made the next update's draws for its main waves' rows (a.ahead_noise).
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
-                                 bool *costs_done);
+                                 bool *costs_done, bool *tail_drawn);
 bool fr_coop_update_fusable(int64_t count);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed

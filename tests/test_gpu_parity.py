@@ -388,18 +388,23 @@ def test_fused_sampling_matches_sample_kernel(rollouts, injected, monkeypatch):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
 
 
-@pytest.mark.parametrize("rollouts,objective", [(2046, "am"), (1000, "am"), (2046, "energy"), (1000, "track_point")])
+@pytest.mark.parametrize("rollouts,objective", [(2046, "am"), (1000, "am"), (4096, "am"), (2046, "energy"),
+                                                (1000, "track_point"), (4096, "track_point")])
 def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
     """Draws made behind the previous publish (MPPI_DRAW_AHEAD, the default for device Philox) with
     the kept rollouts' columns copied in by the rollout launch equal the sampling launch at update
     time, bit for bit, over updates whose shift varies (5, 2, 5, 0 steps) with kept rollouts; for
-    the default objective, the energy-tank variant (articulated-body kernel) and TrackPoint."""
+    the default objective, the energy-tank variant (articulated-body kernel) and TrackPoint.  Both
+    ways of drawing ahead: all rows behind the publish (MPPI_TAIL_DRAWS=0), and the main waves'
+    rows in the rollout launch's tail with the rest behind the publish (the default; 1000 and 4096
+    rollouts leave rows over, so their launches have a fifth wave and draw in the tail)."""
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.32, keep_best_rollouts=20, threads=8)
     times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
     make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
     out = {}
-    for ahead in ("0", "1"):
-        monkeypatch.setenv("MPPI_DRAW_AHEAD", ahead)
+    for ahead in ("0", "1", "tail"):
+        monkeypatch.setenv("MPPI_DRAW_AHEAD", "0" if ahead == "0" else "1")
+        monkeypatch.setenv("MPPI_TAIL_DRAWS", "1" if ahead == "tail" else "0")
         t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), make_cost())
         t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
         t.set_forecast(am.constant_forecast(t.H))
@@ -409,9 +414,10 @@ def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
             t.update(x, tm)
             rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
         out[ahead] = rec
-    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
-        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
-            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+    for mode in ("1", "tail"):
+        for j, (a, b) in enumerate(zip(out["0"], out[mode])):
+            for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+                np.testing.assert_array_equal(u, v, err_msg="%s: update %d %s" % (mode, j, name))
 
 
 def test_two_philox_shards_draw_ahead_equal_unsharded():
