@@ -547,7 +547,7 @@ __global__ __launch_bounds__(RANK_T) void rank_merge_kernel(const double *__rest
 // tile the index tie-break is block-uniform, so one compare per pair.  rank[] is zeroed by the
 // finish kernel that precedes this launch on the engine stream.
 __device__ __forceinline__ void rank_tile(const double *__restrict__ cost, int64_t S, int *__restrict__ rank, unsigned bx,
-                                          unsigned by, uint64_t *kj);
+                                          unsigned by, uint64_t *kj, unsigned js = 0, unsigned ns = 1);
 
 __global__ __launch_bounds__(RANK_T) void rank_tiled_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank)
 {
@@ -555,17 +555,20 @@ __global__ __launch_bounds__(RANK_T) void rank_tiled_kernel(const double *__rest
     rank_tile(cost, S, rank, blockIdx.x, blockIdx.y, kj);
 }
 
+// (js, ns): the block compares against columns [js W, (js + 1) W) of tile by only, W = RANK_T / ns
+// (ns blocks per tile: a chain of W compares per thread instead of RANK_T)
 __device__ __forceinline__ void rank_tile(const double *__restrict__ cost, int64_t S, int *__restrict__ rank, unsigned bx,
-                                          unsigned by, uint64_t *kj)
+                                          unsigned by, uint64_t *kj, unsigned js, unsigned ns)
 {
+    const int W = RANK_T / (int)ns;
     const int64_t i = (int64_t)bx * RANK_T + threadIdx.x;
-    const int64_t j0 = (int64_t)by * RANK_T;
+    const int64_t j0 = (int64_t)by * RANK_T + (int64_t)js * W;
     const int64_t jl = j0 + threadIdx.x;
-    kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
+    if ((int)threadIdx.x < W) kj[threadIdx.x] = (jl < S) ? cost_key(cost[2 + jl]) : ~0ull;
     __syncthreads();
     if (i >= S) return;
     const uint64_t ki = cost_key(cost[2 + i]);
-    const int jn = (int)((S - j0) < RANK_T ? (S - j0) : RANK_T);
+    const int jn = (int)((S - j0) < W ? (S - j0) : W);
     int cnt = 0;
     if (by < bx) {          // every j < i: equal keys count
 #pragma unroll 8
@@ -574,7 +577,7 @@ __device__ __forceinline__ void rank_tile(const double *__restrict__ cost, int64
 #pragma unroll 8
         for (int t = 0; t < jn; t++) cnt += (kj[t] < ki) ? 1 : 0;
     } else {
-        const int il = threadIdx.x;
+        const int il = (int)threadIdx.x - (int)js * W;   // this row's column in the block's range
         for (int t = 0; t < jn; t++) cnt += (kj[t] < ki || (kj[t] == ki && t < il)) ? 1 : 0;
     }
     if (cnt) atomicAdd(&rank[2 + i], cnt);
@@ -639,6 +642,9 @@ __device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned b
     mppi_sample::store_eps<C, true>(a, k, lr, blk, eps);
 }
 
+#ifndef RANK_JS
+#define RANK_JS 4
+#endif
 // The draws ahead and the stable rank of this update's costs in one launch (neither reads the
 // other's output): blocks [0, nr^2) rank tiles, the rest draw (grid nx x H flattened)
 template <int C>
@@ -648,9 +654,10 @@ __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict
     __shared__ uint64_t kj[RANK_T];
     static_assert(RANK_T == 256, "one block size");
     const unsigned b = blockIdx.x;
-    if (b < nr * nr) rank_tile(cost, S, rank, b % nr, b / nr, kj);
+    const unsigned nrb = nr * nr * RANK_JS;
+    if (b < nrb) rank_tile(cost, S, rank, b % nr, (b / nr) % nr, kj, b / (nr * nr), RANK_JS);
     else {
-        const unsigned d = b - nr * nr;
+        const unsigned d = b - nrb;
         draw_ahead_block<C>(a, d % nx, (int)(d / nx), sub_nxb, sub_xbase);
     }
 }
@@ -669,7 +676,7 @@ hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, 
         if (e != hipSuccess) return e;
         nr = 0;
     }
-    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx,
+    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr * RANK_JS + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx,
                        sub_nxb, sub_xbase);
     return hipGetLastError();
 }
