@@ -50,8 +50,10 @@ PMC_JSON = os.path.join(HERE, "profiles", "r02_pmc_rollout.json")
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    # 200 timed updates (~60 ms): the last update's filter(), finished inside the timed region by
+    # the closing synchronize (~0.18 ms alone), is spread over the steady-state updates
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--samples-per-gpu", type=int, default=SAMPLES_PER_GPU)
     p.add_argument("--horizon-steps", type=int, default=int(round(HORISON / 0.01)),
                    help="H (dt = 0.01); 64 = configs[2]/[3], 128 = configs[4]")
