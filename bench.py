@@ -180,6 +180,8 @@ def main():
     groups = count_all // 16
     xrows = count_all - 16 * groups + (1 if count_all - 16 * groups > 0 else 0)
     in_launch = records and os.environ.get("MPPI_COSTS_IN_LAUNCH") != "0" and 0 < groups <= 256 and xrows <= 4 * groups
+    # the launch's tail also writes the next update's eps of its main waves' rows (tail_draws)
+    tail_draws = in_launch and xrows > 0 and os.environ.get("MPPI_TAIL_DRAWS") != "0" and os.environ.get("MPPI_DRAW_AHEAD") != "0"
     cost_ms = float(kt[1] - kt[5]) if records and not in_launch else 0.0   # fr_step_cost_kernel (breakdown pass)
     traffic = None
     if os.path.exists(PMC_JSON) and world == 1 and default_workload:
@@ -225,7 +227,8 @@ def main():
                      "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
                      "flops_per_rollout_step": flops_unit},
-        "hbm": {"rollout_algorithmic_GBs": ((BYTES_PER_ROLLOUT_STEP + (BYTES_REC_PER_ROLLOUT_STEP if in_launch else 0.0))
+        "hbm": {"rollout_algorithmic_GBs": ((BYTES_PER_ROLLOUT_STEP + (BYTES_REC_PER_ROLLOUT_STEP if in_launch else 0.0)
+                                             + (BYTES_EPS_PER_ROLLOUT_STEP if tail_draws else 0.0))
                                             if records else BYTES_EPS_PER_ROLLOUT_STEP) * units / (dyn_ms * 1e-3) / 1e9,
                 "objective_in_rollout_launch": in_launch,
                 "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if records and cost_ms > 0 else None,

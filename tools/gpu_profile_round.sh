@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 T=$1
 O=gpurun_out/$T
 mkdir -p $O
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err || exit 1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 echo "bench ok"; cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_traced.json 2> $O/trace.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/bench_traced.json 2> $O/trace.err || exit 1
 echo "trace ok"
 B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline"
 D=$O/pmc
