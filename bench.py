@@ -43,7 +43,7 @@ BYTES_REC_PER_ROLLOUT_STEP = 336.0
 BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
 # HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
 # tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
-EV_EVERY = 4   # timed updates per rollout-kernel event sample
+EV_EVERY = 8   # timed updates per rollout-kernel event sample
 PMC_JSON = os.path.join(HERE, "profiles", "r02_pmc_rollout.json")
 
 
@@ -172,7 +172,7 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = S_total * traj.H / (elapsed / args.steps)
     lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
-    dyn_ms = dyn / nd                                     # the rollout (dynamics) kernel alone, timed loop
+    dyn_ms = dyn / max(nd, 1)                             # the rollout (dynamics) kernel alone, timed loop
     records = not lane   # the coop kernel writes step records; the objective reads them back
     # one round of four-wave workgroups (fr_coop.hip fr_coop_update_fusable): the launch evaluates
     # the objective itself in the SIMDs' idle tail (MPPI_COSTS_IN_LAUNCH=0: fr_step_cost_kernel)
