@@ -19,9 +19,10 @@ from .trajectory import (AssistedManipulation, Cost, Dynamics, EngineError, Trac
                          comm_unique_id, shard_range)
 
 from .csvlog import MPPILogger  # noqa: E402
+from .dynamics import DynamicsForecast, EndEffectorState, PinocchioDynamicsObject, evaluate_cost  # noqa: E402
 
 __all__ = [
-    "MPPILogger",
+    "MPPILogger", "DynamicsForecast", "EndEffectorState", "PinocchioDynamicsObject", "evaluate_cost",
     "abi", "Configuration", "Smoothing", "constant_forecast", "frankaridgeback_configuration",
     "huddled_state", "point_mass_configuration", "locf_forecast_configuration", "average_forecast_configuration",
     "kalman_forecast_configuration", "AssistedManipulation", "TrackPoint", "Cost", "Dynamics",

@@ -57,15 +57,27 @@ PROTOTYPES = {
     "mppi_optimal_control": (C.c_int, [_h, _dp]),
     "mppi_optimal_cost": (C.c_int, [_h, _dp]),
     "mppi_argmin": (C.c_int, [_h, _i64p]),
+    "mppi_optimal_terms": (C.c_int, [_h, _dp]),
     "mppi_update_duration": (C.c_int, [_h, _dp]),
     "mppi_noise": (C.c_int, [_h, _dp]),
     "mppi_dims": (C.c_int, [_h, _i64p, _i64p, _i64p, _i64p]),
+    "mppi_update_info": (C.c_int, [_h, _i64p, C.c_int]),
     "mppi_smoothing_windows": (C.c_int, [_h, _dp, _dp, _i64p]),
     "mppi_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float)]),
     "mppi_kernel_times_nowait": (C.c_int, [_h, C.POINTER(C.c_float)]),
     "mppi_kernel_times_detail": (C.c_int, [_h, C.POINTER(C.c_float), C.c_int]),
     "mppi_set_timing": (C.c_int, [_h, C.c_int]),
     "mppi_rollout_kernel_times": (C.c_int, [_h, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
+    "mppi_forecast_table": (C.c_int, [_h, C.c_double, C.c_double, C.c_int64, _dp]),
+    "mppi_dynamics_create": (C.c_int, [C.POINTER(abi.mppi_dynamics_desc), _dp, C.c_int, C.POINTER(_h)]),
+    "mppi_dynamics_destroy": (None, [_h]),
+    "mppi_dynamics_set_state": (C.c_int, [_h, _dp, C.c_double]),
+    "mppi_dynamics_step": (C.c_int, [_h, _dp, C.c_double, _dp]),
+    "mppi_dynamics_get_state": (C.c_int, [_h, _dp]),
+    "mppi_dynamics_end_effector": (C.c_int, [_h, _dp]),
+    "mppi_dynamics_query": (C.c_int, [_h, _dp]),
+    "mppi_dynamics_forecast": (C.c_int, [_h, _dp, C.c_double, C.c_double, C.c_int64, _dp, _dp]),
+    "mppi_cost_evaluate": (C.c_int, [C.POINTER(abi.mppi_cost_desc), _h, _dp, _dp, _dp, _dp]),
 }
 
 _lib = None

@@ -38,6 +38,18 @@ MPPI_NOISE_DEVICE_PHILOX = 0
 MPPI_NOISE_HOST_INJECTED = 1
 MPPI_INDEX_WIDE = 0
 MPPI_INDEX_COMPAT_UINT8 = 1
+MPPI_UPDATE_INFO_N = 6   # mppi_update_info slots (MPPI_INFO_*)
+# EndEffectorState layout (MPPI_EE_*) and DynamicsForecast rows (MPPI_DF_*)
+MPPI_EE_POSITION, MPPI_EE_QUATERNION, MPPI_EE_ROTATION = 0, 3, 7
+MPPI_EE_LINEAR_VELOCITY, MPPI_EE_ANGULAR_VELOCITY = 16, 19
+MPPI_EE_LINEAR_ACCELERATION, MPPI_EE_ANGULAR_ACCELERATION = 22, 25
+MPPI_EE_JACOBIAN, MPPI_EE_N = 28, 100
+MPPI_DF_JOINT_POSITION, MPPI_DF_END_EFFECTOR = 0, 12
+MPPI_DF_JOINT_POWER, MPPI_DF_EXTERNAL_POWER, MPPI_DF_ENERGY, MPPI_DF_WRENCH = 112, 113, 114, 115
+MPPI_DF_N = 121
+MPPI_DYNAMICS_QUERY_N = 54
+TERM_NAMES = ("joint_limit", "self_collision", "workspace", "energy_tank", "joint_velocity", "trajectory",
+              "manipulability")
 
 _d = C.c_double
 _dp = C.POINTER(C.c_double)

@@ -69,6 +69,8 @@ struct mppi_handle {
     // the update's rollout launch drew the next update's eps for its main waves' rows (tail_draws):
     // phase 3 draws only the rows it left (launch_draw_ahead's subset)
     bool tail_drawn = false;
+    // what the last update's rollout launch did (mppi_update_info)
+    int64_t info[MPPI_UPDATE_INFO_N] = {};
     int tail_nxb = 0;
     int64_t tail_xbase = 0;
     // MPPI_HOST_TRACE=1: host-side turnaround stamps, averaged and printed by mppi_destroy:
@@ -92,6 +94,9 @@ struct mppi_handle {
     // reference scalar state (mppi.hpp:545-657)
     double last_shift_time = 0, rollout_time = 0, last_rollout_time = 0, update_last = 0, update_duration = 0;
     uint64_t update_count = 0;
+    // the publish flag's sequence: one per phase-3 call, success or failure (update_count only
+    // counts successes, so a failed update must not leave the flag at the next update's value)
+    uint64_t publish_seq = 0;
     // draws ahead (launch_draw_ahead behind phase 3): valid for the update whose inputs match
     struct AheadSig {
         uint64_t update_index, seed;
@@ -100,6 +105,7 @@ struct mppi_handle {
     bool ahead_valid = false;
     int64_t shift_by = 0, shifted = 0;
     int compat_uint8 = 0;
+    double publish_timeout_s = 5.0;   // floor of the bounded publish wait (phase 3)
     int noise_source = MPPI_NOISE_DEVICE_PHILOX;
     uint64_t seed = 0x5EEDull;
     std::vector<double> inj_pending;
@@ -122,6 +128,7 @@ struct mppi_handle {
     } fc;
     double *d_gamma = nullptr;      // [H] pow(gamma, k) (host std::pow)
     double *d_fc_out = nullptr;     // [6] forecast_eval result
+    double *d_terms = nullptr;      // [7] mppi_optimal_terms
     StepConst *d_steps_buf[2] = {nullptr, nullptr};   // per-update constants, alternate updates
     mppi_assisted_manipulation_desc am{};
     mppi_quadratic_cost_desc quad{};
@@ -287,33 +294,43 @@ double left_barrier_h(const mppi_barrier &b, double v)
 
 DevBarrier devb(const mppi_barrier &b) { return DevBarrier{b.bound, b.scale, b.maximum_cost}; }
 
+// trajectory_cost()'s constants for the wrench F (force part) (assisted_manipulation.cpp:237-290)
+StepConst step_const(const mppi_assisted_manipulation_desc &a, const double *F, bool have_forecast, double gamma_k)
+{
+    StepConst s{};
+    s.gamma_k = gamma_k;
+    const double mx = a.trajectory_target_maximum;
+    for (int i = 0; i < 3; i++) {
+        double t = a.trajectory_target_scale * F[i];
+        t = (mx < t) ? mx : t;           // cwiseMin(max)
+        t = (t < -mx) ? -mx : t;         // cwiseMax(-max)
+        s.target[i] = t;
+    }
+    s.tt = (s.target[0] * s.target[0] + s.target[1] * s.target[1]) + s.target[2] * s.target[2];
+    const double distance = std::sqrt(s.tt);
+    s.active = (have_forecast && a.has_forecast && distance > a.trajectory_position_threshold) ? 1 : 0;
+    const mppi_quadratic &pc = a.trajectory_position_cost;
+    s.pos_cost = (pc.constant_cost + pc.linear_cost * std::fabs(distance)) + pc.quadratic_cost * distance * distance;
+    double vt = std::exp(a.trajectory_velocity_dropoff * distance) - 1;
+    vt = (vt < a.trajectory_velocity_minimum) ? a.trajectory_velocity_minimum : ((a.trajectory_velocity_maximum < vt) ? a.trajectory_velocity_maximum : vt);
+    s.vtarget = vt;
+    return s;
+}
+
 // trajectory_cost() per-step constants and pow(gamma, k) (mppi.cpp:326).
 void build_steps(const mppi_handle *h, std::vector<StepConst> &steps)
 {
     steps.assign((size_t)h->H, StepConst{});
-    const mppi_assisted_manipulation_desc &a = h->am;
     for (int64_t k = 0; k < h->H; k++) {
-        StepConst &s = steps[(size_t)k];
-        s.gamma_k = std::pow(h->gamma, (double)k);
-        if (h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION) continue;
+        const double gk = std::pow(h->gamma, (double)k);
+        if (h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION) {
+            steps[(size_t)k].gamma_k = gk;
+            continue;
+        }
         double F[3] = {0, 0, 0};
         if (!h->forecast.empty())
             for (int i = 0; i < 3; i++) F[i] = h->forecast[(size_t)(6 * k + i)];
-        const double mx = a.trajectory_target_maximum;
-        for (int i = 0; i < 3; i++) {
-            double t = a.trajectory_target_scale * F[i];
-            t = (mx < t) ? mx : t;           // cwiseMin(max)
-            t = (t < -mx) ? -mx : t;         // cwiseMax(-max)
-            s.target[i] = t;
-        }
-        s.tt = (s.target[0] * s.target[0] + s.target[1] * s.target[1]) + s.target[2] * s.target[2];
-        const double distance = std::sqrt(s.tt);
-        s.active = (a.has_forecast && distance > a.trajectory_position_threshold) ? 1 : 0;
-        const mppi_quadratic &pc = a.trajectory_position_cost;
-        s.pos_cost = (pc.constant_cost + pc.linear_cost * std::fabs(distance)) + pc.quadratic_cost * distance * distance;
-        double vt = std::exp(a.trajectory_velocity_dropoff * distance) - 1;
-        vt = (vt < a.trajectory_velocity_minimum) ? a.trajectory_velocity_minimum : ((a.trajectory_velocity_maximum < vt) ? a.trajectory_velocity_maximum : vt);
-        s.vtarget = vt;
+        steps[(size_t)k] = step_const(h->am, F, true, gk);
     }
 }
 
@@ -325,6 +342,75 @@ mppi_status upload_steps(mppi_handle *h)
         HIP_TRY(hipMemcpyAsync(d, steps.data(), steps.size() * sizeof(StepConst), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return MPPI_OK;
+}
+
+// The objective's device block (DevCost) from its descriptor: AssistedManipulation's
+// configuration, or TrackPoint's, with the self-collision constant of the zero link positions.
+void build_dev_cost(const mppi_cost_desc &cost, DevCost &c)
+{
+    const mppi_assisted_manipulation_desc &a = cost.assisted_manipulation;
+    c.kind = cost.kind;
+    // the 20 link pairs of both objectives' self_collision_cost (Link enum: PIVOT = 3,
+    // PANDA_LINK1..7 = 4..10; radii index = link - 3), link positions the zero stub
+    static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8}, {4, 9}, {4, 10},
+                                     {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
+    if (cost.kind == MPPI_COST_TRACK_POINT) {
+        const mppi_track_point_desc &t = cost.track_point;
+        c.tp_en_joint = t.enable_joint_limits;
+        c.tp_en_self = t.enable_self_collision_avoidance;
+        c.tp_en_reach = t.enable_reach_limits;
+        for (int i = 0; i < 3; i++) c.tp_point[i] = t.point[i];
+        // joint_limit_cost's static limits (track_point.cpp:45-66)
+        static const double lo[FR_NB] = {-2.0, -2.0, -6.28, -2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973, 0.5, 0.5};
+        static const double up[FR_NB] = {2.0, 2.0, 6.28, 2.8973, 1.7628, 2.8973, 0.0698, 2.8973, 3.7525, 2.8973, 0.5, 0.5};
+        for (int i = 0; i < FR_NB; i++) {
+            c.tp_lo[i] = lo[i];
+            c.tp_up[i] = up[i];
+        }
+        double sc = 0.0;   // track_point.cpp:97-160: collision = radii - distance
+        for (auto &p : pairs) {
+            const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
+            const double radii = t.self_collision_radii[p[0] - 3] + t.self_collision_radii[p[1] - 3];
+            sc += left_barrier_h(t.self_collision_limit, radii - distance);
+        }
+        c.tp_self = sc;
+        c.tp_reach = devb(t.maximum_reach_limit);
+    } else {
+        c.en_joint = a.enable_joint_limit;
+        c.en_self = a.enable_self_collision_limit;
+        c.en_work = a.enable_workspace_limit;
+        c.en_energy = a.enable_energy_limit;
+        c.en_below = devb(a.energy_limit_below);
+        c.en_above = devb(a.energy_limit_above);
+        c.en_vel = a.enable_velocity_cost;
+        c.en_traj = a.enable_trajectory_cost;
+        c.en_manip = a.enable_manipulability_cost;
+        for (int i = 0; i < FR_NB; i++) {
+            c.lower[i] = devb(a.lower_joint_limit[i]);
+            c.upper[i] = devb(a.upper_joint_limit[i]);
+            c.vel_q[i] = a.velocity_cost[i].quadratic_cost;
+        }
+        // self_collision_cost with get_link_position == 0 (assisted_manipulation.cpp:90-158)
+        double sc = 0.0;
+        for (auto &p : pairs) {
+            const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
+            const double radii = a.self_collision_radii[p[0] - 3] + a.self_collision_radii[p[1] - 3];
+            sc += left_barrier_h(a.self_collision_limit, distance - radii);
+        }
+        c.self_collision = sc;
+        c.ws_above = devb(a.workspace_limit_above);
+        c.ws_infront = devb(a.workspace_limit_infront);
+        c.ws_reach = devb(a.workspace_limit_reach);
+        c.yaw_c = a.workspace_cost_yaw.constant_cost;
+        c.yaw_l = a.workspace_cost_yaw.linear_cost;
+        c.yaw_q = a.workspace_cost_yaw.quadratic_cost;
+        c.manip_c = a.manipulability_cost.constant_cost;
+        c.manip_l = a.manipulability_cost.linear_cost;
+        c.manip_q = a.manipulability_cost.quadratic_cost;
+        c.traj_vel_c = a.trajectory_velocity_cost.constant_cost;
+        c.traj_vel_l = a.trajectory_velocity_cost.linear_cost;
+        c.traj_vel_q = a.trajectory_velocity_cost.quadratic_cost;
+    }
 }
 
 mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
@@ -436,6 +522,256 @@ int64_t draws_for(const mppi_handle *h, int64_t shift_by)
 }
 
 }  // namespace
+
+// ---- FrankaRidgeback::PinocchioDynamics as a device object (fr_object.hip) --------------------
+
+struct mppi_dynamics {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevModel *d_model = nullptr;
+    DevPinocchio *d_obj = nullptr;
+    double *d_buf = nullptr;   // forecast rows / cost output / wrench rows
+    size_t buf_doubles = 0;
+    DevPinocchio *h_obj = nullptr;   // pinned host copy for the queries
+    std::string err;
+};
+
+namespace {
+
+mppi_status dfail(mppi_dynamics *d, mppi_status st, const std::string &msg)
+{
+    if (d) d->err = msg;
+    g_last_error = msg;
+    return st;
+}
+
+#define DHIP_TRY(expr)                                                                                         \
+    do {                                                                                                       \
+        hipError_t e_ = (expr);                                                                                \
+        if (e_ != hipSuccess) return dfail(d, MPPI_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+DevModel dev_model(const mppi_frankaridgeback_desc &d)
+{
+    DevModel m{};
+    for (int i = 0; i < FR_NB; i++) {
+        const mppi_body &b = d.bodies[i];
+        std::memcpy(m.b[i].R, b.rotation, sizeof(m.b[i].R));
+        std::memcpy(m.b[i].p, b.translation, sizeof(m.b[i].p));
+        m.b[i].mass = b.mass;
+        std::memcpy(m.b[i].c, b.lever, sizeof(m.b[i].c));
+        std::memcpy(m.b[i].Ic, b.inertia, sizeof(m.b[i].Ic));
+    }
+    std::memcpy(m.ee_R, d.end_effector.rotation, sizeof(m.ee_R));
+    std::memcpy(m.ee_p, d.end_effector.translation, sizeof(m.ee_p));
+    std::memcpy(m.am_R, d.arm_mount.rotation, sizeof(m.am_R));
+    std::memcpy(m.am_p, d.arm_mount.translation, sizeof(m.am_p));
+    const double *R10 = m.b[10].R, *R11 = m.b[11].R, *p10 = m.b[10].p, *p11 = m.b[11].p;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) m.f11_R[3 * r + c] = (R10[r] * R11[c] + R10[3 + r] * R11[3 + c]) + R10[6 + r] * R11[6 + c];
+        m.f11_p[r] = (R10[r] * (p11[0] - p10[0]) + R10[3 + r] * (p11[1] - p10[1])) + R10[6 + r] * (p11[2] - p10[2]);
+    }
+    for (int k = 0; k < 3; k++) m.gravity[k] = d.gravity[k];
+    return m;
+}
+
+mppi_status obj_buffer(mppi_dynamics *d, size_t doubles)
+{
+    if (doubles <= d->buf_doubles) return MPPI_OK;
+    if (d->d_buf) (void)hipFree(d->d_buf);
+    d->d_buf = nullptr;
+    d->buf_doubles = 0;
+    DHIP_TRY(hipMalloc(&d->d_buf, doubles * sizeof(double)));
+    d->buf_doubles = doubles;
+    return MPPI_OK;
+}
+
+mppi_status obj_run(mppi_dynamics *d, ObjArgs &a)
+{
+    DHIP_TRY(hipSetDevice(d->device));
+    a.obj = d->d_obj;
+    a.model = d->d_model;
+    DHIP_TRY(launch_fr_object(a, d->stream));
+    return MPPI_OK;
+}
+
+mppi_status obj_fetch(mppi_dynamics *d)
+{
+    DHIP_TRY(hipMemcpyAsync(d->h_obj, d->d_obj, sizeof(DevPinocchio), hipMemcpyDeviceToHost, d->stream));
+    DHIP_TRY(hipStreamSynchronize(d->stream));
+    return MPPI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+mppi_status mppi_dynamics_create(const mppi_dynamics_desc *desc, const double *initial_state, int device, mppi_dynamics **out)
+{
+    mppi_dynamics *d = nullptr;
+    if (!desc || !initial_state || !out) return dfail(nullptr, MPPI_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (desc->kind != MPPI_DYNAMICS_FRANKARIDGEBACK)
+        return dfail(nullptr, MPPI_ERR_UNSUPPORTED, "the dynamics object is FrankaRidgeback::PinocchioDynamics only");
+    std::string why;
+    if (check_topology(desc->frankaridgeback, why) != MPPI_OK) return dfail(nullptr, MPPI_ERR_UNSUPPORTED, why);
+    d = new mppi_dynamics();
+    d->device = device;
+    auto bail = [&](mppi_status st) {
+        std::string m = d->err;
+        mppi_dynamics_destroy(d);
+        return dfail(nullptr, st, m);
+    };
+#define DCREATE_TRY(expr)                                                                                        \
+    do {                                                                                                         \
+        hipError_t e_ = (expr);                                                                                  \
+        if (e_ != hipSuccess) { d->err = std::string(#expr ": ") + hipGetErrorString(e_); return bail(MPPI_ERR_DEVICE); } \
+    } while (0)
+    DCREATE_TRY(hipSetDevice(device));
+    DCREATE_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    DCREATE_TRY(hipMalloc(&d->d_model, sizeof(DevModel)));
+    DCREATE_TRY(hipMalloc(&d->d_obj, sizeof(DevPinocchio)));
+    DCREATE_TRY(hipHostMalloc((void **)&d->h_obj, sizeof(DevPinocchio), hipHostMallocDefault));
+    const DevModel m = dev_model(desc->frankaridgeback);
+    DCREATE_TRY(hipMemcpy(d->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
+    DCREATE_TRY(hipMemset(d->d_obj, 0, sizeof(DevPinocchio)));   // the constructor's setZero()s (:106-109)
+    DCREATE_TRY(hipDeviceSynchronize());
+#undef DCREATE_TRY
+    if (mppi_dynamics_set_state(d, initial_state, 0.0) != MPPI_OK) return bail(MPPI_ERR_DEVICE);
+    *out = d;
+    return MPPI_OK;
+}
+
+void mppi_dynamics_destroy(mppi_dynamics *d)
+{
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    if (d->d_buf) (void)hipFree(d->d_buf);
+    if (d->d_obj) (void)hipFree(d->d_obj);
+    if (d->d_model) (void)hipFree(d->d_model);
+    if (d->h_obj) (void)hipHostFree(d->h_obj);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+mppi_status mppi_dynamics_set_state(mppi_dynamics *d, const double *state, double time)
+{
+    if (!d || !state) return MPPI_ERR_INVALID;
+    ObjArgs a{};
+    a.op = OBJ_SET_STATE;
+    std::memcpy(a.x, state, FR_X * sizeof(double));
+    a.time = time;
+    mppi_status st = obj_run(d, a);
+    if (st != MPPI_OK) return st;
+    DHIP_TRY(hipStreamSynchronize(d->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_dynamics_step(mppi_dynamics *d, const double *control, double dt, double *state_out)
+{
+    if (!d || !control) return MPPI_ERR_INVALID;
+    ObjArgs a{};
+    a.op = OBJ_STEP;
+    std::memcpy(a.u, control, FR_C * sizeof(double));
+    a.dt = dt;
+    mppi_status st = obj_run(d, a);
+    if (st != MPPI_OK) return st;
+    if (!state_out) {
+        DHIP_TRY(hipStreamSynchronize(d->stream));
+        return MPPI_OK;
+    }
+    st = obj_fetch(d);
+    if (st != MPPI_OK) return st;
+    std::memcpy(state_out, d->h_obj->state, FR_X * sizeof(double));
+    return MPPI_OK;
+}
+
+mppi_status mppi_dynamics_get_state(mppi_dynamics *d, double *state)
+{
+    if (!d || !state) return MPPI_ERR_INVALID;
+    mppi_status st = obj_fetch(d);
+    if (st != MPPI_OK) return st;
+    std::memcpy(state, d->h_obj->state, FR_X * sizeof(double));
+    return MPPI_OK;
+}
+
+mppi_status mppi_dynamics_end_effector(mppi_dynamics *d, double *ee)
+{
+    if (!d || !ee) return MPPI_ERR_INVALID;
+    mppi_status st = obj_fetch(d);
+    if (st != MPPI_OK) return st;
+    std::memcpy(ee, d->h_obj->ee, MPPI_EE_N * sizeof(double));
+    return MPPI_OK;
+}
+
+mppi_status mppi_dynamics_query(mppi_dynamics *d, double *out)
+{
+    if (!d || !out) return MPPI_ERR_INVALID;
+    mppi_status st = obj_fetch(d);
+    if (st != MPPI_OK) return st;
+    const DevPinocchio &P = *d->h_obj;
+    std::memcpy(out, P.q, FR_NB * sizeof(double));
+    std::memcpy(out + 12, P.v, FR_NB * sizeof(double));
+    std::memcpy(out + 24, P.a, FR_NB * sizeof(double));
+    std::memcpy(out + 36, P.tau, FR_NB * sizeof(double));
+    out[48] = P.energy;
+    out[49] = P.power;
+    out[50] = P.time;
+    std::memcpy(out + 51, P.am, 3 * sizeof(double));
+    return MPPI_OK;
+}
+
+mppi_status mppi_dynamics_forecast(mppi_dynamics *d, const double *state, double time, double time_step, int64_t steps,
+                                   const double *wrench, double *out)
+{
+    if (!d || !state || !out || steps < 0) return MPPI_ERR_INVALID;
+    if (steps == 0) return MPPI_OK;
+    const size_t rows = (size_t)steps * MPPI_DF_N, wrows = wrench ? (size_t)steps * 6 : 0;
+    mppi_status st = obj_buffer(d, rows + wrows);
+    if (st != MPPI_OK) return st;
+    ObjArgs a{};
+    a.op = OBJ_FORECAST;
+    std::memcpy(a.x, state, FR_X * sizeof(double));
+    a.time = time;
+    a.dt = time_step;
+    a.steps = steps;
+    a.out = d->d_buf;
+    if (wrench) {
+        DHIP_TRY(hipMemcpyAsync(d->d_buf + rows, wrench, wrows * sizeof(double), hipMemcpyHostToDevice, d->stream));
+        a.wrench = d->d_buf + rows;
+    }
+    st = obj_run(d, a);
+    if (st != MPPI_OK) return st;
+    DHIP_TRY(hipMemcpyAsync(out, d->d_buf, rows * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    DHIP_TRY(hipStreamSynchronize(d->stream));
+    return MPPI_OK;
+}
+
+mppi_status mppi_cost_evaluate(const mppi_cost_desc *cost, mppi_dynamics *d, const double *state, const double *control,
+                               const double *wrench6, double *out8)
+{
+    if (!cost || !d || !state || !out8) return MPPI_ERR_INVALID;
+    (void)control;   // neither objective reads the control (assisted_manipulation.cpp:37-72, track_point.cpp:10-34)
+    if (cost->kind != MPPI_COST_ASSISTED_MANIPULATION && cost->kind != MPPI_COST_TRACK_POINT)
+        return dfail(d, MPPI_ERR_UNSUPPORTED, "get_cost on the device: AssistedManipulation or TrackPoint");
+    mppi_status st = obj_buffer(d, 8);
+    if (st != MPPI_OK) return st;
+    ObjArgs a{};
+    a.op = OBJ_COST;
+    std::memcpy(a.x, state, FR_X * sizeof(double));
+    build_dev_cost(*cost, a.cost);
+    const double zero[3] = {0, 0, 0};
+    a.sc = step_const(cost->assisted_manipulation, wrench6 ? wrench6 : zero, wrench6 != nullptr, 1.0);
+    a.out = d->d_buf;
+    st = obj_run(d, a);
+    if (st != MPPI_OK) return st;
+    DHIP_TRY(hipMemcpyAsync(out8, d->d_buf, 8 * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    DHIP_TRY(hipStreamSynchronize(d->stream));
+    return MPPI_OK;
+}
+
+}  // extern "C"
 
 extern "C" {
 
@@ -575,6 +911,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_cstats, 1));
+    // the first update's statistics start empty (later ones are reset by the finish kernel)
+    CREATE_TRY(hipMemset(h->d_cstats->kmin, 0xFF, sizeof(h->d_cstats->kmin)));
     CREATE_TRY(dalloc(h, &h->d_wpart, 4 * 64));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
@@ -589,6 +927,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     h->d_steps = h->d_steps_buf[0];
     CREATE_TRY(dalloc(h, &h->d_gamma, (size_t)h->H));
     CREATE_TRY(dalloc(h, &h->d_fc_out, 6));
+    CREATE_TRY(dalloc(h, &h->d_terms, 7));
     {
         std::vector<double> g((size_t)h->H);
         for (int64_t k = 0; k < h->H; k++) g[(size_t)k] = std::pow(h->gamma, (double)k);
@@ -630,70 +969,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         for (int k = 0; k < 3; k++) m.gravity[k] = d.gravity[k];
         CREATE_TRY(dalloc(h, &h->d_model, 1));
         CREATE_TRY(hipMemcpy(h->d_model, &m, sizeof(m), hipMemcpyHostToDevice));
-        const mppi_assisted_manipulation_desc &a = cost->assisted_manipulation;
         DevCost c{};
-        c.kind = cost->kind;
-        // the 20 link pairs of both objectives' self_collision_cost (Link enum: PIVOT = 3,
-        // PANDA_LINK1..7 = 4..10; radii index = link - 3), link positions the zero stub
-        static const int pairs[20][2] = {{3, 6}, {3, 7}, {3, 8}, {3, 9}, {3, 10}, {4, 6}, {4, 7}, {4, 8}, {4, 9}, {4, 10},
-                                         {5, 7}, {5, 8}, {5, 9}, {5, 10}, {6, 8}, {6, 9}, {6, 10}, {7, 9}, {7, 10}, {8, 10}};
-        if (cost->kind == MPPI_COST_TRACK_POINT) {
-            const mppi_track_point_desc &t = cost->track_point;
-            c.tp_en_joint = t.enable_joint_limits;
-            c.tp_en_self = t.enable_self_collision_avoidance;
-            c.tp_en_reach = t.enable_reach_limits;
-            for (int i = 0; i < 3; i++) c.tp_point[i] = t.point[i];
-            // joint_limit_cost's static limits (track_point.cpp:45-66)
-            static const double lo[FR_NB] = {-2.0, -2.0, -6.28, -2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973, 0.5, 0.5};
-            static const double up[FR_NB] = {2.0, 2.0, 6.28, 2.8973, 1.7628, 2.8973, 0.0698, 2.8973, 3.7525, 2.8973, 0.5, 0.5};
-            for (int i = 0; i < FR_NB; i++) {
-                c.tp_lo[i] = lo[i];
-                c.tp_up[i] = up[i];
-            }
-            double sc = 0.0;   // track_point.cpp:97-160: collision = radii - distance
-            for (auto &p : pairs) {
-                const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
-                const double radii = t.self_collision_radii[p[0] - 3] + t.self_collision_radii[p[1] - 3];
-                sc += left_barrier_h(t.self_collision_limit, radii - distance);
-            }
-            c.tp_self = sc;
-            c.tp_reach = devb(t.maximum_reach_limit);
-        } else {
-        c.en_joint = a.enable_joint_limit;
-        c.en_self = a.enable_self_collision_limit;
-        c.en_work = a.enable_workspace_limit;
-        c.en_energy = a.enable_energy_limit;
-        c.en_below = devb(a.energy_limit_below);
-        c.en_above = devb(a.energy_limit_above);
-        c.en_vel = a.enable_velocity_cost;
-        c.en_traj = a.enable_trajectory_cost;
-        c.en_manip = a.enable_manipulability_cost;
-        for (int i = 0; i < FR_NB; i++) {
-            c.lower[i] = devb(a.lower_joint_limit[i]);
-            c.upper[i] = devb(a.upper_joint_limit[i]);
-            c.vel_q[i] = a.velocity_cost[i].quadratic_cost;
-        }
-        // self_collision_cost with get_link_position == 0 (assisted_manipulation.cpp:90-158)
-        double sc = 0.0;
-        for (auto &p : pairs) {
-            const double distance = std::sqrt((0.0 * 0.0 + 0.0 * 0.0) + 0.0 * 0.0);
-            const double radii = a.self_collision_radii[p[0] - 3] + a.self_collision_radii[p[1] - 3];
-            sc += left_barrier_h(a.self_collision_limit, distance - radii);
-        }
-        c.self_collision = sc;
-        c.ws_above = devb(a.workspace_limit_above);
-        c.ws_infront = devb(a.workspace_limit_infront);
-        c.ws_reach = devb(a.workspace_limit_reach);
-        c.yaw_c = a.workspace_cost_yaw.constant_cost;
-        c.yaw_l = a.workspace_cost_yaw.linear_cost;
-        c.yaw_q = a.workspace_cost_yaw.quadratic_cost;
-        c.manip_c = a.manipulability_cost.constant_cost;
-        c.manip_l = a.manipulability_cost.linear_cost;
-        c.manip_q = a.manipulability_cost.quadratic_cost;
-        c.traj_vel_c = a.trajectory_velocity_cost.constant_cost;
-        c.traj_vel_l = a.trajectory_velocity_cost.linear_cost;
-        c.traj_vel_q = a.trajectory_velocity_cost.quadratic_cost;
-        }
+        build_dev_cost(*cost, c);
         CREATE_TRY(dalloc(h, &h->d_cost, 1));
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
@@ -1029,6 +1306,21 @@ mppi_status mppi_forecast_get(mppi_handle *h, double time, double *out)
     return MPPI_OK;
 }
 
+mppi_status mppi_forecast_table(mppi_handle *h, double t0, double dt, int64_t steps, double *out)
+{
+    if (!h || !out || steps < 0 || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
+    if (steps == 0) return MPPI_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    double *buf = nullptr;
+    // on the engine stream: behind the Kalman observations that write the prediction table
+    HIP_TRY(hipMallocAsync((void **)&buf, (size_t)steps * 6 * sizeof(double), h->stream));
+    HIP_TRY(launch_forecast_table(forecast_args(h), t0, dt, steps, buf, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, buf, (size_t)steps * 6 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipFreeAsync(buf, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MPPI_OK;
+}
+
 mppi_status mppi_step_constants(mppi_handle *h, double *out)
 {
     if (!h || !out) return MPPI_ERR_INVALID;
@@ -1210,7 +1502,6 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         std::memcpy(sa.x0v, state, (size_t)h->X * sizeof(double));   // the state rides in the launch
         sa.x0_out = h->d_x0;
         sa.X = (int)h->X;
-        sa.stats = h->d_cstats;
         if (h->tdiag)
             for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
         if (!fuse) HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
@@ -1280,6 +1571,12 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
         }
         h->tail_drawn = tail;
+        h->info[MPPI_INFO_COOPERATIVE] = use_coop(h) ? 1 : 0;
+        h->info[MPPI_INFO_FOLDED_FILTER] = folded ? 1 : 0;
+        h->info[MPPI_INFO_OBJECTIVE_IN_LAUNCH] = costs_done ? 1 : 0;
+        h->info[MPPI_INFO_TAIL_DRAWS] = tail ? 1 : 0;
+        h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : (fuse ? 1 : 0);
+        h->info[MPPI_INFO_ROWS] = h->count + (folded ? 1 : 0);
         if (tail) {   // the rows the tail left: the fifth wave's and its SIMD-mate's (fr_coop.hip)
             constexpr int64_t WG_ROWS = 16;
             const int64_t groups = h->count / WG_ROWS;
@@ -1346,12 +1643,13 @@ static FinishArgs finish_args(mppi_handle *h)
     f.U = h->d_U;
     f.opt_cost = h->d_opt;
     f.out = h->h_out_dev;   // the host block, written in place (no copy launch behind the finish)
-    f.seq = (double)(h->update_count + 1);   // != 0: the block's flag starts at 0
+    f.seq = (double)(h->publish_seq + 1);   // != 0: the block's flag starts at 0
     f.x0 = h->d_x0;
     f.x0_opt = h->d_x0_opt;
     f.X = (int)h->X;
     f.rank_zero = h->d_rank;
     f.rank_n = h->S <= RANK_TILED_MAX ? h->R : 0;
+    f.stats_reset = h->d_cstats;
     return f;
 }
 
@@ -1387,6 +1685,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     HIP_TRY(launch_finish(finish_args(h), h->stream));
+    const double seq = (double)(++h->publish_seq);
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     const bool standalone_filter = !(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h));
     if (standalone_filter) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));   // the side stream waits on it
@@ -1424,15 +1723,24 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     // wait for the published block by polling its sequence flag (finish kernels, publish_block): a
     // blocking synchronize sleeps the thread and the wake-up sat on the update's critical path, and
     // an event behind the finish kernel delayed the stream.  The stream is queried now and then so
-    // that a failed launch ends the wait with its error.
+    // that a failed launch ends the wait with its error, and the wait is bounded: a kernel that
+    // never finishes leaves the stream NotReady for good, so past max(5 s, 100 x the last update)
+    // the update fails with MPPI_ERR_DEVICE instead of spinning forever.
     {
-        const double seq = (double)(h->update_count + 1);
         volatile double *flag = h->h_out + HC + 6;
+        const auto t_wait = std::chrono::steady_clock::now();
+        const double limit_s = std::max(h->publish_timeout_s, 100.0 * h->update_duration);
         for (uint64_t spin = 1; *flag != seq; spin++) {
             if ((spin & 4095) == 0) {
                 const hipError_t q = hipStreamQuery(h->stream);
                 if (q != hipErrorNotReady && q != hipSuccess) HIP_TRY(q);
                 if (q == hipSuccess && *flag != seq) return fail(h, MPPI_ERR_DEVICE, "finish kernel did not publish");
+                if (q == hipErrorNotReady &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t_wait).count() > limit_s) {
+                    h->phase_open = false;
+                    return fail(h, MPPI_ERR_DEVICE, "update did not publish within " + std::to_string(limit_s) +
+                                                        " s (device hung?)");
+                }
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -1583,6 +1891,25 @@ mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
     return MPPI_OK;
 }
 
+mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
+{
+    if (!h || !terms7) return MPPI_ERR_INVALID;
+    if (h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || !use_coop(h))
+        return fail(h, MPPI_ERR_UNSUPPORTED, "per-term totals: AssistedManipulation on the cooperative kernel only");
+    HIP_TRY(hipSetDevice(h->device));
+    if (h->opt_state == mppi_handle::OPT_NONE && !h->opt_steps) {   // before the first update: reset(0)
+        for (int i = 0; i < 7; i++) terms7[i] = 0.0;
+        return MPPI_OK;
+    }
+    mppi_status st = wait_optimal(h);   // the filter() row's records are then complete
+    if (st != MPPI_OK) return st;
+    HIP_TRY(launch_fr_terms(h->d_cost, h->opt_steps, h->d_rec_opt, (int)h->H, h->d_terms, h->stream_opt));
+    HIP_TRY(hipMemcpyAsync(h->h_opt + 1, h->d_terms, 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream_opt));
+    HIP_TRY(hipStreamSynchronize(h->stream_opt));
+    std::memcpy(terms7, h->h_opt + 1, 7 * sizeof(double));
+    return MPPI_OK;
+}
+
 mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout)
 {
     if (!h || !rollout) return MPPI_ERR_INVALID;
@@ -1618,6 +1945,13 @@ mppi_status mppi_noise(mppi_handle *h, double *out)
         for (int64_t k = 0; k < h->H; k++)
             for (int64_t c = 0; c < h->C; c++) o[k * h->C + c] = dev[(size_t)((k * h->Rpad + lr) * h->C + c)];
     }
+    return MPPI_OK;
+}
+
+mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
+{
+    if (!h || !info || n < 0 || n > MPPI_UPDATE_INFO_N) return MPPI_ERR_INVALID;
+    std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;
 }
 
@@ -1665,6 +1999,7 @@ mppi_status mppi_set_timing(mppi_handle *h, int level)
         for (auto &e : h->ev_ring) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     }
     h->timing = level;
+    if (level == 2) h->ring_unread = false;   // level 2 times [5] itself (ev[1] / ev_dyn), not the ring
     for (float &m : h->kernel_ms) m = 0.0f;
     return MPPI_OK;
 }
@@ -1696,6 +2031,7 @@ mppi_status mppi_rollout_kernel_times(mppi_handle *h, float *ms, int capacity, i
     }
     *count = n;
     h->ring_count = 0;
+    h->ring_unread = false;   // read: a later level-2 kernel_times(detail) keeps its own [5]
     return MPPI_OK;
 }
 

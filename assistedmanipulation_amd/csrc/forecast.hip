@@ -89,6 +89,20 @@ __global__ __launch_bounds__(64) void forecast_steps_kernel(ForecastArgs f, Step
     out[k] = s;
 }
 
+// forecast(t0 + k dt), k < steps (DynamicsForecast::forecast's wrench rows, dynamics.cpp:113-123:
+// time + step * time_step, two roundings)
+__global__ __launch_bounds__(64) void forecast_table_kernel(ForecastArgs f, double t0, double dt, int64_t steps, double *__restrict__ out)
+{
+    const int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (k >= steps) return;
+    double tk;
+    {
+#pragma clang fp contract(off)
+        tk = t0 + (double)k * dt;
+    }
+    forecast_eval(f, tk, out + k * 6);
+}
+
 __global__ void forecast_eval_kernel(ForecastArgs f, double time, double *out)
 {
     if (threadIdx.x == 0) forecast_eval(f, time, out);
@@ -247,6 +261,13 @@ hipError_t launch_forecast_steps(const ForecastArgs &f, const StepParams &p, con
 hipError_t launch_kalman_observe(DevKalman *kf, double *pred, const KalmanObserve &a, hipStream_t s)
 {
     hipLaunchKernelGGL(kalman_observe_kernel, dim3(1), dim3(KT), 0, s, kf, pred, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_forecast_table(const ForecastArgs &f, double t0, double dt, int64_t steps, double *out, hipStream_t s)
+{
+    if (steps <= 0) return hipSuccess;
+    hipLaunchKernelGGL(forecast_table_kernel, dim3((unsigned)((steps + 63) / 64)), dim3(64), 0, s, f, t0, dt, steps, out);
     return hipGetLastError();
 }
 

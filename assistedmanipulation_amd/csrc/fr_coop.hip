@@ -1620,12 +1620,12 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
 }
 
 // Block 0's share of sampling in fused / draws-ahead launches: U*_shifted and x0 written back for
-// the kernels after the launch, the cost statistics reset (before any row's objective folds in).
+// the kernels after the launch.  (The cost statistics the rows fold into were reset by the previous
+// update's finish kernel, a launch ahead: no reset races the folds inside this launch.)
 template <int NT>
 __device__ __forceinline__ void block0_sample_writes(const FrRolloutArgs &a, int t)
 {
     const SampleArgs &sa = a.samp;
-    if (sa.stats) mppi_sample::reset_cost_stats(sa.stats, t);
     if (sa.sp.shift_by > 0)
         for (int i = t; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
     if (t < sa.X) sa.x0_out[t] = sa.x0v[t];

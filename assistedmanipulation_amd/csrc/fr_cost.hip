@@ -64,9 +64,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     }
 }
 
+// The optimal rollout's per-term totals (AssistedManipulation's accumulators after filter(),
+// mppi.cpp:450-479 with thread 0's cost, reset at its start): one wave over the filter() row's
+// records, lane = step, each term summed over the steps in step order (m_*_cost += per step).
+__global__ __launch_bounds__(64) void fr_terms_kernel(const DevCost *cost, const StepConst *steps, const double *rec, int H,
+                                                      double *out7)
+{
+    const int lane = threadIdx.x;
+    double tot[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int base = 0; base < H; base += 64) {
+        const int n = (H - base < 64) ? H - base : 64;
+        const int k = base + (lane < n ? lane : 0);
+        double t[7];
+        const double *rk = rec + (int64_t)k * FR_NREC;
+        assisted_manipulation_terms(*cost, steps[k], rk, rk[REC_QQD + 4], t);
+#pragma unroll
+        for (int m = 0; m < 7; m++)
+            for (int i = 0; i < n; i++) tot[m] += readlane_f64(t[m], i);
+    }
+    if (lane < 7) {
+        double v = tot[0];
+#pragma unroll
+        for (int m = 1; m < 7; m++) v = lane == m ? tot[m] : v;
+        out7[lane] = v;
+    }
+}
+
 }  // namespace
 
 namespace mppi_eng {
+
+hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s)
+{
+    hipLaunchKernelGGL(fr_terms_kernel, dim3(1), dim3(64), 0, s, cost, steps, rec, H, out7);
+    return hipGetLastError();
+}
 
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s)
 {

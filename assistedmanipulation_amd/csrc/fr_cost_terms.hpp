@@ -151,9 +151,62 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
     return cost;
 }
 
+// The seven terms of AssistedManipulation::get_cost at one step record (the whole record in r), as
+// the reference's per-term accumulators see them (assisted_manipulation.cpp:74-319: m_joint_cost
+// += ..., read back by get_joint_limit_cost() .. get_manipulability_cost(), .hpp:232-258): joint
+// limits, self-collision, workspace, energy, velocity, trajectory, manipulability; a disabled
+// term is 0 (get_cost skips it).  Same arithmetic as assisted_manipulation_cost; the optimal
+// rollout's totals only (mppi_optimal_terms) and the standalone get_cost, so off the rollout
+// kernels' path.  yaw: dynamics->get_state()[2] (workspace_cost, :160-168; in a rollout the
+// record's q_2).
+__device__ __forceinline__ void assisted_manipulation_terms(const DevCost &Cs, const StepConst &sc, const double *r, double yaw,
+                                                            double *t)
+{
+    double j0 = 0.0, j1 = 0.0, v0 = 0.0, v1 = 0.0;
+    for (int j = 0; j < FR_NB; j++) {
+        const double q = r[REC_QQD + 2 * j], vq = fabs(r[REC_QQD + 2 * j + 1]);
+        const double lj = left_barrier(Cs.lower[j], q) + right_barrier(Cs.upper[j], q);
+        const double lv = Cs.vel_q[j] * (vq * vq);
+        if (j < 6) { j0 += lj; v0 += lv; }
+        else { j1 += lj; v1 += lv; }
+    }
+    double s, c;
+    fsincos(yaw, &s, &c, sincos_constants());
+    const double *ee = r + REC_EE, *am = r + REC_AM;
+    double wc = 0.0;
+    {
+        const double r22 = (1.0 - c) + c;
+        const double fw0 = c, fw1 = s, fw2 = 0.0;
+        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
+        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
+        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
+        const double rb2 = am[2] + off2;
+        const double t0 = ee[0] - (am[0] + off0), t1 = ee[1] - (am[1] + off1), t2 = ee[2] - rb2;
+        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
+        wc += left_barrier(Cs.ws_infront, proj);
+        wc += right_barrier(Cs.ws_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
+        const double n1 = sqrt(t0 * t0 + t1 * t1);
+        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
+        const double ya = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
+        const double ay = fabs(ya);
+        const double yc = (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
+        wc += isnan(ya) ? 0.0 : yc;
+        wc += left_barrier(Cs.ws_above, ee[2] - rb2);
+    }
+    const double E = r[REC_E];
+    t[0] = Cs.en_joint ? j0 + j1 : 0.0;
+    t[1] = Cs.en_self ? Cs.self_collision : 0.0;
+    t[2] = Cs.en_work ? wc : 0.0;
+    t[3] = Cs.en_energy ? left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E) : 0.0;
+    t[4] = Cs.en_vel ? v0 + v1 : 0.0;
+    t[5] = Cs.en_traj ? trajectory_term(Cs, sc, r + REC_VL) : 0.0;
+    t[6] = Cs.en_manip ? manipulability_term(Cs, r + REC_JJ) : 0.0;
+}
+
 // TrackPoint::get_cost: the joint terms sum joints 0..9 in order; reach_cost's robot point is the
-// arm mount + R_z(yaw) (0.3, 0, 0.15) (track_point.cpp:162-186)
-__device__ __forceinline__ double track_point_cost(const DevCost &Cs, const double *r)
+// arm mount + R_z(yaw) (0.3, 0, 0.15) (track_point.cpp:162-186), yaw = dynamics->get_state()[2]
+// (in a rollout the record's own q_2)
+__device__ __forceinline__ double track_point_cost(const DevCost &Cs, const double *r, double yaw)
 {
     const double *ee = r + REC_EE, *am = r + REC_AM;
     const double d0 = ee[0] - Cs.tp_point[0], d1 = ee[1] - Cs.tp_point[1], d2 = ee[2] - Cs.tp_point[2];
@@ -168,7 +221,7 @@ __device__ __forceinline__ double track_point_cost(const DevCost &Cs, const doub
         joint += below + above;
     }
     double s, c;
-    fsincos(r[REC_QQD + 4], &s, &c, sincos_constants());
+    fsincos(yaw, &s, &c, sincos_constants());
     const double r22 = (1.0 - c) + c;
     const double off0 = (0.3 * c + (-s) * 0.0) + 0.0 * 0.15;
     const double off1 = (0.3 * s + c * 0.0) + 0.0 * 0.15;
@@ -194,7 +247,7 @@ template <int CK, bool EN, int JS = JT_STRIDE>
 __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
                                            const double2 *src)
 {
-    if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r);
+    if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r, r[REC_QQD + 4]);
     else return sc.gamma_k * assisted_manipulation_cost<EN, JS>(Cs, sc, r, Lj, src);
 }
 

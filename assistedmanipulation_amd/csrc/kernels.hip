@@ -595,7 +595,6 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
     constexpr int NB = DIAG ? (C + 3) / 4 : 1;   // thread pieces per (step, rollout)
     const int k = blockIdx.y;
     if (blockIdx.x == 0 && k == 0 && (int)threadIdx.x < a.X) a.x0_out[threadIdx.x] = a.x0v[threadIdx.x];
-    if (blockIdx.x == 0 && k == 0 && a.stats) mppi_sample::reset_cost_stats(a.stats, threadIdx.x);
     if (blockIdx.x == 0 && a.sp.shift_by > 0 && (int)threadIdx.x < C) {
         const int c = threadIdx.x;
         a.Us[k * C + c] = mppi_sample::shifted_u(a, k, c);
@@ -1200,6 +1199,7 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 {
     __shared__ int sg_err;
     finish_block(a, sg_err);
+    if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, threadIdx.x);
     publish_block(a);
 }
 
@@ -1250,6 +1250,7 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
     }
+    if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, threadIdx.x);
     publish_block(a);
 }
 
@@ -1451,6 +1452,7 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
     }
+    if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, t);
     publish_block(a);
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "engine_types.hpp"
+#include "../../include/mppi_amd.h"
 
 #ifndef GRAD_SPLIT_DEF
 #define GRAD_SPLIT_DEF 8
@@ -55,7 +56,6 @@ struct SampleArgs {
     double *x0_out;
     int X;
     double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
-    CostStats *stats;   // reset by block (0, 0) for this update's costs (may be null)
 };
 
 struct FrRolloutArgs {
@@ -90,7 +90,7 @@ struct FrRolloutArgs {
     // fuse_sample: the launch samples its own rows' eps (samp, sample_device.hpp) before the
     // horizon loop instead of a sample_kernel launch ahead of it (1), or only copies the kept
     // rollouts' columns into draws made ahead (2, draw_ahead_kernel); x0 comes from samp.x0v.
-    // Block 0 writes U*_shifted and x0 back for the kernels after it and resets the cost stats.
+    // Block 0 writes U*_shifted and x0 back for the kernels after it.
     int fuse_sample;
     SampleArgs samp;
     // costs_in_launch (set by launch_fr_coop_update): the waves evaluate the objective of the rows
@@ -178,6 +178,9 @@ struct FinishArgs {
     // the next rank launch accumulates into rank[]: zeroed here when it is the tiled kernel
     int *rank_zero;
     int64_t rank_n;
+    // the cost statistics, consumed by weights_gradient_kernel ahead of this launch: reset here for
+    // the next update's folds (stream-ordered before its rollout launch; may be null)
+    CostStats *stats_reset;
 };
 
 
@@ -270,7 +273,36 @@ bool fr_coop_update_fusable(int64_t count);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
+
+// FrankaRidgeback::PinocchioDynamics as one device-resident object (fr_object.hip): the members of
+// pinocchio_dynamics.hpp:380-425 the methods read and write.
+struct DevPinocchio {
+    double q[FR_NB], v[FR_NB], tau[FR_NB], a[FR_NB];   // m_joint_position / velocity / torque / acceleration
+    double energy, power, time, pad0;                  // EnergyTank, m_power, m_time
+    double state[MAX_X];                               // m_state (X = 31 used)
+    double ee[MPPI_EE_N];                              // m_end_effector_state (mppi_amd.h MPPI_EE_*)
+    double am[3], pad1;                                // the arm-mount frame position (the cost's workspace term)
+};
+enum ObjOp : int { OBJ_SET_STATE = 0, OBJ_STEP = 1, OBJ_FORECAST = 2, OBJ_COST = 3 };
+struct ObjArgs {
+    int op;
+    DevPinocchio *obj;
+    const DevModel *model;
+    double x[MAX_X];      // set_state / forecast / cost: the state
+    double u[FR_C];       // step: the control
+    double time, dt;
+    int64_t steps;        // forecast
+    const double *wrench; // forecast: [steps][6] forecast(t_k), or null (zeros)
+    double *out;          // forecast: [steps][MPPI_DF_N]; cost: [8] total + terms
+    DevCost cost;         // cost: the objective
+    StepConst sc;         // cost: trajectory_cost's constants of the wrench at `time`
+};
+hipError_t launch_fr_object(const ObjArgs &a, hipStream_t s);
+// forecast(t0 + k dt) for k < steps into out[steps][6] (mppi_forecast_table)
+hipError_t launch_forecast_table(const ForecastArgs &f, double t0, double dt, int64_t steps, double *out, hipStream_t s);
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
+// AssistedManipulation's seven per-term totals of one rollout from its [H][FR_NREC] records
+hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s);
 
 
 }  // namespace mppi_eng

@@ -76,10 +76,10 @@ __device__ __forceinline__ void sample_column(const SampleParams &P, int64_t g, 
     }
 }
 
-// The cost statistics before this update's costs are folded in: slot i by thread i (< CS_SLOTS).
-// Device-scope atomic exchanges, performed where the folds' atomics are: with fused sampling the
-// reset and the folds share a launch, and a plain store would wait in this XCD's L2 while the
-// other XCDs' atomics read the previous update's values.
+// The cost statistics emptied for the next update's folds: slot i by thread i (< CS_SLOTS), in the
+// finish kernel (after weights_gradient_kernel read them, one launch ahead of the folds).  Device-
+// scope atomic exchanges, performed where the folds' atomics are (a plain store would sit in this
+// XCD's L2 until the kernel's end-of-launch write-back).
 __device__ __forceinline__ void reset_cost_stats(CostStats *st, int i)
 {
     if (i >= CS_SLOTS) return;

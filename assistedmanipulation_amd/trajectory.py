@@ -184,7 +184,7 @@ class Trajectory:
         self.R, self.H, self.C, self.X = R.value, H.value, Cc.value, X.value
         self._rolled_out_state = np.asarray(configuration.initial_state, dtype=np.float64).copy()
         self._rolled_out_state[:] = 0.0   # m_rollout_state.setZero() (mppi.cpp:121)
-        self._state_buf = np.zeros(self._rolled_out_state.size, dtype=np.float64)
+        self._state_buf = np.zeros(self.X, dtype=np.float64)
         self._state_ptr = _p(self._state_buf)
         self._update_last = 0.0
         self._update_count = 0
@@ -272,6 +272,12 @@ class Trajectory:
         self._check(self._L.mppi_forecast_get(self._h, float(time), _p(out)))
         return out
 
+    def forecast_table(self, t0, dt, steps):
+        """[steps x 6]: forecast(t0 + k dt) of the attached device forecast (mppi_forecast_table)."""
+        out = np.zeros((int(steps), 6))
+        self._check(self._L.mppi_forecast_table(self._h, float(t0), float(dt), int(steps), _p(out)))
+        return out
+
     def step_constants(self):
         """Parity hook: [H x 8] per-step trajectory-cost constants of the last update."""
         out = np.zeros((self.H, 8))
@@ -282,7 +288,9 @@ class Trajectory:
     def update(self, state, time):
         """Trajectory::update (mppi.cpp:154-187)."""
         buf = self._state_buf   # one contiguous buffer and its pointer, built once: the update
-        np.copyto(buf, np.reshape(state, -1))   # path is latency-bound (microseconds per call)
+        if np.size(state) != self.X:   # path is latency-bound (microseconds per call)
+            raise ValueError("state must have %d entries, got %d" % (self.X, np.size(state)))
+        np.copyto(buf, np.reshape(state, -1))
         st = self._L.mppi_update(self._h, self._state_ptr, float(time))
         if st != abi.MPPI_OK:
             self._check(st)
@@ -295,7 +303,9 @@ class Trajectory:
         self._check(self._L.mppi_synchronize(self._h))
 
     def update_phase1(self, state, time):
-        s = np.ascontiguousarray(state, dtype=np.float64)
+        s = np.ascontiguousarray(state, dtype=np.float64).reshape(-1)
+        if s.size != self.X:
+            raise ValueError("state must have %d entries, got %d" % (self.X, s.size))
         self._check(self._L.mppi_update_phase1(self._h, _p(s), float(time)))
         self._rolled_out_state = s.copy()
 
@@ -384,10 +394,25 @@ class Trajectory:
         self._check(self._L.mppi_optimal_cost(self._h, C.byref(d)))
         return d.value
 
+    def get_optimal_terms(self):
+        """The optimal rollout's seven AssistedManipulation term totals (joint limit, self collision,
+        workspace, energy tank, joint velocity, trajectory, manipulability): the accumulators
+        BaseTest / logger::AssistedManipulation read after filter() (mppi_optimal_terms)."""
+        return self._vec(self._L.mppi_optimal_terms, 7)
+
     def argmin(self):
         i = C.c_int64()
         self._check(self._L.mppi_argmin(self._h, C.byref(i)))
         return i.value
+
+    def update_info(self):
+        """What the last update's rollout launch did (mppi_update_info): dict of the engine's own
+        choices (cooperative kernel, folded filter(), objective in the launch, tail draws,
+        sampling mode 0/1/2, rows rolled out)."""
+        out = np.zeros(abi.MPPI_UPDATE_INFO_N, dtype=np.int64)
+        self._check(self._L.mppi_update_info(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), out.size))
+        keys = ("cooperative", "folded_filter", "objective_in_launch", "tail_draws", "sampling", "rows")
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def smoothing_windows(self):
         """(uu, tt, start_idx) of the per-dimension SG windows (SavitzkyGolayFilter::get_windows)."""

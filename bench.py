@@ -2,17 +2,22 @@
 """MPPI rollout throughput on MI355X — BASELINE.json's metric.
 
 A "step" is one mppi::Trajectory::update() (reference src/controller/mppi.cpp:154-187, its own
-timing boundary) of the FrankaRidgeback Pinocchio dynamics + full AssistedManipulation cost,
-4096 samples x 64-step horizon per GPU (BASELINE configs[2]; configs[3] at N = 8), with the
-reference's cadence: updates at t = 0.05 j (5-step shift), keep-best 20, device Philox noise.
-value = samples x horizon x ranks / (max-over-ranks seconds per update).
+timing boundary) with the reference's cadence: updates at t = 0.05 j (5-step shift), keep-best 20,
+device Philox noise.  value = samples x horizon x ranks / (max-over-ranks seconds per update).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Workloads (BASELINE.json configs):
+  frankaridgeback (default)  FrankaRidgeback Pinocchio dynamics + full AssistedManipulation cost,
+                             4096 samples x 64 steps per GPU (configs[2]; configs[3] at N = 8);
+                             --horizon-steps 128 --smoothing 10 for configs[4]'s shape
+  point_mass                 the analytic bring-up plugin, 1024 x 32 (configs[1])
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload point_mass]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -25,26 +30,27 @@ import assistedmanipulation_amd as am  # noqa: E402  (engine's ROCm runtime load
 from assistedmanipulation_amd import abi  # noqa: E402
 
 SAMPLES_PER_GPU = 4096
-HORISON = 0.64            # 64 steps at dt = 0.01
+HORIZON_STEPS = 64        # 0.64 s at dt = 0.01
 KEEP_BEST = 20
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (= fp64 matrix) peak, AMD spec; the rollout is fp64 VALU
 # Algorithmic FLOPs of one rollout-step of the minimal arithmetic the device executes
-# (world-frame zero-bias ABA + kinematics + default cost), counted by the oracle's
+# (world-frame zero-bias dynamics + kinematics + default cost), counted by the oracle's
 # FLOP-counting scalar (tests/test_oracle_cpu.py::test_flop_count_constant pins these values):
-# the cost part (get_cost) runs in fr_step_cost_kernel, the rest in the rollout kernel.
+# the cost part (get_cost) and the rest (dynamics + kinematics).
 FLOPS_PER_ROLLOUT_STEP = 6518.0
 FLOPS_COST_PER_ROLLOUT_STEP = 690.0
 FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STEP
-# Algorithmic HBM bytes per rollout-step: the rollout launch reads its eps column (C = 12 fp64)
-# once; on the records path it also writes a step record (FR_NREC = 42 fp64) the cost kernel reads.
-BYTES_EPS_PER_ROLLOUT_STEP = 96.0
-BYTES_REC_PER_ROLLOUT_STEP = 336.0
-BYTES_PER_ROLLOUT_STEP = BYTES_EPS_PER_ROLLOUT_STEP + BYTES_REC_PER_ROLLOUT_STEP
-# HBM traffic per rollout launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh ->
-# tools/pmc_traffic.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE of the main rollout dispatch.
+# SURVEY §8(d)'s algorithmic HBM bytes per rollout-step: the eps column written once when sampled and
+# read once by the weight reduce, 2 C x sizeof (fp32 in the survey; the device stores fp64 eps).
+BYTES_SURVEY_FR = 2 * 12 * 8.0    # 192 B (FrankaRidgeback, C = 12)
+BYTES_SURVEY_PM = 2 * 3 * 8.0     # 48 B (point mass, C = 3)
+# What the device's rollout launch moves beyond that: it reads the eps column (96 B),
+# and the cooperative kernel writes a 336-B step record that the objective reads back.
+BYTES_EPS_FR = 96.0
+BYTES_REC = 336.0
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
-PMC_JSON = os.path.join(HERE, "profiles", "r02_pmc_rollout.json")
+PMC_JSON = os.path.join(HERE, "profiles", "r03_pmc_rollout.json")
 
 
 def parse():
@@ -54,51 +60,104 @@ def parse():
     # the closing synchronize (~0.18 ms alone), is spread over the steady-state updates
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--samples-per-gpu", type=int, default=SAMPLES_PER_GPU)
-    p.add_argument("--horizon-steps", type=int, default=int(round(HORISON / 0.01)),
-                   help="H (dt = 0.01); 64 = configs[2]/[3], 128 = configs[4]")
-    p.add_argument("--smoothing", type=int, default=0,
-                   help="Savitzky-Golay window (order 1); 10 = configs[4]")
+    p.add_argument("--workload", choices=("frankaridgeback", "point_mass"), default="frankaridgeback")
+    p.add_argument("--samples-per-gpu", type=int, default=None, help="4096 (frankaridgeback) / 1024 (point_mass)")
+    p.add_argument("--horizon-steps", type=int, default=None,
+                   help="H (dt = 0.01); 64 = configs[2]/[3], 128 = configs[4]; 32 for point_mass")
+    p.add_argument("--smoothing", type=int, default=0, help="Savitzky-Golay window (order 1); 10 = configs[4]")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16)
-    return p.parse_args()
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the CPU baseline (0: the CPU share this process may use)")
+    p.add_argument("--cpu-updates", type=int, default=20, help="timed CPU updates (median / p90)")
+    a = p.parse_args()
+    pm = a.workload == "point_mass"
+    if a.samples_per_gpu is None:
+        a.samples_per_gpu = 1024 if pm else SAMPLES_PER_GPU
+    if a.horizon_steps is None:
+        a.horizon_steps = 32 if pm else HORIZON_STEPS
+    return a
 
 
-def cpu_baseline(threads, samples, horison):
+def cpu_share():
+    """CPUs this process may run on: its affinity mask, capped by OMP_NUM_THREADS (the GPU box sets
+    it to the per-GPU CPU share, 16) - not os.cpu_count(), which counts the whole host."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def time_oracle(libpath, conf, dyn, cost, updates, compat_uint8=0, forecast=True):
+    """Median / p90 seconds per Trajectory::update of the oracle (its own steady_clock boundary,
+    mppi.cpp:161-184) over `updates` timed updates after one warm-up, t = 0.05 j."""
+    from oracle import oracle as O
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, dyn.descriptor(), cost.descriptor(), lib_path=libpath, compat_uint8=compat_uint8)
+    orc.set_noise_source(False, 12345)
+    if forecast:
+        orc.set_forecast(am.constant_forecast(orc.H))
+    x = np.asarray(conf.initial_state, dtype=np.float64)
+    orc.update(x, 0.0)   # warm-up
+    durs = []
+    for j in range(1, updates + 1):
+        orc.update(x, 0.05 * j)
+        durs.append(orc.update_duration())
+    return float(np.median(durs)), float(np.percentile(durs, 90)), orc.H
+
+
+def cpu_baseline(args, pm):
     """The oracle (fp64 restatement of the reference's CPU mppi.cpp path, Pinocchio-order
-    arithmetic, contiguous-block thread partition of mppi.cpp:272-307) on this host: a bounded
-    sample of the same workload (a few full updates)."""
+    arithmetic, contiguous-block thread partition of mppi.cpp:272-307) on this host, g++ -O3
+    -march=native: the bench's workload at the process's CPU share (WIDE indices: R > 255 hangs
+    the reference's uint8 loops), and configs[0] (128 x 32, one thread, the reference's own uint8
+    index semantics); median and p90 over --cpu-updates timed updates each."""
     from oracle import oracle as O
     try:
         libpath = O.build(native=True)   # g++ -O3 -march=native on the GPU box host
     except Exception:
         libpath = O.LIB_PATH
-    conf = am.frankaridgeback_configuration(rollouts=samples, horison=horison, keep_best_rollouts=KEEP_BEST,
-                                            threads=threads)
-    cc, keep = conf.to_c()
-    orc = O.OracleTrajectory(cc, am.FrankaRidgebackDynamics().descriptor(), am.AssistedManipulation().descriptor(),
-                             lib_path=libpath)
-    orc.set_noise_source(False, 12345)
-    orc.set_forecast(am.constant_forecast(orc.H))
-    x = am.huddled_state()
-    orc.update(x, 0.0)   # warm-up
-    durs = []
-    t_total = 0.0
-    j = 1
-    while j <= 8 and (t_total < 10.0 or j <= 2):
-        orc.update(x, 0.05 * j)
-        d = orc.update_duration()
-        durs.append(d)
-        t_total += d
-        j += 1
-    med = float(np.median(durs))
-    return {"value": samples * orc.H / med, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
-            "sample": "%d timed updates of the %dx%d FrankaRidgeback workload (median %.3f s/update), "
-                      "oracle/mppi_oracle.cpp fp64, %d threads, -march=native" % (len(durs), samples, orc.H, med, threads)}
+    threads = args.cpu_threads or cpu_share()
+    S, H = args.samples_per_gpu, args.horizon_steps
+    if pm:
+        conf = am.point_mass_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=KEEP_BEST)
+        conf.threads = threads
+        dyn, cost = am.PointMassDynamics(), am.QuadraticCost()
+    else:
+        conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=KEEP_BEST,
+                                                threads=threads)
+        dyn, cost = am.FrankaRidgebackDynamics(), am.AssistedManipulation()
+    med, p90, Ho = time_oracle(libpath, conf, dyn, cost, args.cpu_updates, forecast=not pm)
+    out = {"value": S * Ho / med, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
+           "median_s_per_update": med, "p90_s_per_update": p90,
+           "sample": "%d timed updates of the %dx%d %s workload, oracle/mppi_oracle.cpp fp64, %d threads "
+                     "(the process's CPU share; host %s, %d logical CPUs), -march=native" % (
+                         args.cpu_updates, S, Ho, "point-mass" if pm else "FrankaRidgeback", threads, cpu_model(),
+                         os.cpu_count() or 0)}
+    if not pm:   # configs[0]: the reference's own plumbing case, single thread, uint8 indices
+        c0 = am.frankaridgeback_configuration(rollouts=128, horison=0.32, keep_best_rollouts=KEEP_BEST, threads=1)
+        m0, q0, H0 = time_oracle(libpath, c0, am.FrankaRidgebackDynamics(), am.AssistedManipulation(),
+                                 args.cpu_updates, compat_uint8=1)
+        out["configs0"] = {"value": 128 * H0 / m0, "unit": "rollout-steps/s", "cores": 1,
+                           "median_s_per_update": m0, "p90_s_per_update": q0,
+                           "workload": "128 x 32 FrankaRidgeback, single thread, uint8 index semantics (BASELINE configs[0])"}
+    return out
 
 
 def main():
     args = parse()
+    pm = args.workload == "point_mass"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -108,11 +167,20 @@ def main():
         dist.init_process_group("gloo")
     S_total = args.samples_per_gpu * world
     horison = args.horizon_steps * 0.01
-    sg = am.Smoothing(args.smoothing, 1) if args.smoothing > 0 else None
-    default_workload = args.samples_per_gpu == SAMPLES_PER_GPU and args.horizon_steps == 64 and sg is None
-    conf = am.frankaridgeback_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST,
-                                            smoothing=sg)
-    traj = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
+    sg = am.Smoothing(args.smoothing, 1) if (args.smoothing > 0 and not pm) else None
+    if pm:
+        conf = am.point_mass_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST)
+        traj = am.Trajectory.create(conf, am.PointMassDynamics(), am.QuadraticCost(), device=local_rank)
+        default_workload = args.samples_per_gpu == 1024 and args.horizon_steps == 32
+        cfg_index = 1
+        x = np.zeros(6)
+    else:
+        conf = am.frankaridgeback_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST,
+                                                smoothing=sg)
+        traj = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
+        default_workload = args.samples_per_gpu == SAMPLES_PER_GPU and args.horizon_steps == 64 and sg is None
+        cfg_index = 2 if world == 1 else 3
+        x = am.huddled_state()
     if traj is None:
         raise SystemExit("engine create failed")
     if world > 1:
@@ -120,8 +188,8 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         traj.comm_init(world, rank, uid[0])
     traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
-    traj.set_forecast(am.constant_forecast(traj.H))
-    x = am.huddled_state()
+    if not pm:
+        traj.set_forecast(am.constant_forecast(traj.H))
     traj.set_timing(1)   # creates the engine's timing-event ring outside the timed region
     traj.set_timing(0)
     j = 0
@@ -152,7 +220,8 @@ def main():
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
     dyn_times = traj.rollout_kernel_times()   # the rollout kernel's HIP-event times, sampled updates
-    dyn, nd = sum(dyn_times), len(dyn_times)
+    info = traj.update_info()      # what the engine's rollout launch did (its own choice, not re-derived)
+    dyn_ms = sum(dyn_times) / max(len(dyn_times), 1)
     # the per-phase breakdown from a few further updates with every event recorded (untimed)
     traj.set_timing(2)
     kt = np.zeros(6)
@@ -171,33 +240,71 @@ def main():
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
     value = S_total * traj.H / (elapsed / args.steps)
-    lane = os.environ.get("MPPI_FR_KERNEL") == "lane"   # A/B: the fused one-lane-per-rollout kernel
-    dyn_ms = dyn / max(nd, 1)                             # the rollout (dynamics) kernel alone, timed loop
-    records = not lane   # the coop kernel writes step records; the objective reads them back
-    # one round of four-wave workgroups (fr_coop.hip fr_coop_update_fusable): the launch evaluates
-    # the objective itself in the SIMDs' idle tail (MPPI_COSTS_IN_LAUNCH=0: fr_step_cost_kernel)
-    count_all = traj.R // world + (1 if rank < traj.R % world else 0)
-    groups = count_all // 16
-    xrows = count_all - 16 * groups + (1 if count_all - 16 * groups > 0 else 0)
-    in_launch = records and os.environ.get("MPPI_COSTS_IN_LAUNCH") != "0" and 0 < groups <= 256 and xrows <= 4 * groups
-    # the launch's tail also writes the next update's eps of its main waves' rows (tail_draws)
-    tail_draws = in_launch and xrows > 0 and os.environ.get("MPPI_TAIL_DRAWS") != "0" and os.environ.get("MPPI_DRAW_AHEAD") != "0"
-    cost_ms = float(kt[1] - kt[5]) if records and not in_launch else 0.0   # fr_step_cost_kernel (breakdown pass)
-    traffic = None
-    if os.path.exists(PMC_JSON) and world == 1 and default_workload:
-        with open(PMC_JSON) as f:
-            traffic = json.load(f)["traffic_bytes"]
     count_local = traj.R // world + (1 if rank < traj.R % world else 0)
-    units = count_local * traj.H
-    flops_unit = FLOPS_DYN_PER_ROLLOUT_STEP if records and not in_launch else FLOPS_PER_ROLLOUT_STEP
-    flops = flops_unit * units
-    achieved_tflops = flops / (dyn_ms * 1e-3) / 1e12
+    units = count_local * traj.H            # rollout-steps of this rank's rollout launch
+    units_all = traj.R * traj.H             # of the whole update
+    if pm:
+        # pm_rollout_kernel: one lane per rollout, reads its 24-B eps column per step (fp64)
+        kernel = "pm_rollout_kernel"
+        rollout_bytes = 24.0 * units
+        roofline = {"bound": "hbm", "kernel": kernel, "achieved": rollout_bytes / (dyn_ms * 1e-3) / 1e9,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "bytes_per_launch": rollout_bytes, "bytes_per_rollout_step": 24.0}
+        roofline["frac"] = roofline["achieved"] / roofline["peak"]
+        roofline["traffic"] = None
+        survey_bytes = BYTES_SURVEY_PM
+    else:
+        lane = info["cooperative"] == 0   # MPPI_FR_KERNEL=lane A/B: the fused one-lane-per-rollout kernel
+        in_launch = info["objective_in_launch"] == 1
+        flops_unit = FLOPS_PER_ROLLOUT_STEP if (in_launch or lane) else FLOPS_DYN_PER_ROLLOUT_STEP
+        rows_units = info["rows"] * traj.H   # rollout rows of the launch (+ a folded filter() row)
+        achieved_tflops = flops_unit * rows_units / (dyn_ms * 1e-3) / 1e12
+        traffic = None
+        if os.path.exists(PMC_JSON) and world == 1 and default_workload and not lane:
+            with open(PMC_JSON) as f:
+                traffic = json.load(f)["traffic_bytes"]
+        # the launch's HBM bytes by design: eps read, step records written and (objective in the
+        # launch) read back, the next update's eps written in the tail (tail draws)
+        launch_bytes = ((BYTES_EPS_FR + BYTES_REC * (2 if in_launch else 1)) * rows_units
+                        + (BYTES_EPS_FR * units if info["tail_draws"] else 0.0)) if not lane else BYTES_EPS_FR * units
+        roofline = {"bound": "valu", "kernel": "fr_rollout_kernel" if lane else (
+                        "fr_coop_x_kernel (dynamics + objective)" if in_launch else "fr_coop_kernel"),
+                    "compute": "fp64 VALU, issue-bound at one wave per SIMD (no dense contraction for MFMA)",
+                    "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
+                    "traffic_unit": "HBM bytes per rollout launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
+                                    os.path.relpath(PMC_JSON, HERE),
+                    "flops_per_rollout_step": flops_unit,
+                    "launch_bytes_by_design": launch_bytes,
+                    "launch_GBs_by_design": launch_bytes / (dyn_ms * 1e-3) / 1e9}
+        survey_bytes = BYTES_SURVEY_FR
+    # SURVEY §8(d)'s algorithmic bytes per update (eps written once + read once by the reduce, fp64)
+    # over the whole update's time: the HBM view of the metric; what the design moves beyond it (the
+    # step records' round trip, the rollout's own eps read) is reported beside it as extra traffic
+    hbm = {"survey_bytes_per_rollout_step": survey_bytes,
+           "update_GBs_survey_bytes": survey_bytes * units_all / (ms_per_step * 1e-3) / 1e9,
+           "peak_GBs": HBM_PEAK_GBS}
+    hbm["frac_survey_bytes"] = hbm["update_GBs_survey_bytes"] / HBM_PEAK_GBS
+    if not pm:
+        hbm["extra_bytes_per_rollout_step"] = {"rollout_eps_read": BYTES_EPS_FR,
+                                               "step_record_round_trip": 2 * BYTES_REC if info["objective_in_launch"] else BYTES_REC}
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
+    if pm:
+        workload = "%s%d samples x %d horizon, point-mass analytic dynamics + quadratic cost" % (
+            "BASELINE configs[1]: " if default_workload else "", S_total, traj.H)
+        metric = "MPPI rollouts/sec (samples x horizon steps/s), %dx%d point mass" % (S_total, traj.H)
+        data = "synthetic (x0 = 0, target (1,1,1), Philox noise)"
+    else:
+        workload = "%s%d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, full AssistedManipulation cost stack%s%s" % (
+            ("BASELINE configs[%d]: " % cfg_index) if default_workload else "", S_total, traj.H,
+            ", Savitzky-Golay window %d order 1" % args.smoothing if sg else "", ", sample-sharded over RCCL" if world > 1 else "")
+        metric = "MPPI rollouts/sec (samples x horizon steps/s), %dx%d FrankaRidgeback" % (S_total, traj.H)
+        data = "synthetic (HUDDLED state, constant forecast wrench (20,0,0) N, Philox noise)"
     line = {
-        "metric": "MPPI rollouts/sec (samples x horizon steps/s), %dx%d FrankaRidgeback" % (S_total, traj.H),
+        "metric": metric,
         "value": value,
         "unit": "rollout-steps/s",
         "n_gpus": world,
@@ -208,34 +315,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (HUDDLED state, constant forecast wrench (20,0,0) N, Philox noise)",
-        "config": {"workload": "%s%d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, "
-                               "full AssistedManipulation cost stack%s%s" % (
-                                   ("BASELINE configs[%d]: " % (2 if world == 1 else 3)) if default_workload else "",
-                                   S_total, traj.H, ", Savitzky-Golay window %d order 1" % args.smoothing if sg else "",
-                                   ", sample-sharded over RCCL" if world > 1 else ""),
-                   "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST, "parallelism": "samples-dp%d" % world},
-        "kernel_ms": {"rollout_dynamics": dyn_ms, "rollout_cost": cost_ms, "breakdown_untimed": {
+        "data": data,
+        "config": {"workload": workload, "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST,
+                   "parallelism": "samples-dp%d" % world},
+        "engine": info,
+        "kernel_ms": {"rollout_launch": dyn_ms, "rollout_launch_samples": len(dyn_times), "breakdown_untimed": {
                       "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]}},
-        # The rollout kernel runs fp64 VALU work (no MFMA: the 12-body chain has no dense contraction)
-        # at one wave per SIMD, so it is bound by issue slots and dependency chains, not by a
-        # datapath peak; the fraction is reported against the fp64 vector peak.
-        "roofline": {"bound": "valu", "compute": "fp64 VALU, latency/issue-bound at one wave per SIMD",
-                     "kernel": "fr_rollout_kernel" if lane else ("fr_coop_x_kernel (dynamics + objective)" if in_launch else "fr_coop_x_kernel"),
-                     "achieved": achieved_tflops,
-                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS,
-                     "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_JSON, HERE),
-                     "flops_per_rollout_step": flops_unit},
-        "hbm": {"rollout_algorithmic_GBs": ((BYTES_PER_ROLLOUT_STEP + (BYTES_REC_PER_ROLLOUT_STEP if in_launch else 0.0)
-                                             + (BYTES_EPS_PER_ROLLOUT_STEP if tail_draws else 0.0))
-                                            if records else BYTES_EPS_PER_ROLLOUT_STEP) * units / (dyn_ms * 1e-3) / 1e9,
-                "objective_in_rollout_launch": in_launch,
-                "cost_kernel_algorithmic_GBs": BYTES_REC_PER_ROLLOUT_STEP * units / (cost_ms * 1e-3) / 1e9 if records and cost_ms > 0 else None,
-                "peak_GBs": HBM_PEAK_GBS},
+        "roofline": roofline,
+        "hbm": hbm,
     }
-    if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.samples_per_gpu, horison)
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(args, pm)
         # not vs_baseline (no published number): the GPU / CPU-port ratio, same workload
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line))

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPPI_AMD_ABI_VERSION 3
+#define MPPI_AMD_ABI_VERSION 4
 
 #define MPPI_MAX_BODIES 16
 #define MPPI_MAX_CONTROL 16
@@ -350,10 +350,34 @@ mppi_status mppi_gradient(mppi_handle *h, double *gradient_CxH);
 mppi_status mppi_optimal_control(mppi_handle *h, double *control_CxH);
 mppi_status mppi_optimal_cost(mppi_handle *h, double *cost);
 mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout);
+/* The optimal rollout's per-term totals: FrankaRidgeback::AssistedManipulation's accumulators after
+ * filter() (thread 0's cost, reset at the optimal rollout's start; assisted_manipulation.cpp:24-35,
+ * 74-319), which BaseTest reads by downcasting get_optimal_cost() (test/case/base.cpp:140-146) and
+ * logger::AssistedManipulation logs (logging/assisted_manipulation.cpp:61-90).  terms7[MPPI_TERM_*];
+ * a disabled term is 0.  AssistedManipulation objective only (MPPI_ERR_UNSUPPORTED otherwise). */
+#define MPPI_TERM_JOINT_LIMIT 0      /* get_joint_limit_cost()      (.hpp:232-234) */
+#define MPPI_TERM_SELF_COLLISION 1   /* get_self_collision_cost()   (.hpp:236-238) */
+#define MPPI_TERM_WORKSPACE 2        /* get_workspace_cost()        (.hpp:240-242) */
+#define MPPI_TERM_ENERGY_TANK 3      /* get_energy_tank_cost()      (.hpp:244-246) */
+#define MPPI_TERM_JOINT_VELOCITY 4   /* get_joint_velocity_cost()   (.hpp:248-250) */
+#define MPPI_TERM_TRAJECTORY 5       /* get_trajectory_cost()       (.hpp:252-254) */
+#define MPPI_TERM_MANIPULABILITY 6   /* get_manipulability_cost()   (.hpp:256-258) */
+mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7);
 mppi_status mppi_update_duration(mppi_handle *h, double *seconds);
 mppi_status mppi_noise(mppi_handle *h, double *noise_R_C_H);
 mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
                       int64_t *control_C, int64_t *state_X);
+
+/* What the last update's rollout launch did (diagnostics for bench / tests; the engine decides it
+ * from the device's CU count and the workload): info[i] for i < n (n <= MPPI_UPDATE_INFO_N). */
+#define MPPI_INFO_COOPERATIVE 0           /* 16-lane cooperative kernel (else one lane per rollout) */
+#define MPPI_INFO_FOLDED_FILTER 1         /* the previous update's filter() rode in the launch */
+#define MPPI_INFO_OBJECTIVE_IN_LAUNCH 2   /* the objective ran in the launch (no cost kernel) */
+#define MPPI_INFO_TAIL_DRAWS 3            /* the launch drew the next update's eps (main rows) */
+#define MPPI_INFO_SAMPLING 4              /* 0 sample kernel, 1 sampled in launch, 2 drawn ahead */
+#define MPPI_INFO_ROWS 5                  /* rows rolled out (local rollouts + a folded filter()) */
+#define MPPI_UPDATE_INFO_N 6
+mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
 /* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control
  * dimension the value and time buffers (C x (H + 2w + 1), row per dimension) and start index. */
@@ -378,6 +402,70 @@ mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n);
  * cleared.  Reading them after a timed loop keeps the event queries out of it (querying an event
  * pair right behind the publish held the host ~70 us). */
 mppi_status mppi_rollout_kernel_times(mppi_handle *h, float *ms, int capacity, int *count);
+
+
+/* ------------------------------------------------------------------------------------------
+ * FrankaRidgeback::PinocchioDynamics as a device object (one trajectory).  The reference's
+ * plugin is also an object with its own state (mppi.hpp:47-84, dynamics.hpp:416-537): the Actor's
+ * DynamicsForecast steps one forward every controller period (dynamics.cpp:104-138), and a cost
+ * reads the dynamics' cached end-effector state.  Its state lives in HBM and each call is one
+ * single-thread kernel (pinocchio_dynamics.cpp:142-260 semantics, quirks included: set_state's
+ * calculate() adds NLE onto the torque the previous call left).  FrankaRidgeback only.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct mppi_dynamics mppi_dynamics;
+
+/* EndEffectorState (dynamics.hpp:95-117) of the last calculate(), doubles: */
+#define MPPI_EE_POSITION 0               /* 3: oMf[panda_grasp_joint].translation() */
+#define MPPI_EE_QUATERNION 3             /* 4: orientation, Eigen coefficient order (x, y, z, w) */
+#define MPPI_EE_ROTATION 7               /* 9: the same orientation as a row-major rotation matrix */
+#define MPPI_EE_LINEAR_VELOCITY 16       /* 3: getFrameVelocity(WORLD).linear() */
+#define MPPI_EE_ANGULAR_VELOCITY 19      /* 3 */
+#define MPPI_EE_LINEAR_ACCELERATION 22   /* 3: getFrameAcceleration(WORLD).linear() (no gravity) */
+#define MPPI_EE_ANGULAR_ACCELERATION 25  /* 3 */
+#define MPPI_EE_JACOBIAN 28              /* 72: 6 x 12 row-major, WORLD, top-left 3x3 = R_z(yaw) */
+#define MPPI_EE_N 100
+
+/* One row of DynamicsForecast::forecast per step (dynamics.cpp:113-127), doubles: */
+#define MPPI_DF_JOINT_POSITION 0                   /* 12: m_joint_position[step] */
+#define MPPI_DF_END_EFFECTOR 12                    /* MPPI_EE_N: m_end_effector[step] */
+#define MPPI_DF_JOINT_POWER (12 + MPPI_EE_N)       /* m_joint_power[step] (0 for Pinocchio) */
+#define MPPI_DF_EXTERNAL_POWER (13 + MPPI_EE_N)    /* m_external_power[step] (0 for Pinocchio) */
+#define MPPI_DF_ENERGY (14 + MPPI_EE_N)            /* m_energy[step]: the tank */
+#define MPPI_DF_WRENCH (15 + MPPI_EE_N)            /* 6: m_end_effector_wrench[step] = forecast(t) */
+#define MPPI_DF_N (21 + MPPI_EE_N)
+
+/* PinocchioDynamics::create (pinocchio_dynamics.cpp:19-83; the constructor's set_state of the
+ * configuration's initial state, :84-115).  `initial_state`: X = 31 doubles. */
+mppi_status mppi_dynamics_create(const mppi_dynamics_desc *desc, const double *initial_state, int device,
+                                 mppi_dynamics **out);
+void mppi_dynamics_destroy(mppi_dynamics *d);
+/* set_state (pinocchio_dynamics.cpp:142-151). */
+mppi_status mppi_dynamics_set_state(mppi_dynamics *d, const double *state, double time);
+/* step (pinocchio_dynamics.cpp:226-260): control C = 12; the new state (X) into state_out (may be NULL). */
+mppi_status mppi_dynamics_step(mppi_dynamics *d, const double *control, double dt, double *state_out);
+/* get_state (m_state, X doubles). */
+mppi_status mppi_dynamics_get_state(mppi_dynamics *d, double *state);
+/* get_end_effector_state (MPPI_EE_N doubles). */
+mppi_status mppi_dynamics_end_effector(mppi_dynamics *d, double *ee);
+/* The object's other members after its last call: joint position, velocity, acceleration,
+ * torque (12 each), tank energy, power, time, arm-mount frame position (3) = 54 doubles. */
+#define MPPI_DYNAMICS_QUERY_N 54
+mppi_status mppi_dynamics_query(mppi_dynamics *d, double *out);
+/* DynamicsForecast::forecast(state, time) (dynamics.cpp:104-138): set_state, then `steps` times
+ * record the row and step with Control::Zero() over time_step.  `wrench`: steps x 6 rows of
+ * forecast(time + k time_step) (e.g. mppi_forecast_table), copied into the rows; NULL: zeros.
+ * out: steps x MPPI_DF_N. */
+mppi_status mppi_dynamics_forecast(mppi_dynamics *d, const double *state, double time, double time_step,
+                                   int64_t steps, const double *wrench, double *out);
+/* Cost::get_cost(state, control, dynamics, time) (mppi.hpp:127-132) of AssistedManipulation
+ * (assisted_manipulation.cpp:37-72) or TrackPoint (track_point.cpp:10-34) on the device against the
+ * object's cached kinematics.  wrench6: forecast(time) of the dynamics' forecast handle, or NULL
+ * when it has none (trajectory_cost is then 0, :239-240).  out: the cost, then the seven
+ * AssistedManipulation terms (MPPI_TERM_*; zeros for TrackPoint) = 8 doubles. */
+mppi_status mppi_cost_evaluate(const mppi_cost_desc *cost, mppi_dynamics *d, const double *state,
+                               const double *control, const double *wrench6, double *out8);
+/* forecast(t0 + k dt) for k < steps of the handle's attached forecast (steps x 6). */
+mppi_status mppi_forecast_table(mppi_handle *h, double t0, double dt, int64_t steps, double *out);
 
 #ifdef __cplusplus
 }

@@ -481,7 +481,10 @@ template <class T> struct FrankaDynamics {
     T state[MPPI_FR_STATE];
     // cached kinematics (computed in calculate() BEFORE integration: the one-step lag)
     V3<T> ee_pos, am_pos, ee_lin_vel, ee_ang_vel;
+    V3<T> ee_lin_acc, ee_ang_acc;   // getFrameAcceleration(WORLD) (:211-223)
+    M3<T> ee_rot;                   // oMf[EE].rotation() (:217)
     T J[6][12];
+    T power = T(0);
 
     void init(const Model<T> *m)
     {
@@ -509,18 +512,27 @@ template <class T> struct FrankaDynamics {
             calculate_reduced();
             return;
         }
-        // forwardKinematics(q, v, a) — placements and velocities (accelerations unused)
+        // forwardKinematics(q, v, a) — placements, velocities and accelerations (Pinocchio's
+        // forward pass, local frames: a_i = iXp a_p + S qdd + v_i x (S qd), no gravity)
         for (int i = 0; i < M->nb; i++) {
             const int p = M->b[i].parent;
             D.liMi[i] = compose(M->b[i].placement, M->jointM(i, q[i]));
             D.oMi[i] = p >= 0 ? compose(D.oMi[p], D.liMi[i]) : D.liMi[i];
             Motion<T> S = M->S(i);
-            D.v[i].v = qd[i] * S.v;
-            D.v[i].w = qd[i] * S.w;
+            Motion<T> vj;
+            vj.v = qd[i] * S.v;
+            vj.w = qd[i] * S.w;
+            D.v[i] = vj;
+            D.a[i].v = qdd[i] * S.v;
+            D.a[i].w = qdd[i] * S.w;
             if (p >= 0) {
                 Motion<T> t = actInv(D.liMi[i], D.v[p]);
                 D.v[i].v = D.v[i].v + t.v;
                 D.v[i].w = D.v[i].w + t.w;
+                Motion<T> ta = actInv(D.liMi[i], D.a[p]);
+                Motion<T> c = mcross(D.v[i], vj);
+                D.a[i].v = (ta.v + D.a[i].v) + c.v;
+                D.a[i].w = (ta.w + D.a[i].w) + c.w;
             }
         }
         // updateFramePlacements: oMf = oMi[parent] * placement
@@ -545,6 +557,10 @@ template <class T> struct FrankaDynamics {
         Motion<T> vw = act(D.oMi[M->ee_parent], D.v[M->ee_parent]);
         ee_lin_vel = vw.v;
         ee_ang_vel = vw.w;
+        Motion<T> aw = act(D.oMi[M->ee_parent], D.a[M->ee_parent]);   // getFrameAcceleration(WORLD)
+        ee_lin_acc = aw.v;
+        ee_ang_acc = aw.w;
+        ee_rot = ee.R;
     }
 
     // Minimal arithmetic (used for FLOP counting and to bound the arithmetic difference):
@@ -664,7 +680,7 @@ template <class T> struct FrankaDynamics {
         calculate();
         for (int i = 0; i < 12; i++) qd[i] = qd[i] + qdd[i] * dt;   // semi-implicit Euler
         for (int i = 0; i < 12; i++) q[i] = q[i] + qd[i] * dt;
-        T power = tau[0] * qd[0];
+        power = tau[0] * qd[0];
         for (int i = 1; i < 12; i++) power += tau[i] * qd[i];
         energy = s_max(T(0), energy + power * dt);   // EnergyTank::step
         state[30] = energy;
@@ -1564,6 +1580,150 @@ void oracle_optimal_terms(void *h, double *out7)
     out7[4] = c.velocity; out7[5] = c.trajectory; out7[6] = c.manipulability;
 }
 
+
+// ---- FrankaRidgeback::PinocchioDynamics as an object (the engine's mppi_dynamics_*) ----------
+// pinocchio_dynamics.cpp:84-260 on the Pinocchio-order restatement above: the constructor's
+// setZero()s and set_state, set_state / step / get_state / get_end_effector_state, and
+// DynamicsForecast::forecast (frankaridgeback/dynamics.cpp:104-138).
+struct OracleDyn {
+    orc::Model<double> m;
+    orc::FrankaDynamics<double> d;
+    double time = 0.0;
+};
+
+// EndEffectorState in the engine's MPPI_EE_* layout (100 doubles); the quaternion by Eigen's
+// Quaternion(Matrix3) (quaternionbase_assign_impl), coefficients (x, y, z, w)
+static void oracle_ee_row(const orc::FrankaDynamics<double> &d, double *o)
+{
+    for (int k = 0; k < 3; k++) o[k] = d.ee_pos[k];
+    const double *R = d.ee_rot.a;
+    double q[4];
+    const double t = R[0] + R[4] + R[8];
+    if (t > 0.0) {
+        double s = std::sqrt(t + 1.0);
+        q[3] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (R[7] - R[5]) * s;
+        q[1] = (R[2] - R[6]) * s;
+        q[2] = (R[3] - R[1]) * s;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
+        q[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[3] = (R[3 * k + j] - R[3 * j + k]) * s;
+        q[j] = (R[3 * j + i] + R[3 * i + j]) * s;
+        q[k] = (R[3 * k + i] + R[3 * i + k]) * s;
+    }
+    for (int k = 0; k < 4; k++) o[3 + k] = q[k];
+    for (int k = 0; k < 9; k++) o[7 + k] = R[k];
+    for (int k = 0; k < 3; k++) {
+        o[16 + k] = d.ee_lin_vel[k];
+        o[19 + k] = d.ee_ang_vel[k];
+        o[22 + k] = d.ee_lin_acc[k];
+        o[25 + k] = d.ee_ang_acc[k];
+    }
+    for (int r = 0; r < 6; r++)
+        for (int c = 0; c < 12; c++) o[28 + 12 * r + c] = d.J[r][c];
+}
+
+void *oracle_dyn_create(const mppi_frankaridgeback_desc *desc, const double *x0)
+{
+    OracleDyn *o = new OracleDyn;
+    o->m.load(*desc);
+    o->d.init(&o->m);   // setZero()s (pinocchio_dynamics.cpp:106-109)
+    o->d.set_state(x0);
+    return o;
+}
+
+void oracle_dyn_destroy(void *h) { delete (OracleDyn *)h; }
+
+void oracle_dyn_set_state(void *h, const double *x, double time)
+{
+    OracleDyn *o = (OracleDyn *)h;
+    o->time = time;
+    o->d.set_state(x);
+}
+
+void oracle_dyn_step(void *h, const double *u, double dt, double *x_out)
+{
+    OracleDyn *o = (OracleDyn *)h;
+    const double *x = o->d.step(u, dt);
+    o->time += dt;
+    if (x_out)
+        for (int i = 0; i < MPPI_FR_STATE; i++) x_out[i] = x[i];
+}
+
+void oracle_dyn_get_state(void *h, double *x)
+{
+    for (int i = 0; i < MPPI_FR_STATE; i++) x[i] = ((OracleDyn *)h)->d.state[i];
+}
+
+void oracle_dyn_end_effector(void *h, double *ee100) { oracle_ee_row(((OracleDyn *)h)->d, ee100); }
+
+// q, v, a, tau (12 each), tank energy, power, time, arm-mount position (3): MPPI_DYNAMICS_QUERY_N
+void oracle_dyn_query(void *h, double *out)
+{
+    const OracleDyn *o = (const OracleDyn *)h;
+    const orc::FrankaDynamics<double> &d = o->d;
+    for (int i = 0; i < 12; i++) {
+        out[i] = d.q[i];
+        out[12 + i] = d.qd[i];
+        out[24 + i] = d.qdd[i];
+        out[36 + i] = d.tau[i];
+    }
+    out[48] = d.energy;
+    out[49] = d.power;
+    out[50] = o->time;
+    for (int k = 0; k < 3; k++) out[51 + k] = d.am_pos[k];
+}
+
+// DynamicsForecast::forecast (dynamics.cpp:104-138): rows of MPPI_DF_N (121) doubles
+void oracle_dyn_forecast(void *h, const double *x, double time, double time_step, int64_t steps, const double *wrench,
+                         double *out)
+{
+    OracleDyn *o = (OracleDyn *)h;
+    oracle_dyn_set_state(h, x, time);
+    const double zero[MPPI_FR_CONTROL] = {0};
+    for (int64_t k = 0; k < steps; k++) {
+        double *r = out + k * 121;
+        for (int i = 0; i < 12; i++) r[i] = o->d.q[i];
+        oracle_ee_row(o->d, r + 12);
+        r[112] = 0.0;   // get_joint_power
+        r[113] = 0.0;   // get_external_power
+        r[114] = o->d.energy;
+        for (int i = 0; i < 6; i++) r[115 + i] = wrench ? wrench[6 * k + i] : 0.0;
+        oracle_dyn_step(h, zero, time_step, nullptr);
+    }
+}
+
+// Cost::get_cost(state, control, dynamics, time) against the object (the engine's
+// mppi_cost_evaluate): out8 = cost, seven AssistedManipulation terms (zeros for TrackPoint)
+void oracle_cost_evaluate(const mppi_cost_desc *cost, void *h, const double *x, const double *wrench6, double *out8)
+{
+    OracleDyn *o = (OracleDyn *)h;
+    for (int i = 0; i < 8; i++) out8[i] = 0.0;
+    if (cost->kind == MPPI_COST_TRACK_POINT) {
+        orc::TrackPoint<double> c;
+        c.cfg = cost->track_point;
+        out8[0] = c.get_cost(x, o->d, 0);
+        return;
+    }
+    orc::AssistedManipulation<double> c;
+    c.cfg = cost->assisted_manipulation;
+    if (!wrench6) c.cfg.has_forecast = 0;   // no forecast handle: trajectory_cost is 0 (:239-240)
+    c.forecast = wrench6;
+    c.forecast_rows = wrench6 ? 1 : 0;
+    c.reset(0.0);
+    out8[0] = c.get_cost(x, o->d, 0);
+    const orc::CostTerms &t = c.acc;
+    out8[1] = t.joint; out8[2] = t.self_collision; out8[3] = t.workspace; out8[4] = t.energy;
+    out8[5] = t.velocity; out8[6] = t.trajectory; out8[7] = t.manipulability;
+}
+
 // ---- per-step probes for the golden-vector tests ------------------------------------------
 // calculate() at (q, v) with joint torque tau_u: outputs a (12), ee position (3), arm-mount
 // position (3), frame Jacobian WORLD 6x12 row-major after the yaw overwrite (72), EE spatial
@@ -1590,6 +1750,10 @@ void oracle_kinematics(const mppi_frankaridgeback_desc *desc, const double *q, c
     for (int i = 0; i < 3; i++) out[o++] = d.ee_lin_vel[i];
     for (int i = 0; i < 3; i++) out[o++] = d.ee_ang_vel[i];
     for (int i = 0; i < 12; i++) out[o++] = n[i];
+    if (mode == 1) return;   // the minimal-arithmetic path forms no EE orientation / acceleration
+    for (int i = 0; i < 9; i++) out[o++] = d.ee_rot.a[i];
+    for (int i = 0; i < 3; i++) out[o++] = d.ee_lin_acc[i];
+    for (int i = 0; i < 3; i++) out[o++] = d.ee_ang_acc[i];
 }
 
 // One rollout of FrankaRidgeback + AssistedManipulation from x0 with controls u (H x C,

@@ -76,6 +76,15 @@ def lib(path=None):
     L.oracle_sg_weights.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, dp]
     L.oracle_default_frankaridgeback.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc)]
     L.oracle_default_assisted_manipulation.argtypes = [C.POINTER(abi.mppi_assisted_manipulation_desc)]
+    L.oracle_dyn_create.restype = vp
+    L.oracle_dyn_create.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc), dp]
+    L.oracle_dyn_destroy.argtypes = [vp]
+    L.oracle_dyn_set_state.argtypes = [vp, dp, C.c_double]
+    L.oracle_dyn_step.argtypes = [vp, dp, C.c_double, dp]
+    for n in ("oracle_dyn_get_state", "oracle_dyn_end_effector", "oracle_dyn_query"):
+        getattr(L, n).argtypes = [vp, dp]
+    L.oracle_dyn_forecast.argtypes = [vp, dp, C.c_double, C.c_double, C.c_int64, dp, dp]
+    L.oracle_cost_evaluate.argtypes = [C.POINTER(abi.mppi_cost_desc), vp, dp, dp, dp]
     L.oracle_forecast_create.restype = vp
     L.oracle_forecast_create.argtypes = [C.POINTER(abi.mppi_forecast_config), C.c_char_p, C.c_int]
     L.oracle_forecast_destroy.argtypes = [vp]
@@ -104,12 +113,13 @@ def default_cost():
 
 
 def kinematics(model, q, v, tau, mode=0):
-    """calculate() probe: dict of a, ee, arm_mount, J (6x12), v_ee (6), nle (12)."""
-    out = np.zeros(12 + 3 + 3 + 72 + 6 + 12)
+    """calculate() probe: dict of a, ee, arm_mount, J (6x12), v_ee (6), nle (12); mode 0 also the
+    EE rotation (3x3) and WORLD spatial acceleration a_ee (6)."""
+    out = np.zeros(12 + 3 + 3 + 72 + 6 + 12 + 15)
     q, v, tau = (np.ascontiguousarray(x, dtype=np.float64) for x in (q, v, tau))
     lib().oracle_kinematics(C.byref(model), _p(q), _p(v), _p(tau), mode, _p(out))
     return dict(a=out[:12], ee=out[12:15], arm_mount=out[15:18], J=out[18:90].reshape(6, 12),
-                v_ee=out[90:96], nle=out[96:108])
+                v_ee=out[90:96], nle=out[96:108], R_ee=out[108:117].reshape(3, 3), a_ee=out[117:123])
 
 
 def rollout(model, cost, x0, u_HxC, dt, t0=0.0, forecast=None, scalar=0, mode=0):
@@ -244,6 +254,66 @@ class OracleTrajectory:
 
     def update_duration(self):
         return self._L.oracle_update_duration(self._h)
+
+
+class OracleDynamics:
+    """FrankaRidgeback::PinocchioDynamics as an object (pinocchio_dynamics.cpp:84-260), restated:
+    the checker of the engine's mppi_dynamics_* (tests/test_gpu_dynamics.py)."""
+
+    def __init__(self, initial_state, model=None):
+        self._L = lib()
+        self._model = model if model is not None else default_model()
+        x = np.ascontiguousarray(initial_state, dtype=np.float64)
+        self._h = self._L.oracle_dyn_create(C.byref(self._model), _p(x))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.oracle_dyn_destroy(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_state(self, x, time):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        self._L.oracle_dyn_set_state(self._h, _p(x), float(time))
+
+    def step(self, u, dt):
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        out = np.zeros(abi.MPPI_FR_STATE)
+        self._L.oracle_dyn_step(self._h, _p(u), float(dt), _p(out))
+        return out
+
+    def get_state(self):
+        out = np.zeros(abi.MPPI_FR_STATE)
+        self._L.oracle_dyn_get_state(self._h, _p(out))
+        return out
+
+    def end_effector(self):
+        out = np.zeros(abi.MPPI_EE_N)
+        self._L.oracle_dyn_end_effector(self._h, _p(out))
+        return out
+
+    def query(self):
+        out = np.zeros(abi.MPPI_DYNAMICS_QUERY_N)
+        self._L.oracle_dyn_query(self._h, _p(out))
+        return out
+
+    def forecast_rows(self, x, time, time_step, steps, wrench=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.zeros((int(steps), abi.MPPI_DF_N))
+        w = None if wrench is None else np.ascontiguousarray(wrench, dtype=np.float64)
+        self._L.oracle_dyn_forecast(self._h, _p(x), float(time), float(time_step), int(steps),
+                                    None if w is None else _p(w), _p(out))
+        return out
+
+    def evaluate_cost(self, cost_desc, x, wrench=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        w = None if wrench is None else np.ascontiguousarray(wrench, dtype=np.float64)
+        out = np.zeros(8)
+        self._L.oracle_cost_evaluate(C.byref(cost_desc), self._h, _p(x), None if w is None else _p(w), _p(out))
+        return out[0], out[1:]
 
 
 class OracleForecast:

@@ -211,6 +211,61 @@ class Robot:
         return J
 
 
+def world_jacobian_any(rob, q, link):
+    """world_jacobian for real or complex q (link_pose_any)."""
+    _, axes = rob.link_pose_any(q, link)
+    J = np.zeros((6, len(rob.dof)), dtype=np.complex128 if np.iscomplexobj(q) else np.float64)
+    for jn, (a, o, t) in axes.items():
+        k = rob.dof.index(jn)
+        if t == "revolute":
+            J[:3, k] = np.cross(o, a)
+            J[3:, k] = a
+        else:
+            J[:3, k] = a
+    return J
+
+
+def ee_acceleration(rob, q, v, a, link, h=1e-20):
+    """Spatial acceleration at the world origin (what Pinocchio's getFrameAcceleration(WORLD)
+    returns: the time derivative of the WORLD spatial velocity J(q) v) along q(t) = q + v t,
+    v(t) = v + a t, by complex-step differentiation in t: Im(J(q + i h v)(v + i h a)) / h =
+    Jdot v + J a, exact to rounding, no RNEA."""
+    return (world_jacobian_any(rob, q + 1j * h * v, link) @ (v + 1j * h * a)).imag / h
+
+
+def quaternion_xyzw(R):
+    """A unit quaternion (x, y, z, w) of R with w >= 0 (Shoemake's, independent of Eigen's branch
+    order; compared up to sign)."""
+    w = math.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    x = math.sqrt(max(0.0, 1.0 + R[0, 0] - R[1, 1] - R[2, 2])) / 2
+    y = math.sqrt(max(0.0, 1.0 - R[0, 0] + R[1, 1] - R[2, 2])) / 2
+    z = math.sqrt(max(0.0, 1.0 - R[0, 0] - R[1, 1] + R[2, 2])) / 2
+    x = math.copysign(x, R[2, 1] - R[1, 2])
+    y = math.copysign(y, R[0, 2] - R[2, 0])
+    z = math.copysign(z, R[1, 0] - R[0, 1])
+    return np.array([x, y, z, w])
+
+
+def gen_end_effector(rob, n=24, seed=7):
+    """EndEffectorState fixtures beyond kinematics.npz: the EE orientation (matrix and quaternion)
+    and its WORLD spatial acceleration, at random (q, v) with qdd = M^-1 tau."""
+    rng = np.random.default_rng(seed)
+    x0 = huddled()
+    qs, vs, taus, outs = [], [], [], []
+    for i in range(n):
+        q = x0[:12] + rng.normal(0, 0.6, 12) * (1 if i else 0)
+        q[10:] = np.abs(q[10:]) * 0.05 + 0.01
+        v = rng.normal(0, 1.0, 12)
+        tau = rng.normal(0, 5.0, 12)
+        a = np.linalg.solve(rob.mass_matrix(q), tau)
+        T = rob.frame(q, EE_LINK)
+        R = T[:3, :3]
+        A = ee_acceleration(rob, q, v, a, EE_LINK)
+        qs.append(q); vs.append(v); taus.append(tau)
+        outs.append(np.concatenate([R.reshape(-1), quaternion_xyzw(R), A, a]))
+    return np.array(qs), np.array(vs), np.array(taus), np.array(outs)
+
+
 def fd_world_velocity(rob, q, v, link, h=1e-6):
     """Spatial velocity at the world origin from finite differences of the link pose."""
     T1 = rob.frame(q - h * v, link)
@@ -698,6 +753,12 @@ def main():
         np.savez_compressed(os.path.join(HERE, "update_s16_h8_energy.npz"),
                             **gen_updates(rob, 16, 4, 8, 4, seed=24, energy0=15.0))
         if "--energy" in sys.argv:
+            return
+    if "--ee" in sys.argv or not os.path.exists(os.path.join(HERE, "end_effector.npz")):
+        print("end-effector orientation / acceleration fixtures (complex step)")
+        q, v, tau, out = gen_end_effector(rob)
+        np.savez_compressed(os.path.join(HERE, "end_effector.npz"), q=q, v=v, tau=tau, out=out)
+        if "--ee" in sys.argv:
             return
     print("kinematics fixtures")
     q, v, tau, out = gen_kinematics(rob)

@@ -1,0 +1,152 @@
+"""GPU parity at BASELINE.json's larger workloads, on one GPU, and in the bench's own mode.
+
+- the bench's exact mode at configs[2] (4096 x 64): device Philox, the next update's draws made
+  ahead (tail draws in the rollout launch + rank_draw_kernel behind the publish), the objective
+  in the launch, the previous filter() folded in as a row, keep-best 20, t = 0.05 j; the device's
+  draws are replayed through the oracle (reference draw order, mppi.cpp:242-262);
+- configs[3]'s total (32768 x 64) on one handle against the oracle, and as eight shards of the
+  phase-split ABI (host all-reduces) against the unsharded handle;
+- configs[4]'s per-GPU (8192 x 128) and total (65536 x 128) workloads with the Savitzky-Golay
+  filter (window 10, order 1) against the oracle (mppi.cpp:344-448, filter.cpp:35-110).
+Past one round of workgroups the engine switches paths (one-wave workgroups, fr_step_cost_kernel,
+the large-R softmin launches, the chunk + merge rank, sg_finish_kernel's LDS windows at H = 128):
+these sizes are where those run.  The oracle runs with 16 threads (the GPU box's CPU share).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import assistedmanipulation_amd as am
+from assistedmanipulation_amd import abi
+from oracle import oracle as O
+
+from helpers import assert_update_parity, fr_pair, replay_device_draws, step_both
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+def test_bench_mode_replay_4096x64():
+    """bench.py's update loop exactly (configs[2]), checked against the oracle on the device's own
+    draws for four updates; the launch-mode flags show the bench's path was the one taken."""
+    conf = am.frankaridgeback_configuration(rollouts=4096, horison=0.64, keep_best_rollouts=20, threads=THREADS)
+    dev = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    dev.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    table = am.constant_forecast(dev.H)
+    dev.set_forecast(table)
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, dev.dynamics.descriptor(), dev.cost.descriptor())
+    orc.set_forecast(table)
+    x = am.huddled_state()
+    prev_costs, prev_noise = np.zeros(dev.R), np.zeros((dev.R, dev.H, dev.C))
+    stats = []
+    for j in range(4):
+        costs, noise = replay_device_draws(dev, orc, x, 0.05 * j, prev_costs, prev_noise, 20)
+        info = dev.update_info()
+        assert info["cooperative"] == 1 and info["objective_in_launch"] == 1
+        if j > 0:   # drawn ahead behind the previous publish + in the previous launch's tail
+            assert info["sampling"] == 2 and info["tail_draws"] == 1 and info["folded_filter"] == 1, info
+        # the optimal cost is not read between updates (reading it would run filter() by itself
+        # and the next launch would not fold it, as bench.py's loop does)
+        assert_update_parity(dev, orc, "bench mode upd %d" % j, stats=stats, check_optimal=(j == 3))
+        prev_costs, prev_noise = costs, noise
+    print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
+
+
+def test_config3_total_unsharded_32768x64():
+    """configs[3]'s 32768 x 64 on one handle: one-wave workgroups, fr_step_cost_kernel, the
+    large-R softmin (R > 16384) and the chunk + merge rank (S > 8192)."""
+    conf, dev, orc, sd = fr_pair(S=32768, horison=0.64, threads=THREADS)
+    rng = np.random.default_rng(33)
+    x = am.huddled_state()
+    stats = []
+    for j in range(3):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert dev.update_info()["objective_in_launch"] == 0
+        assert_update_parity(dev, orc, "32768x64 upd %d" % j, stats=stats)
+    print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
+
+
+def _hip():
+    L = C.CDLL("libamdhip64.so.7")
+    L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    L.hipDeviceSynchronize.argtypes = []
+    return L
+
+
+def test_config3_eight_shards_equal_unsharded():
+    """configs[3]'s partition on one GPU: eight phase-split handles of 4096 or 4097
+    rollouts each (the reference's ThreadPool split, mppi.cpp:277-302), with the two all-reduces
+    done on the host between the phases, against one handle of all 32770 rollouts (device Philox:
+    draws are keyed by global rollout, so every rank draws what the single handle draws)."""
+    conf = am.frankaridgeback_configuration(rollouts=32768, horison=0.64, keep_best_rollouts=20, threads=8)
+    mk = lambda: am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    world = 8
+    single, shards = mk(), [mk() for _ in range(world)]
+    for r, t in enumerate([single] + shards):
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        if t is not single:
+            t.set_shard(world, r - 1)
+    hip = _hip()
+    R, HC = single.R, single.H * single.C
+    x = am.huddled_state()
+
+    def allreduce(ptrs, n):
+        bufs = [np.zeros(n) for _ in ptrs]
+        for p, b in zip(ptrs, bufs):
+            assert hip.hipMemcpy(b.ctypes.data, p, n * 8, 2) == 0   # D2H
+        s = bufs[0].copy()
+        for b in bufs[1:]:
+            s += b
+        for p in ptrs:
+            assert hip.hipMemcpy(p, s.ctypes.data, n * 8, 1) == 0   # H2D
+
+    for j in range(3):
+        t = 0.05 * j
+        single.update(x, t)
+        for sh in shards:
+            sh.update_phase1(x, t)
+        hip.hipDeviceSynchronize()
+        allreduce([sh.device_costs_ptr() for sh in shards], R)
+        for sh in shards:
+            sh.update_phase2()
+        hip.hipDeviceSynchronize()
+        allreduce([sh.device_gradient_ptr() for sh in shards], HC)
+        for sh in shards:
+            sh.update_phase3(t)
+        full = single.noise()
+        for r, sh in enumerate(shards):
+            b, e = am.shard_range(R, world, r)
+            mine, ref = sh.noise()[b:e], full[b:e]
+            d = max(2 - b, 0)   # rollout 1 carries -U*, which differs in the last bits (gradient order)
+            np.testing.assert_array_equal(mine[d:], ref[d:], err_msg="update %d shard %d noise" % (j, r))
+            np.testing.assert_allclose(mine[:d], ref[:d], rtol=0, atol=1e-12)
+            if j > 0:   # 4096-4097 rollouts per shard: one round of workgroups, draws ahead
+                assert sh.update_info()["sampling"] == 2
+        for sh in shards:
+            np.testing.assert_allclose(sh.costs(), single.costs(), rtol=1e-13, atol=0)
+            np.testing.assert_allclose(sh.get_optimal_rollout(), single.get_optimal_rollout(), rtol=0, atol=1e-12)
+            np.testing.assert_allclose(sh.get_weights(), single.get_weights(), rtol=0, atol=1e-15)
+            assert sh.argmin() == single.argmin()
+
+
+@pytest.mark.parametrize("S,updates", [(8192, 3), (65536, 2)])
+def test_config4_savitzky_golay_h128(S, updates):
+    """configs[4]: H = 128 with the Savitzky-Golay filter (window 10, order 1) fused into the
+    finish launch (sg_finish_kernel); 8192 is its per-GPU share at N = 8, 65536 its total."""
+    conf, dev, orc, sd = fr_pair(S=S, horison=1.28, smoothing=am.Smoothing(10, 1), threads=THREADS)
+    rng = np.random.default_rng(S)
+    x = am.huddled_state()
+    stats = []
+    for j in range(updates):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert_update_parity(dev, orc, "%dx128 SG upd %d" % (S, j), stats=stats)
+    uu_d, tt_d, st_d = dev.smoothing_windows()
+    uu_o, tt_o, st_o = orc.smoothing_windows(10)
+    np.testing.assert_array_equal(tt_d, tt_o)
+    np.testing.assert_array_equal(st_d, st_o)
+    np.testing.assert_allclose(uu_d, uu_o, rtol=0, atol=1e-9)
+    print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)

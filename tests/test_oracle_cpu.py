@@ -188,3 +188,80 @@ def test_fp32_dynamics_diverge_fp64_do_not(model):
         worst32 = max(worst32, np.nanmax(np.abs(trajs[2].costs() - ref)) / span)
     assert worst64 < 1e-12
     assert worst32 > 1e-3
+
+
+@pytest.mark.parametrize("self_collision", [1, 0])
+def test_operation_orders_delta(model, self_collision):
+    """The scale of tests/helpers.py COST_DFRAC: the oracle's two fp64 operation orders (Pinocchio-
+    order RNEA + ABA, mode 0, and the device's world-frame zero-bias ABA, mode 1) over three 1024 x
+    64 updates, with the default stack and with the constant self-collision term off (then the costs
+    are the state-dependent terms and the barrier jumps).  Measured at 4096 x 64 (same seeds): cost
+    error <= 2.6e-13 of Delta, relative <= 1.6e-12 of the small costs."""
+    from helpers import cost_errors
+    conf = am.frankaridgeback_configuration(rollouts=1024, horison=0.64, threads=8)
+    cc, keep = conf.to_c()
+    cost = am.AssistedManipulation()
+    cost.configuration.enable_self_collision_limit = self_collision
+    d, c = am.FrankaRidgebackDynamics().descriptor(), cost.descriptor()
+    a, b = (O.OracleTrajectory(cc, d, c, mode=m) for m in (0, 1))
+    for t in (a, b):
+        t.set_forecast(am.constant_forecast(t.H))
+    rng = np.random.default_rng(7)
+    sd = np.sqrt(np.diag(conf.covariance))
+    x = am.huddled_state()
+    for j in range(3):
+        eps = rng.standard_normal((a.noise_draws(0.05 * j), 12)) * sd
+        for t in (a, b):
+            t.inject_noise(eps)
+            t.update(x, 0.05 * j)
+        rel, dfrac, sfrac, worst = cost_errors(b.costs(), a.costs(), a.H)
+        assert dfrac < 1e-12 and sfrac < 1e-12 and worst < 0.1, (j, dfrac, sfrac, worst)
+        assert rel < 1e-11, (j, rel)
+        if not self_collision:   # the small costs are the state-dependent terms, not 1.3e13 + terms
+            assert np.nanmin(a.costs()) < 1e6
+
+
+def test_end_effector_orientation_and_acceleration(model):
+    """The EndEffectorState members DynamicsForecast records beyond kinematics.npz (dynamics.cpp:
+    115-116): the EE orientation and its WORLD spatial acceleration (Pinocchio's forward pass,
+    pinocchio_dynamics.cpp:174-223) against the numpy model's rotation and the complex-step time
+    derivative of its J(q) v along (v, a) (tests/golden/gen_golden.py ee_acceleration)."""
+    g = load("end_effector.npz")
+    for q, v, tau, out in zip(g["q"], g["v"], g["tau"], g["out"]):
+        k = O.kinematics(model, q, v, tau, 0)
+        np.testing.assert_allclose(k["a"], out[19:31], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(k["R_ee"], out[:9].reshape(3, 3), rtol=0, atol=1e-13)
+        scale = max(1.0, np.abs(out[13:19]).max())
+        np.testing.assert_allclose(k["a_ee"], out[13:19], rtol=0, atol=1e-9 * scale)
+
+
+def test_dynamics_object_quaternion_and_quirks(model):
+    """The object API (oracle_dyn_*): Eigen's quaternion of the EE rotation (equal to the numpy
+    one up to sign), a step's state, and set_state's stale-torque acceleration (after a
+    step the torque holds tau_u + NLE, and the next set_state adds NLE(q0, v0) on top)."""
+    g = load("end_effector.npz")
+    x0 = am.huddled_state()
+    d = O.OracleDynamics(x0, model)
+    ee = d.end_effector()
+    q = O.kinematics(model, x0[:12], x0[12:24], np.zeros(12), 0)
+    R = q["R_ee"]
+    np.testing.assert_allclose(ee[7:16].reshape(3, 3), R, rtol=0, atol=0)
+    quat = ee[3:7]
+    assert abs(np.linalg.norm(quat) - 1.0) < 1e-14
+    qn = g["out"][0][9:13]   # state 0 of the fixture is HUDDLED
+    np.testing.assert_allclose(quat * np.sign(quat[3]), qn * np.sign(qn[3]), rtol=0, atol=1e-14)
+    np.testing.assert_allclose(ee[28:].reshape(6, 12)[:, 3:10], q["J"][:, 3:10], rtol=0, atol=0)
+    # the constructor's set_state leaves tau = NLE(x0); a first step() zeroes it (:237)
+    qa = d.query()
+    np.testing.assert_allclose(qa[36:48], O.kinematics(model, x0[:12], x0[12:24], np.zeros(12), 0)["nle"], rtol=1e-12)
+    assert np.abs(qa[24:36]).max() < 1e-9   # a = M^-1 (0 + NLE - NLE)
+    u = np.zeros(12)
+    u[3:10] = np.linspace(-3, 3, 7)
+    x1 = d.step(u, 0.01)
+    assert np.all(np.isfinite(x1)) and x1[30] != x0[30]
+    tau_after = d.query()[36:48]
+    d.set_state(x1, 0.01)   # stale torque: a = M^-1 tau_after (not zero)
+    a = d.query()[24:36]
+    assert np.abs(a).max() > 1e-3
+    k = O.kinematics(model, x1[:12], x1[12:24], tau_after, 0)
+    np.testing.assert_allclose(a, k["a"], rtol=1e-9, atol=1e-9)
