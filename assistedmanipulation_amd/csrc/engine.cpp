@@ -164,6 +164,23 @@ struct mppi_handle {
     double *h_opt = nullptr;     // pinned: optimal cost copied back on the side stream
     std::vector<void *> allocations;
     std::string err;
+    // hipGraph path (mppi_set_graph / MPPI_GRAPH=1): the steady-state update's four launches
+    // (rollout, weights + gradient, finish, rank + draws ahead) captured once and replayed with each
+    // update's arguments written into the executable graph's kernel nodes
+    int graph_mode = 0;
+    bool graph_dry = false;             // phases fill `gargs` instead of launching
+    struct GraphArgs {
+        FrRolloutArgs roll;
+        WGradArgs wg;
+        FinishArgs fin;
+        RankDrawLaunch rd;
+        bool x_kernel = false, folded = false;
+    } gargs;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    hipGraphNode_t gnode[4] = {};
+    hipKernelNodeParams gparams[4] = {};
+    int64_t graph_updates = 0;          // updates that ran as the graph (diagnostics)
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -838,6 +855,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     {
         const char *e = getenv("MPPI_HOST_TRACE");
         h->host_trace = e && e[0] == '1';
+        const char *g = getenv("MPPI_GRAPH");   // the hipGraph path by default (mppi_set_graph)
+        h->graph_mode = g && g[0] == '1' ? 1 : 0;
     }
     h->device = device;
     h->dyn_kind = dyn->kind;
@@ -1031,6 +1050,8 @@ void mppi_destroy(mppi_handle *h)
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
     if (h->comm) ncclCommDestroy(h->comm);
+    if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+    if (h->graph) (void)hipGraphDestroy(h->graph);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->h_opt) (void)hipHostFree(h->h_opt);
@@ -1562,10 +1583,11 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
-                                          &folded, &costs_done, &tail));
+                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry));
+            h->gargs.folded = folded;
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
-            if (!costs_done) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+            if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream));
             if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
@@ -1672,20 +1694,23 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.wexp = h->d_wexp;
     w.wpart = h->d_wpart;
     w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
+    h->gargs.wg = w;
+    if (h->graph_dry) return MPPI_OK;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_weights_gradient(w, h->d_gpart, h->world > 1, h->stream));
     return MPPI_OK;
 }
 
-mppi_status mppi_update_phase3(mppi_handle *h)
+// Phase 3's launches (finish, filter() bookkeeping, rank + draws ahead); *seq: the sequence the
+// finish kernel publishes.  With graph_dry the arguments go to gargs and nothing is launched.
+static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
 {
-    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
-    HIP_TRY(hipSetDevice(h->device));
-    const int HC = (int)(h->H * h->C);
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
-    HIP_TRY(launch_finish(finish_args(h), h->stream));
+    h->gargs.fin = finish_args(h);
+    if (!h->graph_dry) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
     const double seq = (double)(++h->publish_seq);
+    *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     const bool standalone_filter = !(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h));
     if (standalone_filter) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));   // the side stream waits on it
@@ -1715,11 +1740,20 @@ mppi_status mppi_update_phase3(mppi_handle *h)
         sa.H = (int)h->H;
         sa.C = (int)h->C;
         for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
-        if (h->tail_drawn) HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, h->tail_nxb, h->tail_xbase));
-        else HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
+        if (h->tail_drawn)
+            HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, h->tail_nxb, h->tail_xbase,
+                                      &h->gargs.rd, h->graph_dry));
+        else HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, 0, 0, &h->gargs.rd, h->graph_dry));
         h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
         h->ahead_valid = true;
     }
+    return MPPI_OK;
+}
+
+// Phase 3's wait for the published block (sequence `seq`) and the host's bookkeeping.
+static mppi_status phase3_wait(mppi_handle *h, double seq)
+{
+    const int HC = (int)(h->H * h->C);
     // wait for the published block by polling its sequence flag (finish kernels, publish_block): a
     // blocking synchronize sleeps the thread and the wake-up sat on the update's critical path, and
     // an event behind the finish kernel delayed the stream.  The stream is queried now and then so
@@ -1781,8 +1815,129 @@ mppi_status mppi_update_phase3(mppi_handle *h)
     return MPPI_OK;
 }
 
+mppi_status mppi_update_phase3(mppi_handle *h)
+{
+    if (!h || !h->phase_open) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    double seq = 0.0;
+    mppi_status st = phase3_launch(h, &seq);
+    if (st != MPPI_OK) return st;
+    return phase3_wait(h, seq);
+}
+
+// The hipGraph path: the steady-state update (FrankaRidgeback on the cooperative kernel, device
+// Philox with the draws made ahead, the previous filter() folded into the rollout launch, the
+// objective and the next draws in its tail, no smoothing, no device forecast, one device) is the
+// chain rollout -> weights + gradient -> finish -> rank + draws ahead.  It is captured from the
+// first such update's launches; later updates write their arguments (the same structs the eager
+// launches take: state and shift by value, the swapped eps buffers, the update index, the publish
+// sequence) into the executable graph's four kernel nodes and launch it once.  Anything else runs
+// the eager launches.
+static bool graph_eligible(const mppi_handle *h)
+{
+    if (!h->graph_mode || h->world != 1 || h->timing != 0 || h->d_trace || h->host_trace) return false;
+    if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
+    if (h->fc.type != FC_NONE || h->sg_window > 0 || h->S > RANK_TILED_MAX) return false;
+    if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
+    return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
+           h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
+}
+
+static mppi_status graph_nodes(mppi_handle *h)
+{
+    size_t n = 0;
+    HIP_TRY(hipGraphGetNodes(h->graph, nullptr, &n));
+    if (n != 4) return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(n) + " nodes, expected 4");
+    hipGraphNode_t nodes[4];
+    HIP_TRY(hipGraphGetNodes(h->graph, nodes, &n));
+    hipGraphNode_t cur = nullptr;
+    for (hipGraphNode_t nd : nodes) {   // the chain's root
+        size_t deps = 0;
+        HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &deps));
+        if (deps == 0) cur = nd;
+    }
+    for (int i = 0; i < 4; i++) {
+        if (!cur) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a kernel chain");
+        hipGraphNodeType ty;
+        HIP_TRY(hipGraphNodeGetType(cur, &ty));
+        if (ty != hipGraphNodeTypeKernel) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a kernel chain");
+        h->gnode[i] = cur;
+        HIP_TRY(hipGraphKernelNodeGetParams(cur, &h->gparams[i]));
+        size_t nd = 0;
+        HIP_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd));
+        if (i < 3 && nd != 1) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a chain");
+        hipGraphNode_t next = nullptr;
+        if (nd == 1) HIP_TRY(hipGraphNodeGetDependentNodes(cur, &next, &nd));
+        cur = next;
+    }
+    return MPPI_OK;
+}
+
+static mppi_status update_graph(mppi_handle *h, const double *state, double time)
+{
+    const bool capture = h->graph_exec == nullptr;
+    if (capture) HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    else h->graph_dry = true;
+    mppi_status st = mppi_update_phase1(h, state, time);
+    if (st == MPPI_OK) st = mppi_update_phase2(h);
+    double seq = 0.0;
+    if (st == MPPI_OK) st = phase3_launch(h, &seq);
+    h->graph_dry = false;
+    if (capture) {
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(h->stream, &g);
+        if (st != MPPI_OK || e != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            h->graph_mode = 0;   // never again: the eager path from here on
+            if (st != MPPI_OK) return st;
+            HIP_TRY(e);
+        }
+        h->graph = g;
+        HIP_TRY(hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0));
+        st = graph_nodes(h);
+        if (st != MPPI_OK) {
+            h->graph_mode = 0;
+            return st;
+        }
+    } else {
+        if (st != MPPI_OK) return st;
+        if (!h->gargs.x_kernel || !h->gargs.folded) return fail(h, MPPI_ERR_DEVICE, "graph update took another launch path");
+        RankDrawLaunch &rd = h->gargs.rd;
+        void *a0[] = {&h->gargs.roll};
+        void *a1[] = {&h->gargs.wg};
+        void *a2[] = {&h->gargs.fin};
+        void *a3[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase};
+        void **args[4] = {a0, a1, a2, a3};
+        for (int i = 0; i < 4; i++) {
+            hipKernelNodeParams p = h->gparams[i];
+            p.kernelParams = args[i];
+            p.extra = nullptr;
+            if (i == 3) p.gridDim = dim3(rd.grid);
+            HIP_TRY(hipGraphExecKernelNodeSetParams(h->graph_exec, h->gnode[i], &p));
+        }
+    }
+    HIP_TRY(hipGraphLaunch(h->graph_exec, h->stream));
+    h->graph_updates++;
+    return phase3_wait(h, seq);
+}
+
+mppi_status mppi_set_graph(mppi_handle *h, int enable)
+{
+    if (!h || enable < 0 || enable > 1) return MPPI_ERR_INVALID;
+    h->graph_mode = enable;
+    return MPPI_OK;
+}
+
+mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count)
+{
+    if (!h || !count) return MPPI_ERR_INVALID;
+    *count = h->graph_updates;
+    return MPPI_OK;
+}
+
 mppi_status mppi_update(mppi_handle *h, const double *state, double time)
 {
+    if (h && state && graph_eligible(h)) return update_graph(h, state, time);
     mppi_status st = mppi_update_phase1(h, state, time);
     if (st != MPPI_OK) return st;
     if (h->world > 1) {

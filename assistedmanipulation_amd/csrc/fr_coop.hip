@@ -1801,6 +1801,8 @@ static bool costs_in_launch_enabled()
     return on;
 }
 
+bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
+
 // Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample
 // their own rows, a.fuse_sample) for `count` rows.
 bool fr_coop_update_fusable(int64_t count)
@@ -1812,10 +1814,11 @@ bool fr_coop_update_fusable(int64_t count)
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
-                                 bool *costs_done, bool *tail_drawn)
+                                 bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry)
 {
     *costs_done = false;
     *tail_drawn = false;
+    if (x_kernel) *x_kernel = false;
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     *folded = false;
@@ -1828,6 +1831,8 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
         if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
+        if (final) *final = a;
+        if (dry) return hipSuccess;
         if (e0) (void)hipEventRecord(e0, s);
         const hipError_t e = launch_fr_coop(a, s);
         if (e1) (void)hipEventRecord(e1, s);
@@ -1842,6 +1847,9 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
     if (xrows == 0 || !a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
     *tail_drawn = a.ahead_noise != nullptr;
+    if (final) *final = a;
+    if (x_kernel) *x_kernel = xrows != 0;
+    if (dry) return hipSuccess;
     if (e0) (void)hipEventRecord(e0, s);
 #ifdef FORCE_X
     if (false) {}

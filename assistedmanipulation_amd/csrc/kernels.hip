@@ -662,7 +662,7 @@ __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict
 }
 
 hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                                       hipStream_t s, int sub_nxb, int64_t sub_xbase)
+                                       hipStream_t s, int sub_nxb, int64_t sub_xbase, RankDrawLaunch *out, bool dry)
 {
     if (a.C != FR_C || a.count <= 0) return hipErrorInvalidValue;
     if (sub_nxb > 0 && (16 * (int64_t)sub_nxb > sub_xbase || sub_xbase > a.count)) return hipErrorInvalidValue;
@@ -671,12 +671,15 @@ hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, 
     const unsigned nx = (unsigned)((rows * NB + 255) / 256);
     unsigned nr = (unsigned)((S + RANK_T - 1) / RANK_T);
     if (S > RANK_TILED_MAX) {   // O(S log S) rank in its own launches, then the draws alone
+        if (dry) return hipErrorInvalidValue;
         const hipError_t e = launch_rank(cost, S, rank, sorted, s);
         if (e != hipSuccess) return e;
         nr = 0;
     }
-    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(nr * nr * RANK_JS + nx * (unsigned)a.H), dim3(256), 0, s, cost, S, rank, nr, a, nx,
-                       sub_nxb, sub_xbase);
+    const unsigned grid = nr * nr * RANK_JS + nx * (unsigned)a.H;
+    if (out) *out = RankDrawLaunch{cost, S, rank, nr, nx, a, sub_nxb, sub_xbase, grid};
+    if (dry) return hipSuccess;
+    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(grid), dim3(256), 0, s, cost, S, rank, nr, a, nx, sub_nxb, sub_xbase);
     return hipGetLastError();
 }
 

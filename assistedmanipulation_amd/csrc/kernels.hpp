@@ -238,8 +238,21 @@ hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 // with the stable rank of this update's costs (one launch when S <= RANK_TILED_MAX; rank[] cleared)
 // sub_nxb > 0: the rollout launch's tail drew the rest, so only the rows it left are drawn - the
 // first wave's rows of its first sub_nxb workgroups (16 b + i, i < 4) and [sub_xbase, count).
+// The rank_draw_kernel launch's arguments (the hipGraph path updates its node with them).
+struct RankDrawLaunch {
+    const double *cost;
+    int64_t S;
+    int *rank;
+    unsigned nr, nx;
+    SampleArgs a;
+    int sub_nxb;
+    int64_t sub_xbase;
+    unsigned grid;
+};
+// dry: fill *out and launch nothing (the one-launch path only: S <= RANK_TILED_MAX)
 hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                             hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0);
+                             hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0, RankDrawLaunch *out = nullptr,
+                             bool dry = false);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
@@ -267,9 +280,13 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
 // The update's rollouts (fr_coop.hip): e0 / e1 = optional timing events around the launch.
 // *tail_drawn: the launch made the next update's draws for its main waves' rows (a.ahead_noise).
+// final (may be null): the arguments the launch used; *x_kernel: it was fr_coop_x_kernel (one round
+// of four-wave workgroups with a fifth wave); dry: decide and fill them, launch nothing.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
-                                 bool *costs_done, bool *tail_drawn);
+                                 bool *costs_done, bool *tail_drawn, FrRolloutArgs *final = nullptr, bool *x_kernel = nullptr,
+                                 bool dry = false);
 bool fr_coop_update_fusable(int64_t count);
+bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);

@@ -298,6 +298,16 @@ class Trajectory:
         self._update_last = float(time)
         self._update_count += 1
 
+    def set_graph(self, enable):
+        """The hipGraph path of update() (mppi_set_graph): the steady-state update as one graph launch."""
+        self._check(self._L.mppi_set_graph(self._h, int(bool(enable))))
+
+    def graph_updates(self):
+        """How many updates ran as the captured graph (mppi_graph_updates)."""
+        n = C.c_int64()
+        self._check(self._L.mppi_graph_updates(self._h, C.byref(n)))
+        return n.value
+
     def synchronize(self):
         """Wait for all device work of this handle (including the overlapped filter())."""
         self._check(self._L.mppi_synchronize(self._h))

@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the CPU baseline (0: the CPU share this process may use)")
     p.add_argument("--cpu-updates", type=int, default=20, help="timed CPU updates (median / p90)")
+    p.add_argument("--graph", type=int, default=-1,
+                   help="1: the hipGraph update path (mppi_set_graph), 0: eager launches, -1: the engine's default")
     a = p.parse_args()
     pm = a.workload == "point_mass"
     if a.samples_per_gpu is None:
@@ -188,6 +190,8 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         traj.comm_init(world, rank, uid[0])
     traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    if args.graph >= 0:
+        traj.set_graph(args.graph)
     if not pm:
         traj.set_forecast(am.constant_forecast(traj.H))
     traj.set_timing(1)   # creates the engine's timing-event ring outside the timed region
@@ -208,6 +212,7 @@ def main():
     # vary, so a sample of the launches gives its average).  The engine keeps the event pairs and
     # they are read after the timed region (mppi_rollout_kernel_times).
     traj.rollout_kernel_times()    # clear the record
+    g0 = traj.graph_updates()
     t0 = time.perf_counter()
     for i in range(args.steps):
         sampled = i % EV_EVERY == 0
@@ -221,6 +226,7 @@ def main():
     elapsed = time.perf_counter() - t0
     dyn_times = traj.rollout_kernel_times()   # the rollout kernel's HIP-event times, sampled updates
     info = traj.update_info()      # what the engine's rollout launch did (its own choice, not re-derived)
+    info["graph_updates_timed"] = traj.graph_updates() - g0   # updates of the timed loop that ran as the hipGraph
     dyn_ms = sum(dyn_times) / max(len(dyn_times), 1)
     # the per-phase breakdown from a few further updates with every event recorded (untimed)
     traj.set_timing(2)

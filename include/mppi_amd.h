@@ -323,6 +323,14 @@ mppi_status mppi_step_constants(mppi_handle *h, double *out_Hx8);
  * publish.  Blocks until the update is complete on the device. */
 mppi_status mppi_update(mppi_handle *h, const double *state, double time);
 
+/* hipGraph path of mppi_update (default off; MPPI_GRAPH=1 at create turns it on): the steady-state
+ * update's four launches (rollout, weights + gradient, finish, rank + draws ahead) are captured
+ * once and replayed as one graph launch with each update's arguments written into its kernel
+ * nodes.  Updates outside that configuration run the eager launches.  mppi_graph_updates counts
+ * the updates that ran as the graph. */
+mppi_status mppi_set_graph(mppi_handle *h, int enable);
+mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count);
+
 /* Phase-split update for callers that run the collectives themselves (multi-GPU with an
  * external communicator, or two shards on one device in tests).  Between phase 1 and 2 the
  * caller all-reduces (sum) mppi_device_costs(h); between phase 2 and 3 it all-reduces (sum)

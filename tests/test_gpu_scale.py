@@ -150,3 +150,37 @@ def test_config4_savitzky_golay_h128(S, updates):
     np.testing.assert_array_equal(st_d, st_o)
     np.testing.assert_allclose(uu_d, uu_o, rtol=0, atol=1e-9)
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
+
+
+@pytest.mark.parametrize("rollouts", [4096, 1000])
+def test_graph_path_equals_eager_launches(rollouts):
+    """The hipGraph path of update() (mppi_set_graph: the steady-state update captured once and
+    replayed with each update's arguments written into its kernel nodes) gives the eager launches'
+    bits over updates with varying shifts (5, 2, 5, 0 steps), including a state change and an
+    interruption (reading the optimal cost runs filter() by itself, so the next update is eager)."""
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.64, keep_best_rollouts=20, threads=8)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17, 0.22, 0.27, 0.32]
+    out = {}
+    for graph in (0, 1):
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.set_graph(graph)
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for j, tm in enumerate(times):
+            if j == 5:
+                x = x.copy()
+                x[12 + 4] = 0.3
+            t.update(x, tm)
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+            if j == 6:
+                rec.append(t.get_optimal_total_cost())
+        out[graph] = (rec, t.graph_updates())
+    assert out[0][1] == 0 and out[1][1] >= 5, out[1][1]
+    for j, (a, b) in enumerate(zip(out[0][0], out[1][0])):
+        if isinstance(a, float):
+            assert a == b
+            continue
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))

@@ -265,3 +265,17 @@ def test_dynamics_object_quaternion_and_quirks(model):
     assert np.abs(a).max() > 1e-3
     k = O.kinematics(model, x1[:12], x1[12:24], tau_after, 0)
     np.testing.assert_allclose(a, k["a"], rtol=1e-9, atol=1e-9)
+
+
+def test_oracle_under_sanitizers():
+    """SURVEY §5 (race detection / sanitizers; the reference builds with -Wall only,
+    src/CMakeLists.txt:8): the oracle and a driver of every C-API path the tests use, built with
+    -fsanitize=address,undefined -fno-sanitize-recover=all (oracle/Makefile `sanitize`), run to a
+    clean exit: no out-of-bounds access, use-after-free, leak or undefined behaviour."""
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.check_call(["make", "-s", "-C", here, "sanitize"], timeout=600)
+    out = subprocess.run([os.path.join(here, "build-san", "sanitize_check")], capture_output=True, timeout=600)
+    assert out.returncode == 0, out.stderr.decode()[-4000:]
+    assert b"sanitize_check: ok" in out.stdout
+    assert b"runtime error" not in out.stderr and b"AddressSanitizer" not in out.stderr
