@@ -855,7 +855,9 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     {
         const char *e = getenv("MPPI_HOST_TRACE");
         h->host_trace = e && e[0] == '1';
-        const char *g = getenv("MPPI_GRAPH");   // the hipGraph path by default (mppi_set_graph)
+        // the hipGraph path (mppi_set_graph) is opt-in: at 4096 x 64 it measured 0.2895 ms/update
+        // against 0.2820 with eager launches (same box, profiles/r03_graph_ab/)
+        const char *g = getenv("MPPI_GRAPH");
         h->graph_mode = g && g[0] == '1' ? 1 : 0;
     }
     h->device = device;
@@ -1599,6 +1601,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         h->info[MPPI_INFO_TAIL_DRAWS] = tail ? 1 : 0;
         h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : (fuse ? 1 : 0);
         h->info[MPPI_INFO_ROWS] = h->count + (folded ? 1 : 0);
+        h->info[MPPI_INFO_HANDOVER] = h->gargs.x_kernel ? -2 : -1;   // -2: read from the device on request
         if (tail) {   // the rows the tail left: the fifth wave's and its SIMD-mate's (fr_coop.hip)
             constexpr int64_t WG_ROWS = 16;
             const int64_t groups = h->count / WG_ROWS;
@@ -2106,6 +2109,12 @@ mppi_status mppi_noise(mppi_handle *h, double *out)
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
 {
     if (!h || !info || n < 0 || n > MPPI_UPDATE_INFO_N) return MPPI_ERR_INVALID;
+    if (n > MPPI_INFO_HANDOVER && h->info[MPPI_INFO_HANDOVER] == -2) {   // the x kernel's Status word
+        int step = -1;
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipMemcpy(&step, &h->d_status->handover, sizeof(int), hipMemcpyDeviceToHost));
+        h->info[MPPI_INFO_HANDOVER] = step;
+    }
     std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;
 }

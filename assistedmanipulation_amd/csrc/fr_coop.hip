@@ -1238,13 +1238,19 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // costs are not summed here: every step's record goes to HBM and fr_step_cost_kernel evaluates
 // the objective for all (rollout, step) pairs at once, a lane each, instead of 16 lanes of a row
 // repeating its row-uniform terms.
-template <int CK, bool EN, bool FROW>
-__device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
-                                          const double *Lmodel, const double *Lx0)
+// HO (handover, fr_coop_x_kernel): 1 = the fifth wave, which checks Lho[HO_REQ] at the top of each
+// step and, once another wave asks, leaves its lanes' (q, qd, E) in Lst and the step in
+// Lho[HO_STEP] and returns that step; 2 = the wave that took them over, resuming at that step (the
+// records up to it are stored).  Returns the step handed over, or -1.
+enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_N = 5 };
+template <int CK, bool EN, bool FROW, int HO = 0>
+__device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
+                                         const double *Lmodel, const double *Lx0, int *Lho = nullptr,
+                                         double *Lst = nullptr)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
-    if (a.trace && lane == 0) {
+    if (a.trace && lane == 0 && HO != 2) {
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -1258,7 +1264,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // FROW: the row after the last rollout is the previous update's filter() (optimal rollout)
     const bool frow = FROW && a.fcost != nullptr && lr == a.count;
     const bool live = lr < a.count || frow;
-    if (!live) return;   // row-uniform: the row's lanes leave together (no DPP partner is lost)
+    if (!live) return -1;   // row-uniform: the row's lanes leave together (no DPP partner is lost)
     const int H = a.H;
     const bool opt_row = a.optimal || frow;   // no noise (mppi.cpp:450-479)
     // U*_shifted row k is Up row min(k + ush, H - 1): with fused sampling (a.fuse_sample) the
@@ -1301,16 +1307,26 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
     L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
 
-    double q = jl ? x0p[jb] : 0.0;
-    double qd = jl ? x0p[FR_NB + jb] : 0.0;
-    double E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+    double q, qd, E;
+    int kb = 0;   // first step of this call
+    if constexpr (HO == 2) {   // the state the fifth wave left at the top of step kb
+        kb = Lho[HO_STEP];
+        q = Lst[3 * lane];
+        qd = Lst[3 * lane + 1];
+        E = Lst[3 * lane + 2];
+    } else {
+        q = jl ? x0p[jb] : 0.0;
+        qd = jl ? x0p[FR_NB + jb] : 0.0;
+        E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+    }
     const double *grav = a.model->gravity;
     double sq, cq;
     const SinCosK scK = sincos_constants();
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
-    coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
+    if constexpr (HO != 2)
+        coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step
     const bool sampled = !opt_row && jl;
@@ -1329,8 +1345,8 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     // whose latency a single wave per SIMD cannot hide within one step
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
-    double eps_n = np[0], ub_n = Up[min(ush, H - 1) * FR_C + jb];
-    store_record(recp(0), j, L, q, qd, kin, E);
+    double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
+    if constexpr (HO != 2) store_record(recp(0), j, L, q, qd, kin, E);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
 #endif
@@ -1338,10 +1354,21 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
     uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
     uint64_t t_top = stamp(sq);
 #endif
-    for (int k = 0; k < H - 1; k++) {
+    int req = 0;   // HO == 1: Lho[HO_REQ] as read during the previous step
+    for (int k = kb; k < H - 1; k++) {
+        if constexpr (HO == 1) {
+            if (__builtin_amdgcn_readfirstlane(req)) {   // another wave resumes these rows at step k
+                Lst[3 * lane] = q;
+                Lst[3 * lane + 1] = qd;
+                Lst[3 * lane + 2] = E;
+                Lho[HO_STEP] = k;
+                return k;
+            }
+        }
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
+        if constexpr (HO == 1) req = __hip_atomic_load(Lho + HO_REQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
         // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
@@ -1422,6 +1449,7 @@ __device__ __forceinline__ void coop_rows(const FrRolloutArgs &a, int64_t lr, in
 #ifdef COOP_TRACE
     if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
+    return -1;
 }
 
 // ---- the objective inside the launch (a.costs_in_launch) ----------------------------------------
@@ -1493,29 +1521,64 @@ __device__ __forceinline__ void tail_draws(const FrRolloutArgs &a, int64_t lr0, 
 }
 
 // Main wave wv (0..3) of the workgroup after its horizon loop.  xr: the workgroup's fifth wave has
-// rows (its SIMD-mate, wave 0, then only signals).
+// rows.  Wave 0 (the fifth wave's SIMD-mate) signals its records stored; then every main wave takes
+// the doubled SIMD's rows one at a time from the counter Lho[HO_COST] (wave 0's four, then the
+// fifth wave's), each once its records are stored.
 template <int CK, bool EN>
 __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
-                                             bool xr)
+                                             int *Lho, bool xr)
 {
+    const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
     if (xr && wv == 0) {
         signal_records(Lflag);
-        return;
+    } else {
+        __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+        for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
+        if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
+        if (!xr) return;
     }
-    __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
 #pragma unroll 1
-    for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
-    if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
-    if (!xr) return;
-    wait_records(Lflag);
-#pragma unroll 1
-    for (int i = wv - 1; i < ROWS_PER_WAVE; i += 3) launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + i, lane, Lmodel);
-    wait_records(Lflag + 1);
-#pragma unroll 1
-    for (int i = wv - 1; i < ROWS_PER_WAVE; i += 3)
-        launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
+    for (;;) {
+        int n = 0;
+        if (lane == 0) n = __hip_atomic_fetch_add(Lho + HO_COST, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        n = __builtin_amdgcn_readfirstlane(n);
+        if (n >= 2 * ROWS_PER_WAVE) break;
+        if (n < ROWS_PER_WAVE) {
+            wait_records(Lflag);
+            launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + n, lane, Lmodel);
+        } else {
+            wait_records(Lflag + 1);
+            launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - ROWS_PER_WAVE), lane, Lmodel);
+        }
+    }
+}
+
+// The doubled SIMD's relief (a.handover): the first of waves 1..3 to end its own rows claims the
+// fifth wave's rows, asks for them (Lho[HO_REQ]) and waits for the fifth wave's answer: 1 = it
+// stopped at the top of step Lho[HO_STEP] and left its state in Lst, 2 = it had already finished.
+// The claiming wave then runs the remaining steps alone on its SIMD, and the fifth wave's SIMD-mate
+// runs on alone too, each at one wave per SIMD instead of sharing the SIMD's issue slots.
+template <int CK, bool EN>
+__device__ __forceinline__ void take_over(const FrRolloutArgs &a, int lane, double *Lk, double *Lw, const double *Lmodel,
+                                          const double *Lx0, int *Lflag, int *Lho, double *Lst)
+{
+    int won = 0;
+    if (lane == 0) {
+        int z = 0;
+        won = __hip_atomic_compare_exchange_strong(Lho + HO_CLAIM, &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+    }
+    if (!__builtin_amdgcn_readfirstlane(won)) return;
+    __hip_atomic_store(Lho + HO_REQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int st;
+    while ((st = __hip_atomic_load(Lho + HO_STATUS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_readfirstlane(st) != 1) return;
+    coop_rows<CK, EN, true, 2>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4), lane,
+                               gridDim.x * 4 + blockIdx.x, Lk, Lw, Lmodel, Lx0, Lho, Lst);
+    if (a.costs_in_launch) signal_records(Lflag + 1);
 }
 
 // The update's state into LDS: from the launch's arguments with fused sampling, else from x0
@@ -1681,7 +1744,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, false);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false);
     }
 }
 
@@ -1696,6 +1759,8 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
     __shared__ int Lflag[2];   // launch_costs: wave 0's and the fifth wave's records are stored
+    __shared__ int Lho[HO_N];  // take_over / launch_costs: request, status, step, claim, cost counter
+    __shared__ double Lst[64 * 3];   // take_over: the fifth wave's (q, qd, E) per lane
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
@@ -1709,6 +1774,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     stage_body_table(a, Lmodel, 320);
     stage_x0(a, Lx0);
     if (threadIdx.x < 2) Lflag[threadIdx.x] = 0;
+    if (threadIdx.x < HO_N) Lho[threadIdx.x] = 0;
     if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
@@ -1727,11 +1793,22 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __builtin_amdgcn_s_setprio(MAIN_PRIO);
 #endif
         coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, xr);
+        if (xr && wv != 0 && a.handover) take_over<CK, EN>(a, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr);
     } else if (xr) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
-        coop_rows<CK, EN, true>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
-        if (a.costs_in_launch) signal_records(Lflag + 1);
+        const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;
+        int ky = -1;
+        if (a.handover) ky = coop_rows<CK, EN, true, 1>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lho, Lst);
+        else coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
+        const uint64_t hm = __ballot(ky >= 0);   // the live rows stop at the same step
+        const bool handed = hm != 0;
+        if (blockIdx.x == 0 && lane == 0)
+            const_cast<Status *>(a.status)->handover = handed ? __builtin_amdgcn_readlane(ky, __builtin_ffsll((long long)hm) - 1) : -1;
+        // records (and the handed-over state) stored before the answer / the flag
+        __builtin_amdgcn_s_waitcnt(0);
+        if (!handed && a.costs_in_launch) signal_records(Lflag + 1);
+        if (a.handover) __hip_atomic_store(Lho + HO_STATUS, handed ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -1803,6 +1880,14 @@ static bool costs_in_launch_enabled()
 
 bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
 
+// take_over in fr_coop_x_kernel; MPPI_HANDOVER=0 leaves the fifth wave's rows on its SIMD (A/B;
+// read per update: tests switch it in-process)
+static bool handover_enabled()
+{
+    const char *e = getenv("MPPI_HANDOVER");
+    return e && e[0] == '1';
+}
+
 // Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample
 // their own rows, a.fuse_sample) for `count` rows.
 bool fr_coop_update_fusable(int64_t count)
@@ -1843,6 +1928,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.xrows = xrows;
     *folded = frow;
     a.costs_in_launch = costs_in_launch_enabled() ? 1 : 0;
+    a.handover = handover_enabled() ? 1 : 0;
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
     if (xrows == 0 || !a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;

@@ -18,7 +18,7 @@ struct Status {
     int all_nan;     // <= 1 valid rollout: "all nan rollouts" (mppi.cpp:369-370)
     int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
-    int pad;
+    int handover;    // fr_coop_x_kernel: step at which the fifth wave's rows moved (take_over), or -1
     double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
     double tsplit[GRAD_SPLIT_DEF];    // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };
@@ -101,6 +101,9 @@ struct FrRolloutArgs {
     // the next update's draws for the main waves' own rows, made in the launch's idle tail into
     // this buffer (fr_coop.hip tail_draws; null: none): rank_draw_kernel then draws only the rest
     double *ahead_noise;
+    // fr_coop_x_kernel: the fifth wave's rows move to the first of waves 1..3 to end its own rows
+    // (fr_coop.hip take_over; MPPI_HANDOVER=0 keeps them on the doubled SIMD)
+    int handover;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:

@@ -384,7 +384,9 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 #define MPPI_INFO_TAIL_DRAWS 3            /* the launch drew the next update's eps (main rows) */
 #define MPPI_INFO_SAMPLING 4              /* 0 sample kernel, 1 sampled in launch, 2 drawn ahead */
 #define MPPI_INFO_ROWS 5                  /* rows rolled out (local rollouts + a folded filter()) */
-#define MPPI_UPDATE_INFO_N 6
+#define MPPI_INFO_HANDOVER 6              /* step at which the fifth wave's rows moved off the doubled
+                                             SIMD (take_over), -1 none; read from the device */
+#define MPPI_UPDATE_INFO_N 7
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
 /* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control

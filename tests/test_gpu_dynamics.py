@@ -21,6 +21,9 @@ pytestmark = pytest.mark.gpu
 # ~4e-10 relative there (measured, step 27 of the stepping test), so they get 1e-8.
 STATE_RTOL = 1e-10
 ACC_RTOL = 1e-8
+# joint velocities integrate those accelerations (qd += qdd dt): measured 1.02e-10 relative on the
+# finger velocity after 38 steps, so the state's velocity half gets 1e-9
+VEL_RTOL = 1e-9
 EE = abi.MPPI_EE_N
 EE_ACC = slice(abi.MPPI_EE_LINEAR_ACCELERATION, abi.MPPI_EE_ANGULAR_ACCELERATION + 3)
 
@@ -34,6 +37,12 @@ def _close(a, b, rtol, what):
         what, err.max(), int(np.argmax(err)), a.reshape(-1)[np.argmax(err)], b.reshape(-1)[np.argmax(err)])
 
 
+def _tol_state():
+    t = np.full(31, STATE_RTOL)   # FrankaRidgeback's state: q, qd, tau, available energy
+    t[12:24] = VEL_RTOL
+    return t
+
+
 def _tol_ee():
     t = np.full(EE, STATE_RTOL)
     t[EE_ACC] = ACC_RTOL
@@ -42,6 +51,7 @@ def _tol_ee():
 
 def _tol_query():
     t = np.full(abi.MPPI_DYNAMICS_QUERY_N, STATE_RTOL)
+    t[12:24] = VEL_RTOL   # joint velocities
     t[24:36] = ACC_RTOL   # joint accelerations
     return t
 
@@ -80,9 +90,9 @@ def test_object_steps_match_oracle():
     rng = np.random.default_rng(3)
     for k, u in enumerate(_controls(rng, 40)):
         xd, xo = dev.step(u, 0.01), orc.step(u, 0.01)
-        _close(xd, xo, STATE_RTOL, "state step %d" % k)
+        _close(xd, xo, _tol_state(), "state step %d" % k)
         _ee_close(dev.get_end_effector_state_row(), orc.end_effector(), "EE step %d" % k)
-    _close(dev.get_state(), orc.get_state(), STATE_RTOL, "get_state")
+    _close(dev.get_state(), orc.get_state(), _tol_state(), "get_state")
     x1 = dev.get_state()
     dev.set_state(x1, 0.4)
     orc.set_state(x1, 0.4)
@@ -91,7 +101,7 @@ def test_object_steps_match_oracle():
     _close(qd, qo, _tol_query(), "members after set_state (stale torque)")
     _ee_close(dev.get_end_effector_state_row(), orc.end_effector(), "EE after set_state")
     for k, u in enumerate(_controls(rng, 10)):
-        _close(dev.step(u, 0.01), orc.step(u, 0.01), STATE_RTOL, "state step %d after set_state" % k)
+        _close(dev.step(u, 0.01), orc.step(u, 0.01), _tol_state(), "state step %d after set_state" % k)
     ee = dev.get_end_effector_state()
     assert ee.jacobian.shape == (6, 12) and abs(np.linalg.norm(ee.orientation) - 1.0) < 1e-14
     np.testing.assert_allclose(ee.rotation @ ee.rotation.T, np.eye(3), rtol=0, atol=1e-14)

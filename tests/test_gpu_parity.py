@@ -420,6 +420,41 @@ def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
                 np.testing.assert_array_equal(u, v, err_msg="%s: update %d %s" % (mode, j, name))
 
 
+@pytest.mark.parametrize("rollouts,objective", [(4096, "am"), (4096, "energy"), (4096, "track_point"), (1000, "am"),
+                                                (4097, "am")])
+def test_handover_equals_doubled_simd(rollouts, objective, monkeypatch):
+    """take_over (fr_coop.hip): the fifth wave's rows move, mid-horizon, to the first of waves 1..3
+    to end its own rows, off the SIMD the fifth wave shares with wave 0.  The moved rows resume from
+    the (q, qd, E) the fifth wave left at the top of a step, so every output equals the launch that
+    keeps them on the doubled SIMD (MPPI_HANDOVER=0), bit for bit, over updates with kept rollouts
+    and shifts; 1000 rollouts have fifth waves in three workgroups, 4097 four leftover rows."""
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.64, keep_best_rollouts=20, threads=8)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
+    make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
+    out, steps = {}, []
+    for ho in ("0", "1"):
+        monkeypatch.setenv("MPPI_HANDOVER", ho)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), make_cost())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for tm in times:
+            t.update(x, tm)
+            info = t.update_info()
+            if ho == "1":
+                steps.append(info["handover"])
+            else:
+                assert info["handover"] == -1, info
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[ho] = rec + [(np.float64(t.get_optimal_total_cost()),) * 4]   # the folded filter() rows
+    print("handover steps:", steps)
+    assert all(0 < k < 63 for k in steps), steps
+    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+
+
 def test_two_philox_shards_draw_ahead_equal_unsharded():
     """Device Philox across two shards on one GPU (phase-split ABI, host all-reduces): each shard
     holds 4098 rollouts, so its rollout launch runs one round of workgroups and its draws are made
@@ -501,22 +536,32 @@ def test_rollout_kernel_event_ring(S):
     np.testing.assert_array_equal(u_timed, u_plain)
 
 
-def test_default_stack_without_self_collision_4096():
+@pytest.mark.parametrize("barriers", ["no_self_collision", "none"])
+def test_default_stack_without_self_collision_4096(barriers):
     """The bench's kernel path (cooperative CRBA + Gauss-Jordan solve, objective in the launch) at
-    4096 x 64 with enable_self_collision_limit = 0: the costs are then the state-dependent terms
-    (joint limits, workspace, velocity, trajectory, manipulability) instead of 1.28e13 + those, so
-    the relative cost bar measures the dynamics (VERDICT r02 weak #2)."""
+    4096 x 64 without the constant self-collision term (1.28e13 per rollout).
+    "no_self_collision": the other terms stay; from the huddled state every rollout still breaches
+    a joint-limit / workspace barrier on some steps (1e10 each, measured minimum 7e10), so the costs
+    count breaches.  "none": every barrier off (joint, self-collision, workspace, energy), leaving
+    the smooth velocity / trajectory / manipulability terms, so the relative cost bar measures the
+    dynamics and kinematics alone."""
     cost = am.AssistedManipulation()
-    cost.configuration.enable_self_collision_limit = 0
+    c = cost.configuration
+    c.enable_self_collision_limit = 0
+    if barriers == "none":
+        c.enable_joint_limit = c.enable_workspace_limit = c.enable_energy_limit = 0
     conf, dev, orc, sd = fr_pair(S=4096, horison=0.64, threads=16, cost=cost)
     rng = np.random.default_rng(7)
     x = am.huddled_state()
     stats = []
     for j in range(3):
         step_both(dev, orc, x, 0.05 * j, rng, sd)
-        assert_update_parity(dev, orc, "nosc upd %d" % j, stats=stats)
+        assert_update_parity(dev, orc, "%s upd %d" % (barriers, j), stats=stats)
         assert dev.update_info()["objective_in_launch"] == 1
-        assert np.nanmin(orc.costs()) < 1e6   # no 1e13 constant under the small costs
+        co = orc.costs()
+        assert np.nanmax(co) < (1e12 if barriers != "none" else 1e9), np.nanmax(co)   # no 1.28e13 constant
+        if barriers == "none":
+            assert np.nanmax(co) - np.nanmin(co) > 0.0
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
 
 
