@@ -2109,11 +2109,12 @@ mppi_status mppi_noise(mppi_handle *h, double *out)
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
 {
     if (!h || !info || n < 0 || n > MPPI_UPDATE_INFO_N) return MPPI_ERR_INVALID;
-    if (n > MPPI_INFO_HANDOVER && h->info[MPPI_INFO_HANDOVER] == -2) {   // the x kernel's Status word
-        int step = -1;
+    if (n > MPPI_INFO_HANDOVER) {   // Status words of the last rollout launch
+        int w[2] = {-1, 0};
         HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipMemcpy(&step, &h->d_status->handover, sizeof(int), hipMemcpyDeviceToHost));
-        h->info[MPPI_INFO_HANDOVER] = step;
+        HIP_TRY(hipMemcpy(w, &h->d_status->handover, sizeof(w), hipMemcpyDeviceToHost));
+        if (h->info[MPPI_INFO_HANDOVER] == -2) h->info[MPPI_INFO_HANDOVER] = w[0];
+        h->info[MPPI_INFO_WAIT_TIMEOUTS] = w[1];
     }
     std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;

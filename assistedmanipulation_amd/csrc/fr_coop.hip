@@ -413,8 +413,298 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
         : "+&v"(m[0]), "+&v"(m[1]), "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
         : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
 }
+// pivot 0: eleven FMAs with pivot 0's quotient, and pivot 1's quotient computed between them
+__device__ __forceinline__ double gj_pivot_0(double *Mc, double nt, double inv_next)
+{
+    double nn;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %11, -%0, %13\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn)
+        : "v"(nt), "v"(inv_next));
+    return nn;
+}
+// pivot 1: eleven FMAs with pivot 1's quotient, and pivot 2's quotient computed between them
+__device__ __forceinline__ double gj_pivot_1(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[0]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 2: eleven FMAs with pivot 2's quotient, and pivot 3's quotient computed between them
+__device__ __forceinline__ double gj_pivot_2(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 3: eleven FMAs with pivot 3's quotient, and pivot 4's quotient computed between them
+__device__ __forceinline__ double gj_pivot_3(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 4: eleven FMAs with pivot 4's quotient, and pivot 5's quotient computed between them
+__device__ __forceinline__ double gj_pivot_4(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 5: eleven FMAs with pivot 5's quotient, and pivot 6's quotient computed between them
+__device__ __forceinline__ double gj_pivot_5(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 6: eleven FMAs with pivot 6's quotient, and pivot 7's quotient computed between them
+__device__ __forceinline__ double gj_pivot_6(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 7: eleven FMAs with pivot 7's quotient, and pivot 8's quotient computed between them
+__device__ __forceinline__ double gj_pivot_7(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 8: eleven FMAs with pivot 8's quotient, and pivot 9's quotient computed between them
+__device__ __forceinline__ double gj_pivot_8(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 9: eleven FMAs with pivot 9's quotient, and pivot 10's quotient computed between them
+__device__ __forceinline__ double gj_pivot_9(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[10]), "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 10: eleven FMAs with pivot 10's quotient, and pivot 11's quotient computed between them
+__device__ __forceinline__ double gj_pivot_10(double *Mc, double nt)
+{
+    double nn, d, r, t, e;
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %12, %0 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %13, %12\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %14, -%0, %13\n\t"
+        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %11, %14, %15, %14\n\t"
+        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
+        : "v"(nt));
+    return nn;
+}
+// pivot 11: eleven FMAs with pivot 11's quotient
+__device__ __forceinline__ void gj_pivot_11(double *Mc, double nt)
+{
+    asm(""
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10])
+        : "v"(nt));
+}
+// the same pivots without the pipelining (GJ_SERIAL builds, A/B)
 // pivot 0 (d = the composite mass of body 0; inv = 1 / d)
-__device__ __forceinline__ void gj_pivot_0(double *Mc, double inv)
+__device__ __forceinline__ void gj_serial_pivot_0(double *Mc, double inv)
 {
     const double nt = -Mc[0] * inv;
     asm(""
@@ -433,7 +723,7 @@ __device__ __forceinline__ void gj_pivot_0(double *Mc, double inv)
         : "v"(nt));
 }
 // pivot 1 (d = the composite mass of body 1; inv = 1 / d)
-__device__ __forceinline__ void gj_pivot_1(double *Mc, double inv)
+__device__ __forceinline__ void gj_serial_pivot_1(double *Mc, double inv)
 {
     const double nt = -Mc[1] * inv;
     asm(""
@@ -452,7 +742,7 @@ __device__ __forceinline__ void gj_pivot_1(double *Mc, double inv)
         : "v"(nt));
 }
 // pivot 2
-__device__ __forceinline__ void gj_pivot_2(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_2(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
@@ -473,7 +763,7 @@ __device__ __forceinline__ void gj_pivot_2(double *Mc)
         : "v"(nt));
 }
 // pivot 3
-__device__ __forceinline__ void gj_pivot_3(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_3(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
@@ -494,7 +784,7 @@ __device__ __forceinline__ void gj_pivot_3(double *Mc)
         : "v"(nt));
 }
 // pivot 4
-__device__ __forceinline__ void gj_pivot_4(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_4(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
@@ -515,7 +805,7 @@ __device__ __forceinline__ void gj_pivot_4(double *Mc)
         : "v"(nt));
 }
 // pivot 5
-__device__ __forceinline__ void gj_pivot_5(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_5(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
@@ -536,7 +826,7 @@ __device__ __forceinline__ void gj_pivot_5(double *Mc)
         : "v"(nt));
 }
 // pivot 6
-__device__ __forceinline__ void gj_pivot_6(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_6(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
@@ -557,7 +847,7 @@ __device__ __forceinline__ void gj_pivot_6(double *Mc)
         : "v"(nt));
 }
 // pivot 7
-__device__ __forceinline__ void gj_pivot_7(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_7(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
@@ -578,7 +868,7 @@ __device__ __forceinline__ void gj_pivot_7(double *Mc)
         : "v"(nt));
 }
 // pivot 8
-__device__ __forceinline__ void gj_pivot_8(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_8(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
@@ -599,7 +889,7 @@ __device__ __forceinline__ void gj_pivot_8(double *Mc)
         : "v"(nt));
 }
 // pivot 9
-__device__ __forceinline__ void gj_pivot_9(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_9(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
@@ -620,7 +910,7 @@ __device__ __forceinline__ void gj_pivot_9(double *Mc)
         : "v"(nt));
 }
 // pivot 10
-__device__ __forceinline__ void gj_pivot_10(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_10(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
@@ -641,7 +931,7 @@ __device__ __forceinline__ void gj_pivot_10(double *Mc)
         : "v"(nt));
 }
 // pivot 11
-__device__ __forceinline__ void gj_pivot_11(double *Mc)
+__device__ __forceinline__ void gj_serial_pivot_11(double *Mc)
 {
     double d;
     asm("v_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
@@ -811,6 +1101,7 @@ struct LaneConst {
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
     int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
+    double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
 };
@@ -872,6 +1163,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 #else
     if constexpr (EN) inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);   // coop_aba's input
 #endif
+#ifdef DUMMY_BODY0
     {
         const double live = M[T_NROT] + M[T_ROT];   // 1 for a real body, 0 on lanes 12..15
         bd.m = M[T_M] * live;
@@ -883,6 +1175,18 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
             bd.S[k] = S[k];
         }
     }
+#else
+    {   // lanes 12..15: the table's dummy body has zero mass and inertia, so h = Ib = 0 there
+        bd.m = M[T_M];
+#pragma unroll
+        for (int k = 0; k < 3; k++) bd.h[k] = M[T_M] * com[k];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            bd.Ib[k] = Ib[k];
+            bd.S[k] = S[k];
+        }
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < 6; k++) Lk[L_S + L.slot * S_STR + k] = S[k];
     Lk[L_S + L.slot * S_STR + 6] = qd;
@@ -1113,7 +1417,11 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     // strictly-upper part of column j: M_ij for the ancestors i of j (finger 11 hangs off body 9,
     // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column
 #pragma unroll
+#ifdef ANC_BFI
     for (int i = 0; i < 11; i++) Mc[i] = msel(__builtin_amdgcn_sbfe(L.anc, i, 1), 0.0, Mc[i]);
+#else
+    for (int i = 0; i < 11; i++) Mc[i] *= L.ancd[i];
+#endif
     Mc[11] = 0.0;
     // row j of the block: that column, then tau_j and zeros in slots 12..15, then the diagonal over
     // slot j (LDS stores of a wave land in order).  Entry (i, j) of the block is then column i's
@@ -1131,8 +1439,17 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 #ifdef PHASE_TRACE
     t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
 #endif
-    gj_pivot_0(Mc, L.inv_m0); gj_pivot_1(Mc, L.inv_m1); gj_pivot_2(Mc); gj_pivot_3(Mc); gj_pivot_4(Mc); gj_pivot_5(Mc);
-    gj_pivot_6(Mc); gj_pivot_7(Mc); gj_pivot_8(Mc); gj_pivot_9(Mc); gj_pivot_10(Mc); gj_pivot_11(Mc);
+#ifdef GJ_SERIAL
+    gj_serial_pivot_0(Mc, L.inv_m0); gj_serial_pivot_1(Mc, L.inv_m1); gj_serial_pivot_2(Mc); gj_serial_pivot_3(Mc);
+    gj_serial_pivot_4(Mc); gj_serial_pivot_5(Mc); gj_serial_pivot_6(Mc); gj_serial_pivot_7(Mc); gj_serial_pivot_8(Mc);
+    gj_serial_pivot_9(Mc); gj_serial_pivot_10(Mc); gj_serial_pivot_11(Mc);
+#else
+    double nt = -Mc[0] * L.inv_m0;   // each pivot's block returns the next pivot's quotient
+    nt = gj_pivot_0(Mc, nt, L.inv_m1);
+    nt = gj_pivot_1(Mc, nt); nt = gj_pivot_2(Mc, nt); nt = gj_pivot_3(Mc, nt); nt = gj_pivot_4(Mc, nt);
+    nt = gj_pivot_5(Mc, nt); nt = gj_pivot_6(Mc, nt); nt = gj_pivot_7(Mc, nt); nt = gj_pivot_8(Mc, nt);
+    nt = gj_pivot_9(Mc, nt); nt = gj_pivot_10(Mc, nt); gj_pivot_11(Mc, nt);
+#endif
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
     // tau' at L_TP and every other lane its column in its own block row (read above, dead now), so
     // lane j reads M'_jj back at slot j of that row: no per-lane register select, no branch.
@@ -1171,9 +1488,15 @@ __global__ void fr_body_table_kernel(const DevModel *model, const DevCost *cost,
         double v;
         if (f < T_P) v = Rs[f];
         else if (f < T_M) v = ps[f - T_P];
+#ifdef DUMMY_BODY0
         else if (f == T_M) v = db.mass;
         else if (f < T_I) v = db.c[f - T_C];
         else if (f < T_F) v = db.Ic[f - T_I];
+#else
+        else if (f == T_M) v = live * db.mass;   // the dummy body (lanes 12..15) is massless:
+        else if (f < T_I) v = live * db.c[f - T_C];   // its world inertia, F and M column vanish
+        else if (f < T_F) v = live * db.Ic[f - T_I];
+#endif
         else if (f < T_MA) v = (b == FR_EE_PARENT) ? dm.ee_p[f - T_F] : ((b == FR_AM_PARENT) ? dm.am_p[f - T_F] : 0.0);
         else if (f < T_AX) {
             const int r = f - T_MA;
@@ -1242,11 +1565,19 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // step and, once another wave asks, leaves its lanes' (q, qd, E) in Lst and the step in
 // Lho[HO_STEP] and returns that step; 2 = the wave that took them over, resuming at that step (the
 // records up to it are stored).  Returns the step handed over, or -1.
-enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_N = 5 };
-template <int CK, bool EN, bool FROW, int HO = 0>
+// PROG (the update launch's main waves): the wave stores its step into *Lprog at the top of each
+// step - wave 0 of a workgroup with a fifth wave into Lho[HO_MSTEP], the others into a sink - and
+// the fifth wave (HO == 1) raises its priority while it is behind wave 0, lowers it while ahead.
+// The two share a SIMD, whose arbiter otherwise issues the older wave (wave 0) first: the fifth
+// wave then reached only about a third of its horizon by the time the first other wave ended
+// (step 23 of 63 at 4096 x 64), and its remaining steps ran alone after that at one wave per SIMD
+// however they were placed.  At equal progress both have about 40 % left when another SIMD frees
+// up, and take_over runs those on two SIMDs at once.
+enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_MSTEP = 5, HO_SINK = 6, HO_N = 7 };
+template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, int *Lho = nullptr,
-                                         double *Lst = nullptr)
+                                         double *Lst = nullptr, int *Lprog = nullptr)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1302,6 +1633,12 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         if (j == FR_NB - 1) anc &= ~(1 << (FR_NB - 2));   // finger 11 is not under finger 10
         asm volatile("" : "+v"(anc));
         L.anc = anc;
+#pragma unroll
+        for (int i = 0; i < 11; i++) {
+            double d = ((anc >> i) & 1) ? 1.0 : 0.0;
+            asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
+            L.ancd[i] = d;
+        }
     }
     L.mc = M[T_MC];
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
@@ -1354,8 +1691,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
     uint64_t t_top = stamp(sq);
 #endif
-    int req = 0;   // HO == 1: Lho[HO_REQ] as read during the previous step
+    int req = 0, mstep = 0;   // HO == 1: Lho[HO_REQ] and wave 0's step, read during the previous step
     for (int k = kb; k < H - 1; k++) {
+        if constexpr (PROG) *Lprog = k;
         if constexpr (HO == 1) {
             if (__builtin_amdgcn_readfirstlane(req)) {   // another wave resumes these rows at step k
                 Lst[3 * lane] = q;
@@ -1364,11 +1702,16 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
                 Lho[HO_STEP] = k;
                 return k;
             }
+            if (k < __builtin_amdgcn_readfirstlane(mstep)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
         }
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
-        if constexpr (HO == 1) req = __hip_atomic_load(Lho + HO_REQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (HO == 1) {
+            req = __hip_atomic_load(Lho + HO_REQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            mstep = __hip_atomic_load(Lho + HO_MSTEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
 #endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
         // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
@@ -1486,9 +1829,22 @@ __device__ __forceinline__ void signal_records(int *flag)
     __builtin_amdgcn_s_waitcnt(0);
     __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void wait_records(int *flag)
+// Bounded: a wave that never signals (a bug) costs about a second, not a hung GPU; the timeout is
+// counted in Status::wait_timeouts (mppi_update_info MPPI_INFO_WAIT_TIMEOUTS, asserted 0 by tests).
+constexpr int WAIT_SPINS = 1 << 20;
+__device__ __forceinline__ void note_wait_timeout(const FrRolloutArgs &a)
 {
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(8);
+    if (a.status) atomicAdd(&const_cast<Status *>(a.status)->wait_timeouts, 1);
+}
+__device__ __forceinline__ void wait_records(const FrRolloutArgs &a, int *flag)
+{
+    // the flag read through readfirstlane: a uniform (scalar-branch) loop whatever the exec mask
+    for (int i = 0; i < WAIT_SPINS; i++) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
+            return;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
 }
 
 // The next update's draws for the wave's own four rows (a.ahead_noise), made in the launch's idle
@@ -1540,16 +1896,17 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
         if (!xr) return;
     }
 #pragma unroll 1
-    for (;;) {
-        int n = 0;
-        if (lane == 0) n = __hip_atomic_fetch_add(Lho + HO_COST, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        n = __builtin_amdgcn_readfirstlane(n);
+    for (int it = 0; it <= 2 * ROWS_PER_WAVE; it++) {
+        // every lane executes the add (lane 0 adds 1, the others 0), so no lane-dependent branch
+        // surrounds the atomic; lane 0's old value is the item
+        const int n = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(Lho + HO_COST, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (n >= 2 * ROWS_PER_WAVE) break;
         if (n < ROWS_PER_WAVE) {
-            wait_records(Lflag);
+            wait_records(a, Lflag);
             launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + n, lane, Lmodel);
         } else {
-            wait_records(Lflag + 1);
+            wait_records(a, Lflag + 1);
             launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - ROWS_PER_WAVE), lane, Lmodel);
         }
     }
@@ -1572,9 +1929,12 @@ __device__ __forceinline__ void take_over(const FrRolloutArgs &a, int lane, doub
     }
     if (!__builtin_amdgcn_readfirstlane(won)) return;
     __hip_atomic_store(Lho + HO_REQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    int st;
-    while ((st = __hip_atomic_load(Lho + HO_STATUS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
-        __builtin_amdgcn_s_sleep(1);
+    int st = 0;
+    for (int i = 0; i < WAIT_SPINS && st == 0; i++) {
+        st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lho + HO_STATUS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (st == 0) __builtin_amdgcn_s_sleep(1);
+    }
+    if (st == 0 && lane == 0) note_wait_timeout(a);
     if (__builtin_amdgcn_readfirstlane(st) != 1) return;
     coop_rows<CK, EN, true, 2>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4), lane,
                                gridDim.x * 4 + blockIdx.x, Lk, Lw, Lmodel, Lx0, Lho, Lst);
@@ -1792,7 +2152,8 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #ifdef MAIN_PRIO
         __builtin_amdgcn_s_setprio(MAIN_PRIO);
 #endif
-        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
+        coop_rows<CK, EN, false, 0, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0,
+                                          nullptr, nullptr, Lho + (wv == 0 ? HO_MSTEP : HO_SINK));
         if (xr && wv != 0 && a.handover) take_over<CK, EN>(a, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
         if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr);
     } else if (xr) {

@@ -19,6 +19,8 @@ struct Status {
     int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
     int handover;    // fr_coop_x_kernel: step at which the fifth wave's rows moved (take_over), or -1
+    int wait_timeouts;   // fr_coop_x_kernel: bounded in-launch waits that gave up (a bug if nonzero)
+    int pad[3];
     double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
     double tsplit[GRAD_SPLIT_DEF];    // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };

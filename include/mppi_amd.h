@@ -386,7 +386,9 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 #define MPPI_INFO_ROWS 5                  /* rows rolled out (local rollouts + a folded filter()) */
 #define MPPI_INFO_HANDOVER 6              /* step at which the fifth wave's rows moved off the doubled
                                              SIMD (take_over), -1 none; read from the device */
-#define MPPI_UPDATE_INFO_N 7
+#define MPPI_INFO_WAIT_TIMEOUTS 7         /* in-launch waits that gave up since create (a bug if
+                                             nonzero; the launch went on); read from the device */
+#define MPPI_UPDATE_INFO_N 8
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
 /* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control

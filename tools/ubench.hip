@@ -17,6 +17,8 @@ __global__ void bench(double *out, long long *cyc, double seed)
     __syncthreads();
     int addr = (threadIdx.x & 7) * 8;
     int i0 = threadIdx.x, i1 = 1, i2 = 2 + threadIdx.x, i3 = 3;
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    d4 m0 = {a0, a1, a2, a3}, m1 = m0, m2 = m0, m3 = m0;
     long long t0 = clock64();
     for (int it = 0; it < ITERS; it++) {
         if (MODE == 0) {   // 8 independent f64 FMA chains
@@ -70,6 +72,24 @@ __global__ void bench(double *out, long long *cyc, double seed)
                               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(b), "v"(c));)
         } else if (MODE == 15) {   // dependent v_add_f64 chain
             REP8(asm volatile("v_add_f64 %0, %0, %1\n v_add_f64 %0, %0, %1\n" : "+v"(a0) : "v"(c));)
+        } else if (MODE == 16) {   // independent v_mfma_f64_16x16x4_f64, 4 accumulators (the M = S^T F A/B)
+            REP8({
+                m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, m0, 0, 0, 0);
+                m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, m1, 0, 0, 0);
+                m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b, m2, 0, 0, 0);
+                m3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b, m3, 0, 0, 0);
+            })
+        } else if (MODE == 17) {   // dependent v_mfma_f64_16x16x4_f64 chain
+            REP8({
+                m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, m0, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, m0, 0, 0, 0);
+            })
+        } else if (MODE == 18) {   // dependent v_rcp_f64 chain
+            REP8(asm volatile("v_rcp_f64 %0, %0\n s_nop 0\n v_rcp_f64 %0, %0\n s_nop 0\n" : "+v"(a0));)
+        } else if (MODE == 19) {   // dependent fmac_f64_dpp -> mov_b64_dpp bcast -> rcp -> fma (one pivot's chain)
+            REP8(asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                              "v_mov_b64_dpp %0, %0 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n s_nop 0\n"
+                              : "+v"(a0) : "v"(c));)
         } else if (MODE == 11) {   // independent f32 FMA (reference point)
             float f0 = a0, f1 = a1;
             REP8(asm volatile("v_fma_f32 %0, %2, %2, %0\n v_fma_f32 %1, %2, %2, %1\n" : "+v"(f0), "+v"(f1) : "v"((float)c));)
@@ -78,7 +98,7 @@ __global__ void bench(double *out, long long *cyc, double seed)
     }
     long long t1 = clock64();
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
-    out[blockIdx.x * 64 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    out[blockIdx.x * 64 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + m0.x + m1.y + m2.z + m3.w;
 }
 
 template <int MODE>
@@ -91,7 +111,8 @@ void run(const char *name, int blocks, double *d_out, long long *d_cyc)
     double m = 0;
     for (int i = 0; i < blocks; i++) m += h[i];
     m /= blocks;
-    printf("%-34s blocks=%5d  cyc/instr = %.2f\n", name, blocks, m / (ITERS * 16.0 * (MODE == 0 || MODE == 14 ? 2 : 1)));
+    const double per = MODE == 0 || MODE == 14 ? 32.0 : (MODE == 16 ? 32.0 : (MODE == 19 ? 8.0 : 16.0));
+    printf("%-34s blocks=%5d  cyc/instr = %.2f\n", name, blocks, m / (ITERS * per));
 }
 
 int main()
@@ -116,6 +137,10 @@ int main()
         run<13>("fmac_f64_dpp dependent (+nop1)", blocks, d_out, d_cyc);
         run<14>("fmac_f64_dpp indep (4 acc)", blocks, d_out, d_cyc);
         run<15>("add_f64 dependent", blocks, d_out, d_cyc);
+        run<16>("mfma_f64_16x16x4 indep (4 acc)", blocks, d_out, d_cyc);
+        run<17>("mfma_f64_16x16x4 dependent", blocks, d_out, d_cyc);
+        run<18>("rcp_f64 dependent (+nop0)", blocks, d_out, d_cyc);
+        run<19>("fmac_dpp->mov_b64_dpp pair (per pair)", blocks, d_out, d_cyc);
     }
     return 0;
 }
