@@ -1133,10 +1133,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     D[4] -= 1.0;
     D[8] -= 1.0;
     FKSTAMP(0, D[8])
+#ifndef ABL_NOSCAN   // instruction-count ablations (compile-only probes, tools/isa_regions.sh)
     scan_level2<1>(D, p);
     scan_level2<2>(D, p);
     scan_level2<4>(D, p);
     scan_level2<8>(D, p);
+#endif
     delta_col2(D);
     FKSTAMP(1, p[2])
     double R[9];
@@ -1157,7 +1159,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     S[4] = w[1] * rotf;
     S[5] = w[2] * rotf;
     double com[3], Iw[6], Ib[6];
+#ifdef ABL_NOWI
+    for (int k = 0; k < 3; k++) com[k] = p[k];
+    for (int k = 0; k < 6; k++) Iw[k] = Ib[k] = R[k];
+#else
     world_inertia(M, R, p, com, Iw, Ib);
+#endif
 #ifdef OLD_ABA
     inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);
 #else
@@ -1390,6 +1397,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     double own[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) own[k] = v[k];
+#ifndef ABL_NOISCAN
 #pragma unroll
     for (int k = 0; k < 9; k++) v[k] += shl<1>(v[k]);
 #pragma unroll
@@ -1400,6 +1408,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     for (int k = 0; k < 9; k++) v[k] += shl<8>(v[k]);
 #pragma unroll
     for (int k = 0; k < 9; k++) v[k] = msel(L.m_j10, v[k], own[k]);
+#endif
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
     const double m = L.mc, h0 = v[0], h1 = v[1], h2 = v[2];
@@ -1412,7 +1421,11 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     F[4] = (h2 * S[0] - h0 * S[2]) + ((I01 * S[3] + I11 * S[4]) + I12 * S[5]);
     F[5] = (h0 * S[1] - h1 * S[0]) + ((I02 * S[3] + I12 * S[4]) + I22 * S[5]);
     double Mc[12];
+#ifdef ABL_NOCD
+    for (int i = 0; i < 11; i++) Mc[i] = F[i % 6];
+#else
     column_dots(S, F, Mc);
+#endif
     const double diag = ((S[0] * F[0] + S[1] * F[1]) + (S[2] * F[2] + S[3] * F[3])) + (S[4] * F[4] + S[5] * F[5]);
     // strictly-upper part of column j: M_ij for the ancestors i of j (finger 11 hangs off body 9,
     // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column
@@ -1439,7 +1452,8 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 #ifdef PHASE_TRACE
     t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
 #endif
-#ifdef GJ_SERIAL
+#ifdef ABL_NOGJ
+#elif defined(GJ_SERIAL)
     gj_serial_pivot_0(Mc, L.inv_m0); gj_serial_pivot_1(Mc, L.inv_m1); gj_serial_pivot_2(Mc); gj_serial_pivot_3(Mc);
     gj_serial_pivot_4(Mc); gj_serial_pivot_5(Mc); gj_serial_pivot_6(Mc); gj_serial_pivot_7(Mc); gj_serial_pivot_8(Mc);
     gj_serial_pivot_9(Mc); gj_serial_pivot_10(Mc); gj_serial_pivot_11(Mc);
@@ -2241,12 +2255,13 @@ static bool costs_in_launch_enabled()
 
 bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
 
-// take_over in fr_coop_x_kernel; MPPI_HANDOVER=0 leaves the fifth wave's rows on its SIMD (A/B;
-// read per update: tests switch it in-process)
+// take_over in fr_coop_x_kernel (the default: 0.2874 -> 0.2694 ms/update at 4096 x 64, two
+// interleaved rounds on one box, profiles/r03_handover_ab/); MPPI_HANDOVER=0 leaves the fifth
+// wave's rows on its SIMD (A/B; read per update: tests switch it in-process)
 static bool handover_enabled()
 {
     const char *e = getenv("MPPI_HANDOVER");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample

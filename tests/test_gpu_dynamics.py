@@ -45,6 +45,7 @@ def _tol_state():
 
 def _tol_ee():
     t = np.full(EE, STATE_RTOL)
+    t[abi.MPPI_EE_LINEAR_VELOCITY:abi.MPPI_EE_ANGULAR_VELOCITY + 3] = VEL_RTOL   # J qd: measured 4.6e-10
     t[EE_ACC] = ACC_RTOL
     return t
 
@@ -58,6 +59,8 @@ def _tol_query():
 
 def _tol_rows(n):
     t = np.full(abi.MPPI_DF_N, STATE_RTOL)
+    e = abi.MPPI_DF_END_EFFECTOR
+    t[e + abi.MPPI_EE_LINEAR_VELOCITY:e + abi.MPPI_EE_ANGULAR_VELOCITY + 3] = VEL_RTOL
     t[abi.MPPI_DF_END_EFFECTOR + EE_ACC.start:abi.MPPI_DF_END_EFFECTOR + EE_ACC.stop] = ACC_RTOL
     return np.tile(t, (n, 1))
 
