@@ -1716,7 +1716,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
                 Lho[HO_STEP] = k;
                 return k;
             }
-            if (k < __builtin_amdgcn_readfirstlane(mstep)) __builtin_amdgcn_s_setprio(3);
+            if (k <= __builtin_amdgcn_readfirstlane(mstep) + 2) __builtin_amdgcn_s_setprio(3);
             else __builtin_amdgcn_s_setprio(0);
         }
         const double eps_l = eps_n, ub_l = ub_n;
@@ -1860,6 +1860,17 @@ __device__ __forceinline__ void wait_records(const FrRolloutArgs &a, int *flag)
     }
     if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
 }
+// the same bounded wait, returning the value it saw (0 if it gave up)
+__device__ __forceinline__ int wait_nonzero(const FrRolloutArgs &a, int *word)
+{
+    for (int i = 0; i < WAIT_SPINS; i++) {
+        const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v != 0) return v;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
+    return 0;
+}
 
 // The next update's draws for the wave's own four rows (a.ahead_noise), made in the launch's idle
 // tail after the rows' objective: draw_ahead_block's values (Philox by (rollout, step) with the
@@ -1890,18 +1901,25 @@ __device__ __forceinline__ void tail_draws(const FrRolloutArgs &a, int64_t lr0, 
     }
 }
 
-// Main wave wv (0..3) of the workgroup after its horizon loop.  xr: the workgroup's fifth wave has
-// rows.  Wave 0 (the fifth wave's SIMD-mate) signals its records stored; then every main wave takes
-// the doubled SIMD's rows one at a time from the counter Lho[HO_COST] (wave 0's four, then the
-// fifth wave's), each once its records are stored.
+// Main wave wv (0..3) of the workgroup after its horizon loop: the objective of its own rows and
+// the next update's draws for them.  xr (the workgroup has a fifth wave): wave 0 (the fifth wave's
+// SIMD-mate) and the wave that took the fifth wave's rows over (helper, take_over) leave their own
+// rows to a queue that every main wave of the workgroup works through once its own share is done,
+// one item at a time from the counter Lho[HO_COST]:
+//   0..3   the helper's rows (stored when it claimed: Lflag[2]),  4  the helper's draws,
+//   5..8   wave 0's rows (Lflag[0]),  9..12  the fifth wave's rows (Lflag[1]).
+// The helper's items exist only with a.handover, where some wave always claims (the first of
+// waves 1..3 to end its rows); they wait for the claim.
+constexpr int CQ_HELPER = 0, CQ_HDRAW = ROWS_PER_WAVE, CQ_MATE = ROWS_PER_WAVE + 1, CQ_FIFTH = 2 * ROWS_PER_WAVE + 1,
+              CQ_N = 3 * ROWS_PER_WAVE + 1;
 template <int CK, bool EN>
 __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
-                                             int *Lho, bool xr)
+                                             int *Lho, bool xr, bool helper)
 {
     const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
     if (xr && wv == 0) {
         signal_records(Lflag);
-    } else {
+    } else if (!helper) {
         __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -1910,18 +1928,28 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
         if (!xr) return;
     }
 #pragma unroll 1
-    for (int it = 0; it <= 2 * ROWS_PER_WAVE; it++) {
+    for (int it = 0; it <= CQ_N; it++) {
         // every lane executes the add (lane 0 adds 1, the others 0), so no lane-dependent branch
         // surrounds the atomic; lane 0's old value is the item
         const int n = __builtin_amdgcn_readfirstlane(
             __hip_atomic_fetch_add(Lho + HO_COST, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (n >= 2 * ROWS_PER_WAVE) break;
-        if (n < ROWS_PER_WAVE) {
+        if (n >= CQ_N) break;
+        if (n < CQ_MATE) {
+            if (!a.handover) continue;
+            const int hw = wait_nonzero(a, Lho + HO_CLAIM);   // the helper's wave index (1..3)
+            if (hw == 0) continue;
+            if (n < CQ_HDRAW) {
+                wait_records(a, Lflag + 2);
+                launch_row_cost<CK, EN>(a, (w0 + hw) * ROWS_PER_WAVE + n, lane, Lmodel);
+            } else if (a.ahead_noise) {
+                tail_draws(a, (w0 + hw) * ROWS_PER_WAVE, lane);
+            }
+        } else if (n < CQ_FIFTH) {
             wait_records(a, Lflag);
-            launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + n, lane, Lmodel);
+            launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + (n - CQ_MATE), lane, Lmodel);
         } else {
             wait_records(a, Lflag + 1);
-            launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - ROWS_PER_WAVE), lane, Lmodel);
+            launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - CQ_FIFTH), lane, Lmodel);
         }
     }
 }
@@ -1931,28 +1959,32 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
 // stopped at the top of step Lho[HO_STEP] and left its state in Lst, 2 = it had already finished.
 // The claiming wave then runs the remaining steps alone on its SIMD, and the fifth wave's SIMD-mate
 // runs on alone too, each at one wave per SIMD instead of sharing the SIMD's issue slots.
+// Returns whether this wave claimed (its own rows' objective and draws then go to the workgroup's
+// queue, launch_costs).
 template <int CK, bool EN>
-__device__ __forceinline__ void take_over(const FrRolloutArgs &a, int lane, double *Lk, double *Lw, const double *Lmodel,
-                                          const double *Lx0, int *Lflag, int *Lho, double *Lst)
+__device__ __forceinline__ bool take_over(const FrRolloutArgs &a, int wv, int lane, double *Lk, double *Lw,
+                                          const double *Lmodel, const double *Lx0, int *Lflag, int *Lho, double *Lst)
 {
     int won = 0;
     if (lane == 0) {
         int z = 0;
-        won = __hip_atomic_compare_exchange_strong(Lho + HO_CLAIM, &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        won = __hip_atomic_compare_exchange_strong(Lho + HO_CLAIM, &z, wv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
     }
-    if (!__builtin_amdgcn_readfirstlane(won)) return;
+    if (!__builtin_amdgcn_readfirstlane(won)) return false;
     __hip_atomic_store(Lho + HO_REQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (a.costs_in_launch) signal_records(Lflag + 2);   // its own rows' records, for the queue
     int st = 0;
     for (int i = 0; i < WAIT_SPINS && st == 0; i++) {
         st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lho + HO_STATUS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (st == 0) __builtin_amdgcn_s_sleep(1);
     }
     if (st == 0 && lane == 0) note_wait_timeout(a);
-    if (__builtin_amdgcn_readfirstlane(st) != 1) return;
+    if (__builtin_amdgcn_readfirstlane(st) != 1) return true;
     coop_rows<CK, EN, true, 2>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4), lane,
                                gridDim.x * 4 + blockIdx.x, Lk, Lw, Lmodel, Lx0, Lho, Lst);
     if (a.costs_in_launch) signal_records(Lflag + 1);
+    return true;
 }
 
 // The update's state into LDS: from the launch's arguments with fused sampling, else from x0
@@ -2118,7 +2150,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false, false);
     }
 }
 
@@ -2132,7 +2164,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
-    __shared__ int Lflag[2];   // launch_costs: wave 0's and the fifth wave's records are stored
+    __shared__ int Lflag[3];   // launch_costs: wave 0's, the fifth wave's and the helper's records are stored
     __shared__ int Lho[HO_N];  // take_over / launch_costs: request, status, step, claim, cost counter
     __shared__ double Lst[64 * 3];   // take_over: the fifth wave's (q, qd, E) per lane
     const int wv = (int)(threadIdx.x >> 6);
@@ -2147,7 +2179,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int rk = kept_rank(a, lr);
     stage_body_table(a, Lmodel, 320);
     stage_x0(a, Lx0);
-    if (threadIdx.x < 2) Lflag[threadIdx.x] = 0;
+    if (threadIdx.x < 3) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < HO_N) Lho[threadIdx.x] = 0;
     if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
@@ -2168,8 +2200,12 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
         coop_rows<CK, EN, false, 0, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0,
                                           nullptr, nullptr, Lho + (wv == 0 ? HO_MSTEP : HO_SINK));
-        if (xr && wv != 0 && a.handover) take_over<CK, EN>(a, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr);
+        bool helper = false;
+        if (xr && wv != 0 && a.handover) helper = take_over<CK, EN>(a, wv, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr, helper);
+#ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective rows and draws)
+        if (a.trace && lane == 0) a.trace[4 * wblk + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
     } else if (xr) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
         const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;
