@@ -1913,6 +1913,8 @@ __device__ __forceinline__ void tail_draws(const FrRolloutArgs &a, int64_t lr0, 
 constexpr int CQ_HELPER = 0, CQ_HDRAW = ROWS_PER_WAVE, CQ_MATE = ROWS_PER_WAVE + 1, CQ_FIFTH = 2 * ROWS_PER_WAVE + 1,
               CQ_N = 3 * ROWS_PER_WAVE + 1;
 template <int CK, bool EN>
+__device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho);
+template <int CK, bool EN>
 __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
                                              int *Lho, bool xr, bool helper)
 {
@@ -1927,6 +1929,17 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
         if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
         if (!xr) return;
     }
+    cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+}
+
+// The workgroup's objective queue (launch_costs), worked by every main wave after its own share, by
+// the fifth wave once it handed its rows over, and by the two queue waves (5 and 6) that wait for it
+// on SIMDs 1 and 2: the last rows end on two SIMDs at once, and their eight objective passes then
+// run as one round instead of two.
+template <int CK, bool EN>
+__device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho)
+{
+    const int64_t w0 = (int64_t)blockIdx.x * 4;
 #pragma unroll 1
     for (int it = 0; it <= CQ_N; it++) {
         // every lane executes the add (lane 0 adds 1, the others 0), so no lane-dependent branch
@@ -2156,8 +2169,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and a fifth wave
 // for the extra rows [xbase, count) plus the folded filter() row (xrows of them in all).
+constexpr int XW = 7;   // fr_coop_x_kernel's waves: four main, the fifth, two queue waves
 template <int CK, bool EN>
-__global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
+__global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
 {
     constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
     __shared__ __attribute__((aligned(16))) double lds_kin[5 * ROWS_PER_WAVE * KS];
@@ -2175,23 +2189,23 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (a.trace && lane == 0 && wv < 4) a.trace[4 * (blockIdx.x * 4 + wv) + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
     const int64_t lr = wv < 4 ? (int64_t)(blockIdx.x * 4 + wv) * ROWS_PER_WAVE + rowi
-                              : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row
-    const int rk = kept_rank(a, lr);
-    stage_body_table(a, Lmodel, 320);
+                              : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row (waves < 5)
+    const int rk = wv < 5 ? kept_rank(a, lr) : 0x7FFFFFFF;
+    stage_body_table(a, Lmodel, 64 * XW);
     stage_x0(a, Lx0);
     if (threadIdx.x < 3) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < HO_N) Lho[threadIdx.x] = 0;
     if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
-        fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
+        if (wv < 5) fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
     }
     __syncthreads();
-    double *Lk = lds_kin + wrow * KS, *Lw = lds_scr + wrow * LDS_SCR;
+    double *Lk = lds_kin + (wv < 5 ? wrow : 0) * KS, *Lw = lds_scr + (wv < 5 ? wrow : 0) * LDS_SCR;
     const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the fifth wave has rows
     if (a.fuse_sample == 2) {
         if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the doubled SIMD
-        if (wv < 4 || xr) kept_rows_wave(a, lr, lane, rk);
+        if (wv < 4 || (wv == 4 && xr)) kept_rows_wave(a, lr, lane, rk);
     }
     if (wv < 4) {
         const int wblk = blockIdx.x * 4 + wv;
@@ -2206,7 +2220,7 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective rows and draws)
         if (a.trace && lane == 0) a.trace[4 * wblk + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    } else if (xr) {
+    } else if (wv == 4 && xr) {
         const int wblk = gridDim.x * 4 + blockIdx.x;
         const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;
         int ky = -1;
@@ -2220,6 +2234,9 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __builtin_amdgcn_s_waitcnt(0);
         if (!handed && a.costs_in_launch) signal_records(Lflag + 1);
         if (a.handover) __hip_atomic_store(Lho + HO_STATUS, handed ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (handed && a.costs_in_launch) cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+    } else if (wv > 4 && xr && a.costs_in_launch) {
+        cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
     }
 }
 
@@ -2252,8 +2269,8 @@ static void launch_k(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 template <int CK, bool EN>
 static void launch_x(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
-    static const unsigned pad = one_per_cu_pad(fr_coop_x_kernel<CK, EN>, 5);
-    hipLaunchKernelGGL((fr_coop_x_kernel<CK, EN>), dim3(nb), dim3(320), pad, s, a);
+    static const unsigned pad = one_per_cu_pad(fr_coop_x_kernel<CK, EN>, XW);
+    hipLaunchKernelGGL((fr_coop_x_kernel<CK, EN>), dim3(nb), dim3(64 * XW), pad, s, a);
 }
 
 template <int WPB, bool FROW>
