@@ -1579,15 +1579,25 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // step and, once another wave asks, leaves its lanes' (q, qd, E) in Lst and the step in
 // Lho[HO_STEP] and returns that step; 2 = the wave that took them over, resuming at that step (the
 // records up to it are stored).  Returns the step handed over, or -1.
-// PROG (the update launch's main waves): the wave stores its step into *Lprog at the top of each
-// step - wave 0 of a workgroup with a fifth wave into Lho[HO_MSTEP], the others into a sink - and
-// the fifth wave (HO == 1) raises its priority while it is behind wave 0, lowers it while ahead.
+// PROG (the update launch's main waves): main wave w stores its step into Lho[HO_P0 + w] at the
+// top of each step.  The fifth wave (HO == 1) raises its priority while it is not ahead of wave 0
+// by HO_BIAS steps, lowers it otherwise; optionally (HO_SELF) it hands its rows over by itself once
+// one of waves 1..3 nears its end, instead of waiting to be asked.
 // The two share a SIMD, whose arbiter otherwise issues the older wave (wave 0) first: the fifth
 // wave then reached only about a third of its horizon by the time the first other wave ended
 // (step 23 of 63 at 4096 x 64), and its remaining steps ran alone after that at one wave per SIMD
 // however they were placed.  At equal progress both have about 40 % left when another SIMD frees
 // up, and take_over runs those on two SIMDs at once.
-enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_MSTEP = 5, HO_SINK = 6, HO_N = 7 };
+enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_P0 = 8, HO_N = 12 };
+// Tuning, same box, three interleaved rounds (tools/gpu_r03_ho_ab.sh, profiles/r03_ho_tuning.txt):
+// bias 2 / 4 / 6 with self-handover off 0.2495 / 0.2471 / 0.2480 ms/update, bias 2 / 4 with it at
+// H - 3 0.2478 / 0.2481: within the boxes' noise, bias 4 without it the best.
+#ifndef HO_BIAS
+#define HO_BIAS 4   // the fifth wave keeps priority until it is this many steps ahead of wave 0
+#endif
+#ifndef HO_SELF
+#define HO_SELF 0   // it hands over by itself once one of waves 1..3 reaches step H - HO_SELF (0: never)
+#endif
 template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, int *Lho = nullptr,
@@ -1705,18 +1715,20 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
     uint64_t t_top = stamp(sq);
 #endif
-    int req = 0, mstep = 0;   // HO == 1: Lho[HO_REQ] and wave 0's step, read during the previous step
+    int req = 0, mstep = 0, hstep = 0;   // HO == 1, read during the previous step: Lho[HO_REQ], wave 0's
+                                         // step, the furthest step of waves 1..3
     for (int k = kb; k < H - 1; k++) {
         if constexpr (PROG) *Lprog = k;
         if constexpr (HO == 1) {
-            if (__builtin_amdgcn_readfirstlane(req)) {   // another wave resumes these rows at step k
+            if (__builtin_amdgcn_readfirstlane(req) || (HO_SELF > 0 && __builtin_amdgcn_readfirstlane(hstep) >= H - HO_SELF)) {
+                // another wave resumes these rows at step k
                 Lst[3 * lane] = q;
                 Lst[3 * lane + 1] = qd;
                 Lst[3 * lane + 2] = E;
                 Lho[HO_STEP] = k;
                 return k;
             }
-            if (k <= __builtin_amdgcn_readfirstlane(mstep) + 2) __builtin_amdgcn_s_setprio(3);
+            if (k <= __builtin_amdgcn_readfirstlane(mstep) + HO_BIAS) __builtin_amdgcn_s_setprio(3);
             else __builtin_amdgcn_s_setprio(0);
         }
         const double eps_l = eps_n, ub_l = ub_n;
@@ -1724,7 +1736,10 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
         if constexpr (HO == 1) {
             req = __hip_atomic_load(Lho + HO_REQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            mstep = __hip_atomic_load(Lho + HO_MSTEP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            typedef int i4 __attribute__((ext_vector_type(4)));
+            const i4 pg = *reinterpret_cast<const volatile i4 *>(Lho + HO_P0);   // the main waves' steps
+            mstep = pg.x;
+            hstep = max(pg.y, max(pg.z, pg.w));
         }
 #endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
@@ -2179,7 +2194,8 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
     __shared__ int Lflag[3];   // launch_costs: wave 0's, the fifth wave's and the helper's records are stored
-    __shared__ int Lho[HO_N];  // take_over / launch_costs: request, status, step, claim, cost counter
+    __shared__ __attribute__((aligned(16))) int Lho[HO_N];   // take_over / launch_costs: request, status, step,
+                                                               // claim, cost counter, the main waves' steps
     __shared__ double Lst[64 * 3];   // take_over: the fifth wave's (q, qd, E) per lane
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -2213,7 +2229,7 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         __builtin_amdgcn_s_setprio(MAIN_PRIO);
 #endif
         coop_rows<CK, EN, false, 0, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0,
-                                          nullptr, nullptr, Lho + (wv == 0 ? HO_MSTEP : HO_SINK));
+                                          nullptr, nullptr, Lho + HO_P0 + wv);
         bool helper = false;
         if (xr && wv != 0 && a.handover) helper = take_over<CK, EN>(a, wv, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
         if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr, helper);
