@@ -1101,6 +1101,7 @@ struct LaneConst {
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
     int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
+    int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
@@ -1552,11 +1553,29 @@ __device__ __forceinline__ double vreg(double x)
     asm("" : "+v"(x));   // not volatile: a volatile asm would end the scheduling region here
     return x;
 }
+template <bool EN>
 __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst &L, double q, double qd, const CoopKin &kin,
                                              double E)
 {
 #ifdef ABL_NOREC
     return;
+#endif
+#ifndef REC_SELECT
+    if constexpr (!EN) {
+        // Without the tank E = 0, and the dummy lanes 12..15 hold q = qd = 0: they store their pair
+        // over slots 30..31 (E, pad), which hold zeros either way, so no select builds their part of
+        // the record.  The EE / arm-mount / E slots are row-uniform values that every lane of the row
+        // stores alike (the same bytes to the same addresses): four stores instead of sixteen
+        // v_bfi_b32.
+        *reinterpret_cast<double2 *>(rp + L.rec_off) = double2{q, qd};
+        double2 *e = reinterpret_cast<double2 *>(rp + REC_EE);
+        e[0] = double2{kin.ee[0], kin.ee[1]};
+        e[1] = double2{kin.ee[2], kin.am[0]};
+        e[2] = double2{kin.am[1], kin.am[2]};
+        e[3] = double2{0.0, 0.0};
+        rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
+        return;
+    }
 #endif
     double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
     a0 = msel(L.m_j13, a0, kin.ee[2]);
@@ -1657,6 +1676,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         if (j == FR_NB - 1) anc &= ~(1 << (FR_NB - 2));   // finger 11 is not under finger 10
         asm volatile("" : "+v"(anc));
         L.anc = anc;
+        int ro = j < FR_NB ? 2 * j : REC_E;
+        asm volatile("" : "+v"(ro));
+        L.rec_off = ro;
 #pragma unroll
         for (int i = 0; i < 11; i++) {
             double d = ((anc >> i) & 1) ? 1.0 : 0.0;
@@ -1697,7 +1719,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     asm volatile("" : "+v"(nstride));
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
 #ifdef NO_EPS_PREFETCH
-    store_record(recp(0), j, L, q, qd, kin, E);
+    store_record<EN>(recp(0), j, L, q, qd, kin, E);
     for (int k = 0; k < H - 1; k++) {
         const double eps_l = np[(int64_t)k * nstride];
         const double ub_l = Up[min(k + ush, H - 1) * FR_C + jb];
@@ -1707,7 +1729,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
-    if constexpr (HO != 2) store_record(recp(0), j, L, q, qd, kin, E);
+    if constexpr (HO != 2) store_record<EN>(recp(0), j, L, q, qd, kin, E);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
 #endif
@@ -1796,7 +1818,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             const double power = bsum<0, FR_NB>(tau_l * qd + kin.pw, 1.0) + a.dt * bsum<0, 6>(pe, 1.0);
             E = smax(0.0, E + power * a.dt);
         }
-        store_record(recp(k + 1), j, L, q, qd, kin, E);
+        store_record<EN>(recp(k + 1), j, L, q, qd, kin, E);
 #ifdef ABL_SINCOS
         sq = q - q * q * q * (1.0 / 6.0);
         cq = 1.0 - q * q * 0.5;
