@@ -338,79 +338,70 @@ __device__ __forceinline__ int opaque_mask(bool c)
 }
 
 // ---- BEGIN generated by tools/gen_gj.py: mass-matrix solve helpers ----
-// m[i] = S_i . F for i = 0..10, S_i broadcast from lane i: eleven chains of six, round-robin
+// m[i] = S_i . F for i = 0..10, S_i broadcast from lane i: rows 0 and 1 are F[0] and F[1] (the
+// base's unit axes); rows 2..10 nine chains of six, round-robin
 __device__ __forceinline__ void column_dots(const double *S, const double *F, double *m)
 {
+    m[0] = F[0];
+    m[1] = F[1];
 #pragma unroll
-    for (int i = 0; i < 11; i++) m[i] = 0.0;
+    for (int i = 2; i < 11; i++) m[i] = 0.0;
     asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %11, %17 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %11, %17 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %11, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %11, %17 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %11, %17 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %11, %17 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %11, %17 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %12, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %18 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %12, %18 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %12, %18 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %12, %18 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %13, %19 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %13, %19 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %13, %19 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %13, %19 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %13, %19 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %13, %19 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %14, %20 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %14, %20 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %14, %20 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %20 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %14, %20 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %14, %20 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %14, %20 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %14, %20 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %15, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %15, %21 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %15, %21 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %15, %21 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %15, %21 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %15, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %15, %21 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %15, %21 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %15, %21 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %15, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %16, %22 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %16, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %16, %22 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %16, %22 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %16, %22 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %16, %22 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %16, %22 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %16, %22 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %16, %22 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        : "+&v"(m[0]), "+&v"(m[1]), "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
+        "v_fmac_f64_dpp %0, %9, %15 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %9, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %9, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %9, %15 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %9, %15 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %9, %15 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %9, %15 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %9, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %10, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %10, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %10, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %11, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %11, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %17 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %11, %17 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %11, %17 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %12, %18 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %12, %18 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %12, %18 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %13, %19 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %13, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %13, %19 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %13, %19 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %14, %20 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %14, %20 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %14, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %14, %20 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %14, %20 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %14, %20 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        : "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
         : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
 }
 // pivot 0: eleven FMAs with pivot 0's quotient, and pivot 1's quotient computed between them
@@ -1093,6 +1084,8 @@ struct CoopBody {
 struct LaneConst {
     int slot;       // LDS body slot (dummy for lanes 12..15)
     bool is_rz;
+    double rz, nrz;   // is_rz as 1.0 / 0.0 and its complement: the joint rotation's (cos, sin) by one FMA
+                      // and one multiply instead of four v_cndmask_b32
     int ka, kb;     // kinematic sum min(j, 8): S component x, y slot (S component or qd)
     bool vsum;      // the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
     // opaque lane masks (0 / -1) for msel, built once before the horizon loop
@@ -1118,8 +1111,8 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 #else
 #define FKSTAMP(i, dep)
 #endif
-    const double cz = L.is_rz ? cq : 1.0;
-    const double sz = L.is_rz ? sq : 0.0;
+    const double cz = __builtin_fma(L.rz, cq, L.nrz);   // cq on revolute lanes, 1 elsewhere
+    const double sz = L.rz * sq;                         // sq on revolute lanes, 0 elsewhere
     const double qprev = shr<1>(q);
     double D[9], p[3];
 #pragma unroll
@@ -1653,6 +1646,12 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     const double *M = Lmodel + (jl ? j : FR_NB) * MB;
     LaneConst L;
     L.is_rz = jl && FR_KIND[jb] == KIND_RZ;
+    {
+        double rz = L.is_rz ? 1.0 : 0.0, nrz = 1.0 - rz;
+        asm volatile("" : "+v"(rz), "+v"(nrz));   // kept in registers across the loop
+        L.rz = rz;
+        L.nrz = nrz;
+    }
     L.slot = jl ? j : FR_NB;
     {
         const int m = j < 9 ? j : 8;   // kinematic sum of the lane: a, b component nibbles
