@@ -1587,37 +1587,27 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // costs are not summed here: every step's record goes to HBM and fr_step_cost_kernel evaluates
 // the objective for all (rollout, step) pairs at once, a lane each, instead of 16 lanes of a row
 // repeating its row-uniform terms.
-// HO (handover, fr_coop_x_kernel): 1 = the fifth wave, which checks Lho[HO_REQ] at the top of each
-// step and, once another wave asks, leaves its lanes' (q, qd, E) in Lst and the step in
-// Lho[HO_STEP] and returns that step; 2 = the wave that took them over, resuming at that step (the
-// records up to it are stored).  Returns the step handed over, or -1.
-// PROG (the update launch's main waves): main wave w stores its step into Lho[HO_P0 + w] at the
-// top of each step.  The fifth wave (HO == 1) raises its priority while it is not ahead of wave 0
-// by HO_BIAS steps, lowers it otherwise; optionally (HO_SELF) it hands its rows over by itself once
-// one of waves 1..3 nears its end, instead of waiting to be asked.
-// The two share a SIMD, whose arbiter otherwise issues the older wave (wave 0) first: the fifth
-// wave then reached only about a third of its horizon by the time the first other wave ended
-// (step 23 of 63 at 4096 x 64), and its remaining steps ran alone after that at one wave per SIMD
-// however they were placed.  At equal progress both have about 40 % left when another SIMD frees
-// up, and take_over runs those on two SIMDs at once.
-enum { HO_REQ = 0, HO_STATUS = 1, HO_STEP = 2, HO_CLAIM = 3, HO_COST = 4, HO_P0 = 8, HO_N = 12 };
-// Tuning, same box, three interleaved rounds (tools/gpu_r03_ho_ab.sh, profiles/r03_ho_tuning.txt):
-// bias 2 / 4 / 6 with self-handover off 0.2495 / 0.2471 / 0.2480 ms/update, bias 2 / 4 with it at
-// H - 3 0.2478 / 0.2481: within the boxes' noise, bias 4 without it the best.
-#ifndef HO_BIAS
-#define HO_BIAS 4   // the fifth wave keeps priority until it is this many steps ahead of wave 0
-#endif
-#ifndef HO_SELF
-#define HO_SELF 0   // it hands over by itself once one of waves 1..3 reaches step H - HO_SELF (0: never)
-#endif
-template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false>
+// HO = 3 (the relay, fr_coop_x_kernel): the call runs steps [kb, ke) only.  kb > 0 resumes from
+// the lanes' (q, qd, E) the previous relay stage left in Lst at the top of step kb (the records up
+// to it are stored); ke < H - 1 leaves the state there for the next stage.
+//
+// The relay exists because R + 1 = S + 3 rows of four per wave need one wave more than there are
+// SIMDs: at 4096 x 64 the workgroup that holds the rows left over runs them in a fifth wave.  On
+// one SIMD beside a main wave the two shared its issue slots for the whole horizon; a single wave
+// leaves about 30 % of them idle (one VALU instruction per ~5.6 cycles against ~4 for two waves,
+// profiles/r03_ubench.txt), so a second wave with priority takes most of the slots it needs from
+// that slack.  The rows therefore travel: relay stage r (wave 4 + r, on SIMD r) runs a quarter of
+// the horizon at priority 3 and hands the state to the next stage through LDS, so each of the four
+// main waves loses about a quarter of what wave 0 alone lost before.
+enum { HO_STAGE = 0, HO_COST = 1, HO_N = 4 };
+template <int CK, bool EN, bool FROW, int HO = 0>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
-                                         const double *Lmodel, const double *Lx0, int *Lho = nullptr,
-                                         double *Lst = nullptr, int *Lprog = nullptr)
+                                         const double *Lmodel, const double *Lx0, double *Lst = nullptr, int kb = 0,
+                                         int ke = 0x7FFFFFFF)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
-    if (a.trace && lane == 0 && HO != 2) {
+    if (a.trace && lane == 0 && kb == 0) {
         uint32_t hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -1690,9 +1680,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
 
     double q, qd, E;
-    int kb = 0;   // first step of this call
-    if constexpr (HO == 2) {   // the state the fifth wave left at the top of step kb
-        kb = Lho[HO_STEP];
+    if (HO != 3) kb = 0;
+    const int kend = HO == 3 ? min(ke, H - 1) : H - 1;   // steps [kb, kend) in this call
+    if (kb > 0) {   // the state the previous relay stage left at the top of step kb
         q = Lst[3 * lane];
         qd = Lst[3 * lane + 1];
         E = Lst[3 * lane + 2];
@@ -1707,7 +1697,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
-    if constexpr (HO != 2)
+    if (kb == 0)
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
 
     // eps and U*_shifted of step k: loaded at the top of the step
@@ -1728,7 +1718,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
-    if constexpr (HO != 2) store_record<EN>(recp(0), j, L, q, qd, kin, E);
+    if (kb == 0) store_record<EN>(recp(0), j, L, q, qd, kin, E);
 #ifdef PHASE_FK
     uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
 #endif
@@ -1736,32 +1726,10 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
     uint64_t t_top = stamp(sq);
 #endif
-    int req = 0, mstep = 0, hstep = 0;   // HO == 1, read during the previous step: Lho[HO_REQ], wave 0's
-                                         // step, the furthest step of waves 1..3
-    for (int k = kb; k < H - 1; k++) {
-        if constexpr (PROG) *Lprog = k;
-        if constexpr (HO == 1) {
-            if (__builtin_amdgcn_readfirstlane(req) || (HO_SELF > 0 && __builtin_amdgcn_readfirstlane(hstep) >= H - HO_SELF)) {
-                // another wave resumes these rows at step k
-                Lst[3 * lane] = q;
-                Lst[3 * lane + 1] = qd;
-                Lst[3 * lane + 2] = E;
-                Lho[HO_STEP] = k;
-                return k;
-            }
-            if (k <= __builtin_amdgcn_readfirstlane(mstep) + HO_BIAS) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(0);
-        }
+    for (int k = kb; k < kend; k++) {
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
-        if constexpr (HO == 1) {
-            req = __hip_atomic_load(Lho + HO_REQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            typedef int i4 __attribute__((ext_vector_type(4)));
-            const i4 pg = *reinterpret_cast<const volatile i4 *>(Lho + HO_P0);   // the main waves' steps
-            mstep = pg.x;
-            hstep = max(pg.y, max(pg.z, pg.w));
-        }
 #endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
         // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
@@ -1829,6 +1797,11 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         ph[3] += t_end - t_fwd;
         t_top = t_end;
 #endif
+    }
+    if (HO == 3 && kend < H - 1) {   // the next relay stage resumes at step kend
+        Lst[3 * lane] = q;
+        Lst[3 * lane + 1] = qd;
+        Lst[3 * lane + 2] = E;
     }
     // the final step's dynamics are never observed (deviation 5)
 #ifdef PHASE_TRACE
@@ -1937,41 +1910,49 @@ __device__ __forceinline__ void tail_draws(const FrRolloutArgs &a, int64_t lr0, 
     }
 }
 
+// Whether launch row lr exists (a rollout of the shard or the folded filter() row)
+__device__ __forceinline__ bool row_live(const FrRolloutArgs &a, int64_t lr)
+{
+    return lr < a.count || (a.fcost != nullptr && lr == a.count);
+}
+
+// LDS flags of fr_coop_x_kernel (Lflag): main wave w's records are stored (w), the relay's rows
+// are done (LF_RELAY), main wave w's kept columns are copied (LF_KEPT + w: its rows' previous eps
+// is read, so their next draws may overwrite it).
+constexpr int LF_RELAY = 4, LF_KEPT = 5, LF_N = 9;
+
 // Main wave wv (0..3) of the workgroup after its horizon loop: the objective of its own rows and
-// the next update's draws for them.  xr (the workgroup has a fifth wave): wave 0 (the fifth wave's
-// SIMD-mate) and the wave that took the fifth wave's rows over (helper, take_over) leave their own
-// rows to a queue that every main wave of the workgroup works through once its own share is done,
-// one item at a time from the counter Lho[HO_COST]:
-//   0..3   the helper's rows (stored when it claimed: Lflag[2]),  4  the helper's draws,
-//   5..8   wave 0's rows (Lflag[0]),  9..12  the fifth wave's rows (Lflag[1]).
-// The helper's items exist only with a.handover, where some wave always claims (the first of
-// waves 1..3 to end its rows); they wait for the claim.
-constexpr int CQ_HELPER = 0, CQ_HDRAW = ROWS_PER_WAVE, CQ_MATE = ROWS_PER_WAVE + 1, CQ_FIFTH = 2 * ROWS_PER_WAVE + 1,
-              CQ_N = 3 * ROWS_PER_WAVE + 1;
+// the next update's draws for them.  In a workgroup with a relay (xr) the waves instead work
+// through the workgroup's objective queue (cost_queue), which the relay waves joined as soon as
+// their stages ended.
 template <int CK, bool EN>
 __device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho);
 template <int CK, bool EN>
 __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
-                                             int *Lho, bool xr, bool helper)
+                                             int *Lho, bool xr)
 {
     const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
-    if (xr && wv == 0) {
-        signal_records(Lflag);
-    } else if (!helper) {
-        __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-#pragma unroll 1
-        for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
-        if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
-        if (!xr) return;
+    if (xr) {
+        signal_records(Lflag + wv);
+        cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+        return;
     }
-    cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+    __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+    for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
+    if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// The workgroup's objective queue (launch_costs), worked by every main wave after its own share, by
-// the fifth wave once it handed its rows over, and by the two queue waves (5 and 6) that wait for it
-// on SIMDs 1 and 2: the last rows end on two SIMDs at once, and their eight objective passes then
-// run as one round instead of two.
+// The objective queue of a workgroup with a relay, one item at a time from the counter
+// Lho[HO_COST], taken by whichever of its eight waves is free (relay waves once their stage ended,
+// main waves after their loops):
+//   0..2    the next update's draws for main waves 1..3's rows (wave 0's are left to
+//           rank_draw_kernel, as the engine expects of the first wave of these workgroups),
+//   3..18   the main waves' rows, wave by wave,
+//   19..22  the relay's rows.
+// An item waits for its wave's flag; the draws go first, since they can run while the loops do.
+constexpr int CQ_DRAW = 0, CQ_MAIN = 3, CQ_RELAY = CQ_MAIN + 4 * ROWS_PER_WAVE, CQ_N = CQ_RELAY + ROWS_PER_WAVE;
 template <int CK, bool EN>
 __device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho)
 {
@@ -1983,56 +1964,66 @@ __device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, con
         const int n = __builtin_amdgcn_readfirstlane(
             __hip_atomic_fetch_add(Lho + HO_COST, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (n >= CQ_N) break;
-        if (n < CQ_MATE) {
-            if (!a.handover) continue;
-            const int hw = wait_nonzero(a, Lho + HO_CLAIM);   // the helper's wave index (1..3)
-            if (hw == 0) continue;
-            if (n < CQ_HDRAW) {
-                wait_records(a, Lflag + 2);
-                launch_row_cost<CK, EN>(a, (w0 + hw) * ROWS_PER_WAVE + n, lane, Lmodel);
-            } else if (a.ahead_noise) {
-                tail_draws(a, (w0 + hw) * ROWS_PER_WAVE, lane);
-            }
-        } else if (n < CQ_FIFTH) {
-            wait_records(a, Lflag);
-            launch_row_cost<CK, EN>(a, w0 * ROWS_PER_WAVE + (n - CQ_MATE), lane, Lmodel);
+        if (n < CQ_MAIN) {
+            if (!a.ahead_noise) continue;
+            const int w = 1 + n - CQ_DRAW;
+            wait_records(a, Lflag + LF_KEPT + w);
+            tail_draws(a, (w0 + w) * ROWS_PER_WAVE, lane);
+        } else if (n < CQ_RELAY) {
+            const int w = (n - CQ_MAIN) / ROWS_PER_WAVE, i = (n - CQ_MAIN) % ROWS_PER_WAVE;
+            const int64_t lr = (w0 + w) * ROWS_PER_WAVE + i;
+            if (!row_live(a, lr)) continue;
+            wait_records(a, Lflag + w);
+            launch_row_cost<CK, EN>(a, lr, lane, Lmodel);
         } else {
-            wait_records(a, Lflag + 1);
-            launch_row_cost<CK, EN>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - CQ_FIFTH), lane, Lmodel);
+            const int64_t lr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - CQ_RELAY);
+            if (!row_live(a, lr)) continue;
+            wait_records(a, Lflag + LF_RELAY);
+            launch_row_cost<CK, EN>(a, lr, lane, Lmodel);
         }
     }
 }
 
-// The doubled SIMD's relief (a.handover): the first of waves 1..3 to end its own rows claims the
-// fifth wave's rows, asks for them (Lho[HO_REQ]) and waits for the fifth wave's answer: 1 = it
-// stopped at the top of step Lho[HO_STEP] and left its state in Lst, 2 = it had already finished.
-// The claiming wave then runs the remaining steps alone on its SIMD, and the fifth wave's SIMD-mate
-// runs on alone too, each at one wave per SIMD instead of sharing the SIMD's issue slots.
-// Returns whether this wave claimed (its own rows' objective and draws then go to the workgroup's
-// queue, launch_costs).
+// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
+__device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
+
+// Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): waits for stage r - 1
+// (Lho[HO_STAGE] == r), runs its quarter of the horizon at priority 3 and passes the state on; the
+// last stage raises the relay's records flag.  Without a.handover wave 4 runs every step itself at
+// the main waves' priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage
+// ran (false: the previous stage never signalled, counted in Status::wait_timeouts).
 template <int CK, bool EN>
-__device__ __forceinline__ bool take_over(const FrRolloutArgs &a, int wv, int lane, double *Lk, double *Lw,
-                                          const double *Lmodel, const double *Lx0, int *Lflag, int *Lho, double *Lst)
+__device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
+                                            const double *Lmodel, const double *Lx0, int *Lflag, int *Lho, double *Lst)
 {
-    int won = 0;
-    if (lane == 0) {
-        int z = 0;
-        won = __hip_atomic_compare_exchange_strong(Lho + HO_CLAIM, &z, wv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+    const int H = a.H;
+    const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
+    const int wblk = gridDim.x * 4 + blockIdx.x;
+    if (!a.handover) {
+        coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
+    } else {
+        if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
+            int st = 0;
+            for (int i = 0; i < (1 << 22) && st < r; i++) {
+                st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lho + HO_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (st < r) __builtin_amdgcn_s_sleep(2);
+            }
+            if (st < r) {
+                if (lane == 0) note_wait_timeout(a);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_setprio(3);
+        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H), relay_step(r + 1, H));
+        __builtin_amdgcn_s_setprio(0);
+        if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
+            __builtin_amdgcn_s_waitcnt(0);
+            __hip_atomic_store(Lho + HO_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return true;
+        }
     }
-    if (!__builtin_amdgcn_readfirstlane(won)) return false;
-    __hip_atomic_store(Lho + HO_REQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (a.costs_in_launch) signal_records(Lflag + 2);   // its own rows' records, for the queue
-    int st = 0;
-    for (int i = 0; i < WAIT_SPINS && st == 0; i++) {
-        st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lho + HO_STATUS, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (st == 0) __builtin_amdgcn_s_sleep(1);
-    }
-    if (st == 0 && lane == 0) note_wait_timeout(a);
-    if (__builtin_amdgcn_readfirstlane(st) != 1) return true;
-    coop_rows<CK, EN, true, 2>(a, a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4), lane,
-                               gridDim.x * 4 + blockIdx.x, Lk, Lw, Lmodel, Lx0, Lho, Lst);
-    if (a.costs_in_launch) signal_records(Lflag + 1);
+    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(1, H) : -1;
+    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
     return true;
 }
 
@@ -2199,13 +2190,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false, false);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false);
     }
 }
 
-// The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and a fifth wave
-// for the extra rows [xbase, count) plus the folded filter() row (xrows of them in all).
-constexpr int XW = 7;   // fr_coop_x_kernel's waves: four main, the fifth, two queue waves
+// The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and, in the
+// workgroups with rows left over (the extra rows [xbase, count) plus the folded filter() row,
+// xrows of them, four per workgroup), four relay waves that carry those rows through the horizon
+// a quarter each (relay_stage), one per SIMD.  Elsewhere waves 4..7 exit at once.
+constexpr int XW = 8;
 template <int CK, bool EN>
 __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
 {
@@ -2214,14 +2207,12 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
-    __shared__ int Lflag[3];   // launch_costs: wave 0's, the fifth wave's and the helper's records are stored
-    __shared__ __attribute__((aligned(16))) int Lho[HO_N];   // take_over / launch_costs: request, status, step,
-                                                               // claim, cost counter, the main waves' steps
-    __shared__ double Lst[64 * 3];   // take_over: the fifth wave's (q, qd, E) per lane
+    __shared__ int Lflag[LF_N];   // records stored (main waves, relay), kept columns copied
+    __shared__ int Lho[HO_N];     // the relay's stage, the objective queue's counter
+    __shared__ double Lst[64 * 3];   // the relay's (q, qd, E) per lane between stages
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
-    const int wrow = wv * ROWS_PER_WAVE + rowi;
 #ifdef PRO_TRACE   // kernel entry per main wave (slot 3; coop_rows records the loop's start and end)
     if (a.trace && lane == 0 && wv < 4) a.trace[4 * (blockIdx.x * 4 + wv) + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -2230,50 +2221,38 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int rk = wv < 5 ? kept_rank(a, lr) : 0x7FFFFFFF;
     stage_body_table(a, Lmodel, 64 * XW);
     stage_x0(a, Lx0);
-    if (threadIdx.x < 3) Lflag[threadIdx.x] = 0;
+    if (threadIdx.x < LF_N) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < HO_N) Lho[threadIdx.x] = 0;
-    if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the fifth wave's rows
+    if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the relay's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
         if (wv < 5) fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
     }
     __syncthreads();
-    double *Lk = lds_kin + (wv < 5 ? wrow : 0) * KS, *Lw = lds_scr + (wv < 5 ? wrow : 0) * LDS_SCR;
-    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the fifth wave has rows
+    // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
+    const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
+    double *Lk = lds_kin + slot * KS, *Lw = lds_scr + slot * LDS_SCR;
+    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
     if (a.fuse_sample == 2) {
-        if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the doubled SIMD
+        if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the SIMD of the relay's first stage
         if (wv < 4 || (wv == 4 && xr)) kept_rows_wave(a, lr, lane, rk);
     }
     if (wv < 4) {
+        if (xr) {   // the queue's draws for this wave's rows may now overwrite their previous eps
+            __builtin_amdgcn_s_waitcnt(0);
+            __hip_atomic_store(Lflag + LF_KEPT + wv, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (a.handover) __builtin_amdgcn_s_setprio(1);   // above the queue's early work, below the relay
+        }
         const int wblk = blockIdx.x * 4 + wv;
-#ifdef MAIN_PRIO
-        __builtin_amdgcn_s_setprio(MAIN_PRIO);
-#endif
-        coop_rows<CK, EN, false, 0, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0,
-                                          nullptr, nullptr, Lho + HO_P0 + wv);
-        bool helper = false;
-        if (xr && wv != 0 && a.handover) helper = take_over<CK, EN>(a, wv, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr, helper);
+        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
+        __builtin_amdgcn_s_setprio(0);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr);
 #ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective rows and draws)
         if (a.trace && lane == 0) a.trace[4 * wblk + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    } else if (wv == 4 && xr) {
-        const int wblk = gridDim.x * 4 + blockIdx.x;
-        const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;
-        int ky = -1;
-        if (a.handover) ky = coop_rows<CK, EN, true, 1>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lho, Lst);
-        else coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
-        const uint64_t hm = __ballot(ky >= 0);   // the live rows stop at the same step
-        const bool handed = hm != 0;
-        if (blockIdx.x == 0 && lane == 0)
-            const_cast<Status *>(a.status)->handover = handed ? __builtin_amdgcn_readlane(ky, __builtin_ffsll((long long)hm) - 1) : -1;
-        // records (and the handed-over state) stored before the answer / the flag
-        __builtin_amdgcn_s_waitcnt(0);
-        if (!handed && a.costs_in_launch) signal_records(Lflag + 1);
-        if (a.handover) __hip_atomic_store(Lho + HO_STATUS, handed ? 1 : 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (handed && a.costs_in_launch) cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
-    } else if (wv > 4 && xr && a.costs_in_launch) {
-        cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+    } else if (xr) {
+        if (wv == 4 || a.handover) relay_stage<CK, EN>(a, wv - 4, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
+        if (a.costs_in_launch) cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
     }
 }
 
@@ -2345,9 +2324,9 @@ static bool costs_in_launch_enabled()
 
 bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
 
-// take_over in fr_coop_x_kernel (the default: 0.2874 -> 0.2694 ms/update at 4096 x 64, two
-// interleaved rounds on one box, profiles/r03_handover_ab/); MPPI_HANDOVER=0 leaves the fifth
-// wave's rows on its SIMD (A/B; read per update: tests switch it in-process)
+// The relay in fr_coop_x_kernel (relay_stage, the default); MPPI_HANDOVER=0 leaves the rows left
+// over on wave 4 for the whole horizon, beside main wave 0 (A/B; read per update: tests switch it
+// in-process)
 static bool handover_enabled()
 {
     const char *e = getenv("MPPI_HANDOVER");
