@@ -1599,11 +1599,11 @@ static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC
 // that slack.  The rows therefore travel: relay stage r (wave 4 + r, on SIMD r) runs a quarter of
 // the horizon at priority 3 and hands the state to the next stage through LDS, so each of the four
 // main waves loses about a quarter of what wave 0 alone lost before.
-enum { HO_STAGE = 0, HO_COST = 1, HO_N = 4 };
-template <int CK, bool EN, bool FROW, int HO = 0>
+// PROG: the wave stores its step into *Lprog at the top of each step (the objective chunks, cost_work).
+template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, double *Lst = nullptr, int kb = 0,
-                                         int ke = 0x7FFFFFFF)
+                                         int ke = 0x7FFFFFFF, int *Lprog = nullptr)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1727,6 +1727,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     uint64_t t_top = stamp(sq);
 #endif
     for (int k = kb; k < kend; k++) {
+        if constexpr (PROG) __hip_atomic_store(Lprog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
@@ -1916,27 +1917,136 @@ __device__ __forceinline__ bool row_live(const FrRolloutArgs &a, int64_t lr)
     return lr < a.count || (a.fcost != nullptr && lr == a.count);
 }
 
-// LDS flags of fr_coop_x_kernel (Lflag): main wave w's records are stored (w), the relay's rows
-// are done (LF_RELAY), main wave w's kept columns are copied (LF_KEPT + w: its rows' previous eps
-// is read, so their next draws may overwrite it).
+// ---- the objective in chunks, beside the horizon loops (fr_coop_x_kernel) ----------------------
+// One wave per SIMD leaves about 30 % of its issue slots idle (r03_ubench).  fr_coop_x_kernel fills
+// them with a second wave per SIMD that evaluates the objective while the rows still run: the step
+// costs of a row group (a main wave's four rows, or the relay's) in chunks of CH steps, lane =
+// (row, step), as soon as the chunk's records are stored.  Those waves run at priority 0, the main
+// waves at 1.  Each chunk's 64 step costs go to LDS (Lcs); the wave that completes a group's last
+// chunk sums every row's step costs in step order (the reference's J += cost, mppi.cpp:322-337:
+// the same additions as rollout_cost) and writes J.  A main wave stores its loop step into LDS
+// (Lq[Q_PROG + g]) at the top of every step.  Seeing step p there means the wave has waited, in
+// step p - 1, for the eps loads it issued in step p - 2 after storing record p - 2; vector memory
+// operations complete in order on gfx9 (one vmcnt for loads and stores), so records up to p - 2
+// are complete.  A chunk is taken when records up to its last are complete with a step to spare
+// (p >= last + 3), and the last chunk after the wave's loop (its flag, behind s_waitcnt 0).  Chunks
+// of CH = 16 records are whole 128-byte lines (16 x 336 B = 42 lines, rows 21504 B apart), so no
+// line a chunk reads is written after it.  The relay's rows are taken after their last stage.
+constexpr int CH = 16;          // steps per chunk
+constexpr int HC_MAX = 128;     // the horizon bound of the objective in this launch (Lcs)
+// LDS words (Lq): the main waves' steps, the groups' next chunk to take and chunks completed, the
+// relay's stage
+enum { Q_PROG = 0, Q_NEXT = 4, Q_DONE = 9, Q_STAGE = 14, Q_N = 16 };
+// LDS flags (Lflag): main wave g's records are stored (g), the relay's rows are done (LF_RELAY),
+// main wave g's kept columns are copied (LF_KEPT + g: its rows' previous eps is read, so their next
+// draws may overwrite it)
 constexpr int LF_RELAY = 4, LF_KEPT = 5, LF_N = 9;
 
-// Main wave wv (0..3) of the workgroup after its horizon loop: the objective of its own rows and
-// the next update's draws for them.  In a workgroup with a relay (xr) the waves instead work
-// through the workgroup's objective queue (cost_queue), which the relay waves joined as soon as
-// their stages ended.
-template <int CK, bool EN>
-__device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho);
-template <int CK, bool EN>
-__device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel, int *Lflag,
-                                             int *Lho, bool xr)
+__device__ __forceinline__ int lds_read(int *w)
 {
-    const int64_t w0 = (int64_t)blockIdx.x * 4;   // the workgroup's first main wave
-    if (xr) {
-        signal_records(Lflag + wv);
-        cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
-        return;
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4)
+__device__ __forceinline__ int64_t group_row0(const FrRolloutArgs &a, int g)
+{
+    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
+}
+// whether chunk c of group g can be read: its records are complete
+__device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
+{
+    if (g == 4) return lds_read(Lflag + LF_RELAY) != 0;
+    const int last = min((c + 1) * CH, a.H) - 1;
+    if (last < a.H - 1 && lds_read(Lq + Q_PROG + g) >= last + 3) return true;
+    return lds_read(Lflag + g) != 0;
+}
+
+// The step costs of chunk c of group g into Lcs; the pass that completes the group sums its rows
+template <int CK, bool EN>
+__device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c, int lane, const double *Lmodel, double *Lcs,
+                                          int *Lq)
+{
+    const int H = a.H, nch = (H + CH - 1) / CH;
+    const int i = lane >> 4, k = c * CH + (lane & 15);
+    const int64_t lr0 = group_row0(a, g), lr = lr0 + i;
+    const bool rl = row_live(a, lr), live = rl && k < H;
+    const bool frow = a.fcost != nullptr && lr == a.count;
+    const int64_t lrv = rl ? lr : lr0;   // any live row's records when unused
+    const double *rec = frow ? a.frec : a.rec + lrv * H * FR_NREC;
+    const StepConst *stp = frow ? a.fsteps : a.steps;
+    const int kk = live ? k : 0;
+    const double cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_NREC, Lmodel + T_LO);
+    if (live) Lcs[(g * ROWS_PER_WAVE + i) * HC_MAX + k] = cs;
+    // the stores before the count: the wave that completes the group reads every chunk's costs
+    const int n = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_fetch_add(Lq + Q_DONE + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (n + 1 != nch) return;
+    if (lane < ROWS_PER_WAVE) {
+        const int64_t r = lr0 + lane;
+        if (row_live(a, r)) {
+            const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
+            double J = 0.0;
+            for (int q = 0; q < H; q++) J += cr[q];
+            J = isnan(J) ? (double)NAN : J;
+            if (a.fcost != nullptr && r == a.count) {
+                if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
+            } else {
+                a.cost_out[a.begin + r] = J;
+                mppi_cost::fold_cost_stats(a.stats, J, r);
+            }
+        }
     }
+}
+
+// A wave's objective work: chunks of any group, its own group (first) first, each taken from the
+// group's counter when it is ready (a chunk taken just as another wave took the one before it
+// waits for its records); returns once every chunk is taken.  Bounded.
+template <int CK, bool EN>
+__device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int ng, int lane, const double *Lmodel,
+                                         double *Lcs, int *Lflag, int *Lq)
+{
+    const int nch = (a.H + CH - 1) / CH;
+#pragma unroll 1
+    for (int spin = 0; spin < WAIT_SPINS; spin++) {
+        bool left = false, did = false;
+#pragma unroll 1
+        for (int d = 0; d < ng && !did; d++) {
+            const int g = first + d < ng ? first + d : first + d - ng;
+            const int c0 = lds_read(Lq + Q_NEXT + g);
+            if (c0 >= nch) continue;
+            left = true;
+            if (!chunk_ready(a, g, c0, Lflag, Lq)) continue;
+            // every lane executes the add (lane 0 adds 1): no lane-dependent branch around it
+            const int c = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(Lq + Q_NEXT + g, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (c >= nch) continue;
+            int w = 0;
+            while (!chunk_ready(a, g, c, Lflag, Lq) && w < WAIT_SPINS) {
+                __builtin_amdgcn_s_sleep(4);
+                w++;
+            }
+            if (w == WAIT_SPINS && lane == 0) note_wait_timeout(a);
+            cost_chunk<CK, EN>(a, g, c, lane, Lmodel, Lcs, Lq);
+            did = true;
+        }
+        if (!left) return;
+        if (!did) __builtin_amdgcn_s_sleep(8);
+    }
+    if (lane == 0) note_wait_timeout(a);
+}
+
+// The next update's draws for main wave g's rows, once its kept columns are copied
+__device__ __forceinline__ void group_draws(const FrRolloutArgs &a, int g, int lane, int *Lflag)
+{
+    wait_records(a, Lflag + LF_KEPT + g);
+    tail_draws(a, group_row0(a, g), lane);
+}
+
+// fr_coop_kernel's four-wave launch (no rows left over): each main wave evaluates its own rows'
+// objective after its loop (rollout_cost, a pass per row, lane = step) and makes their next draws
+template <int CK, bool EN>
+__device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel)
+{
+    const int64_t w0 = (int64_t)blockIdx.x * 4;
     __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -1944,57 +2054,19 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// The objective queue of a workgroup with a relay, one item at a time from the counter
-// Lho[HO_COST], taken by whichever of its eight waves is free (relay waves once their stage ended,
-// main waves after their loops):
-//   0..2    the next update's draws for main waves 1..3's rows (wave 0's are left to
-//           rank_draw_kernel, as the engine expects of the first wave of these workgroups),
-//   3..18   the main waves' rows, wave by wave,
-//   19..22  the relay's rows.
-// An item waits for its wave's flag; the draws go first, since they can run while the loops do.
-constexpr int CQ_DRAW = 0, CQ_MAIN = 3, CQ_RELAY = CQ_MAIN + 4 * ROWS_PER_WAVE, CQ_N = CQ_RELAY + ROWS_PER_WAVE;
-template <int CK, bool EN>
-__device__ __forceinline__ void cost_queue(const FrRolloutArgs &a, int lane, const double *Lmodel, int *Lflag, int *Lho)
-{
-    const int64_t w0 = (int64_t)blockIdx.x * 4;
-#pragma unroll 1
-    for (int it = 0; it <= CQ_N; it++) {
-        // every lane executes the add (lane 0 adds 1, the others 0), so no lane-dependent branch
-        // surrounds the atomic; lane 0's old value is the item
-        const int n = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(Lho + HO_COST, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (n >= CQ_N) break;
-        if (n < CQ_MAIN) {
-            if (!a.ahead_noise) continue;
-            const int w = 1 + n - CQ_DRAW;
-            wait_records(a, Lflag + LF_KEPT + w);
-            tail_draws(a, (w0 + w) * ROWS_PER_WAVE, lane);
-        } else if (n < CQ_RELAY) {
-            const int w = (n - CQ_MAIN) / ROWS_PER_WAVE, i = (n - CQ_MAIN) % ROWS_PER_WAVE;
-            const int64_t lr = (w0 + w) * ROWS_PER_WAVE + i;
-            if (!row_live(a, lr)) continue;
-            wait_records(a, Lflag + w);
-            launch_row_cost<CK, EN>(a, lr, lane, Lmodel);
-        } else {
-            const int64_t lr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (n - CQ_RELAY);
-            if (!row_live(a, lr)) continue;
-            wait_records(a, Lflag + LF_RELAY);
-            launch_row_cost<CK, EN>(a, lr, lane, Lmodel);
-        }
-    }
-}
-
 // Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
 __device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
 
-// Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): waits for stage r - 1
-// (Lho[HO_STAGE] == r), runs its quarter of the horizon at priority 3 and passes the state on; the
+// Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): makes the next
+// update's draws for main wave r's rows (r > 0; wave 0's are left to rank_draw_kernel, as the
+// engine expects of the first wave of these workgroups), waits for stage r - 1 (Lq[Q_STAGE] == r),
+// runs its quarter of the horizon at priority 3 and passes the state on; the
 // last stage raises the relay's records flag.  Without a.handover wave 4 runs every step itself at
 // the main waves' priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage
 // ran (false: the previous stage never signalled, counted in Status::wait_timeouts).
 template <int CK, bool EN>
 __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
-                                            const double *Lmodel, const double *Lx0, int *Lflag, int *Lho, double *Lst)
+                                            const double *Lmodel, const double *Lx0, int *Lflag, int *Lq, double *Lst)
 {
     const int H = a.H;
     const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
@@ -2002,10 +2074,11 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
     if (!a.handover) {
         coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
     } else {
+        if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
         if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
             int st = 0;
             for (int i = 0; i < (1 << 22) && st < r; i++) {
-                st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lho + HO_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
                 if (st < r) __builtin_amdgcn_s_sleep(2);
             }
             if (st < r) {
@@ -2016,9 +2089,12 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
         __builtin_amdgcn_s_setprio(3);
         coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H), relay_step(r + 1, H));
         __builtin_amdgcn_s_setprio(0);
+#ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
+        if (a.trace && blockIdx.x == 0 && lane == 0) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
         if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
-            __hip_atomic_store(Lho + HO_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(Lq + Q_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             return true;
         }
     }
@@ -2190,14 +2266,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, nullptr, nullptr, false);
+        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel);
     }
 }
 
-// The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and, in the
-// workgroups with rows left over (the extra rows [xbase, count) plus the folded filter() row,
-// xrows of them, four per workgroup), four relay waves that carry those rows through the horizon
-// a quarter each (relay_stage), one per SIMD.  Elsewhere waves 4..7 exit at once.
+// The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and four more
+// waves, one per SIMD beside each main wave, that evaluate the objective in chunks while the rows
+// run (cost_work) and make the next update's draws.  In the workgroups with rows left over (the
+// extra rows [xbase, count) plus the folded filter() row, xrows of them, four per workgroup) those
+// four waves first carry the rows left over through the horizon, a quarter each (relay_stage).
 constexpr int XW = 8;
 template <int CK, bool EN>
 __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_x_kernel(FrRolloutArgs a)
@@ -2207,9 +2284,10 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ __attribute__((aligned(16))) double lds_scr[5 * ROWS_PER_WAVE * LDS_SCR];
     __shared__ double Lmodel[LDS_MODEL];
     __shared__ double Lx0[MAX_X];
-    __shared__ int Lflag[LF_N];   // records stored (main waves, relay), kept columns copied
-    __shared__ int Lho[HO_N];     // the relay's stage, the objective queue's counter
+    __shared__ int Lflag[LF_N];      // records stored (main waves, relay), kept columns copied
+    __shared__ int Lq[Q_N];          // the main waves' steps, chunk counters, the relay's stage
     __shared__ double Lst[64 * 3];   // the relay's (q, qd, E) per lane between stages
+    __shared__ double Lcs[5 * ROWS_PER_WAVE * HC_MAX];   // step costs of the groups' rows
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
@@ -2222,37 +2300,50 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     stage_body_table(a, Lmodel, 64 * XW);
     stage_x0(a, Lx0);
     if (threadIdx.x < LF_N) Lflag[threadIdx.x] = 0;
-    if (threadIdx.x < HO_N) Lho[threadIdx.x] = 0;
+    if (threadIdx.x < Q_N) Lq[threadIdx.x] = threadIdx.x < Q_NEXT ? -1 : 0;
     if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the relay's rows
         const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
         const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
         if (wv < 5) fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
     }
+    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
+    const int ng = xr ? 5 : 4;   // row groups of the objective
+    if (!xr && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
     __syncthreads();
     // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
     const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
     double *Lk = lds_kin + slot * KS, *Lw = lds_scr + slot * LDS_SCR;
-    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
     if (a.fuse_sample == 2) {
         if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the SIMD of the relay's first stage
         if (wv < 4 || (wv == 4 && xr)) kept_rows_wave(a, lr, lane, rk);
     }
+    const bool cil = a.costs_in_launch != 0;
     if (wv < 4) {
-        if (xr) {   // the queue's draws for this wave's rows may now overwrite their previous eps
+        if (cil) {   // the next draws for this wave's rows may now overwrite their previous eps
             __builtin_amdgcn_s_waitcnt(0);
             __hip_atomic_store(Lflag + LF_KEPT + wv, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (a.handover) __builtin_amdgcn_s_setprio(1);   // above the queue's early work, below the relay
+            __builtin_amdgcn_s_setprio(1);   // above the objective's waves, below the relay
         }
         const int wblk = blockIdx.x * 4 + wv;
-        coop_rows<CK, EN, false>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0);
+        coop_rows<CK, EN, false, 0, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, Lk, Lw, Lmodel, Lx0,
+                                          nullptr, 0, 0x7FFFFFFF, Lq + Q_PROG + wv);
         __builtin_amdgcn_s_setprio(0);
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel, Lflag, Lho, xr);
-#ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective rows and draws)
+        if (cil) {
+            signal_records(Lflag + wv);
+            cost_work<CK, EN>(a, wv, ng, lane, Lmodel, Lcs, Lflag, Lq);
+        }
+#ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective work)
         if (a.trace && lane == 0) a.trace[4 * wblk + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    } else if (xr) {
-        if (wv == 4 || a.handover) relay_stage<CK, EN>(a, wv - 4, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lho, Lst);
-        if (a.costs_in_launch) cost_queue<CK, EN>(a, lane, Lmodel, Lflag, Lho);
+    } else {
+        const int s = wv - 4;   // this wave's SIMD
+        const bool relay = xr && (s == 0 || a.handover);
+        if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
+        if (!cil) return;
+        // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
+        // rows of a workgroup with rows left over are left to rank_draw_kernel)
+        if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
+        cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
 }
 
@@ -2372,7 +2463,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.xbase = groups * WG_ROWS;
     a.xrows = xrows;
     *folded = frow;
-    a.costs_in_launch = costs_in_launch_enabled() ? 1 : 0;
+    a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;   // Lcs holds HC_MAX steps
     a.handover = handover_enabled() ? 1 : 0;
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments

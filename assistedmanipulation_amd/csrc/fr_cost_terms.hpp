@@ -251,6 +251,23 @@ __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &
     else return sc.gamma_k * assisted_manipulation_cost<EN, JS>(Cs, sc, r, Lj, src);
 }
 
+// gamma_k times the objective at the step record rk (FR_NREC doubles, 16-byte aligned)
+template <int CK, bool EN, int JS = JT_STRIDE>
+__device__ __forceinline__ double record_step_cost(const DevCost &Cs, const StepConst &sc, const double *rk, const double *Lj)
+{
+    constexpr int NREC2 = FR_NREC / 2;
+    double r[FR_NREC];
+    const double2 *src = reinterpret_cast<const double2 *>(rk);
+    constexpr int NLOAD = CK == CK_TRACK_POINT ? NREC2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
+#pragma unroll
+    for (int i = 0; i < NLOAD; i++) {
+        const double2 v = src[i];
+        r[2 * i] = v.x;
+        r[2 * i + 1] = v.y;
+    }
+    return step_cost<CK, EN, JS>(Cs, sc, r, Lj, src);
+}
+
 // J of one rollout from its H step records (rollout-major, FR_NREC doubles each) by one wave:
 // lane k evaluates step k (64 steps a pass) and the wave sums the step costs in step order, as the
 // reference accumulates J += cost (mppi.cpp:322-337); a NaN step makes the sum NaN (the reference's
@@ -264,16 +281,7 @@ __device__ __forceinline__ double rollout_cost(const DevCost &Cs, const StepCons
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
-        double r[FR_NREC];
-        const double2 *src = reinterpret_cast<const double2 *>(rec) + (int64_t)k * NREC2;
-        constexpr int NLOAD = CK == CK_TRACK_POINT ? NREC2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
-#pragma unroll
-        for (int i = 0; i < NLOAD; i++) {
-            const double2 v = src[i];
-            r[2 * i] = v.x;
-            r[2 * i + 1] = v.y;
-        }
-        const double c = step_cost<CK, EN, JS>(Cs, stp[k], r, Lj, src);
+        const double c = record_step_cost<CK, EN, JS>(Cs, stp[k], rec + (int64_t)k * (2 * NREC2), Lj);
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
     }
     return isnan(J) ? (double)NAN : J;

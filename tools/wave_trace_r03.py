@@ -21,3 +21,5 @@ print("block 0 waves: loop end", ["%.1f" % us(le[w]) for w in range(4)], "wave e
 fx = rec[nmain]
 print("fifth wave rows: start %.1f end %.1f" % (us(fx[0]), us(fx[1])))
 print("launch end (last wave end) %.1f us" % max(us(we).max(), us(fx[1])))
+if len(sys.argv) > 3 and sys.argv[3] == "relay":   # relay builds: block 0's stage ends in the next slot
+    print("relay stage ends:", ["%.1f" % us(x) for x in rec[nmain + 1]])
