@@ -1070,6 +1070,11 @@ void mppi_destroy(mppi_handle *h)
     delete h;
 }
 
+// The sharded update path (cost vector and partial gradient all-reduced, the weights from the
+// all-reduced costs): world > 1, or a one-rank communicator (mppi_comm_init with world 1), which
+// runs the same path through RCCL on one GPU
+static inline bool sharded(const mppi_handle *h) { return h->world > 1 || h->comm != nullptr; }
+
 mppi_status mppi_set_shard(mppi_handle *h, int world, int rank)
 {
     if (!h) return MPPI_ERR_INVALID;
@@ -1098,7 +1103,6 @@ mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char uniqu
     if (!h) return MPPI_ERR_INVALID;
     mppi_status st = mppi_set_shard(h, world, rank);
     if (st != MPPI_OK) return st;
-    if (world == 1) return MPPI_OK;
     ncclUniqueId id;
     std::memcpy(&id, unique_id, 128);
     HIP_TRY(hipSetDevice(h->device));
@@ -1370,14 +1374,14 @@ void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 // kernel (CostStats); sharded ones see only their own costs there and reduce after the all-reduce.
 static bool cost_stats_used(const mppi_handle *h)
 {
-    return h->world == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
+    return !sharded(h) && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
 }
 
 // Where an update's rollout costs go: d_costs, or the rank's zero-padded local vector that the
 // engine's own all-reduce sums into d_costs
 static double *rollout_costs_out(const mppi_handle *h)
 {
-    return (h->world > 1 && h->comm) ? h->d_costs_local : h->d_costs;
+    return h->comm ? h->d_costs_local : h->d_costs;
 }
 
 static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
@@ -1647,7 +1651,7 @@ static FinishArgs finish_args(mppi_handle *h)
     f.status = h->d_status;
     f.status_w = h->d_status;
     f.gsplit = h->d_gsplit;
-    f.ns = h->world > 1 ? 0 : GRAD_SPLIT;
+    f.ns = sharded(h) ? 0 : GRAD_SPLIT;
     f.gpart = h->d_gpart;
     f.gradient = h->d_grad;
     f.Ushift = h->d_Us;
@@ -1700,7 +1704,7 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     h->gargs.wg = w;
     if (h->graph_dry) return MPPI_OK;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
-    HIP_TRY(launch_weights_gradient(w, h->d_gpart, h->world > 1, h->stream));
+    HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
     return MPPI_OK;
 }
 
@@ -1838,7 +1842,7 @@ mppi_status mppi_update_phase3(mppi_handle *h)
 // the eager launches.
 static bool graph_eligible(const mppi_handle *h)
 {
-    if (!h->graph_mode || h->world != 1 || h->timing != 0 || h->d_trace || h->host_trace) return false;
+    if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
     if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
     if (h->fc.type != FC_NONE || h->sg_window > 0 || h->S > RANK_TILED_MAX) return false;
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
@@ -1943,13 +1947,13 @@ mppi_status mppi_update(mppi_handle *h, const double *state, double time)
     if (h && state && graph_eligible(h)) return update_graph(h, state, time);
     mppi_status st = mppi_update_phase1(h, state, time);
     if (st != MPPI_OK) return st;
-    if (h->world > 1) {
+    if (sharded(h)) {
         if (!h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
         NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R, ncclDouble, ncclSum, h->comm, h->stream));
     }
     st = mppi_update_phase2(h);
     if (st != MPPI_OK) return st;
-    if (h->world > 1)
+    if (sharded(h))
         NCCL_TRY(ncclAllReduce(h->d_gpart, h->d_gpart, (size_t)(h->H * h->C), ncclDouble, ncclSum, h->comm, h->stream));
     return mppi_update_phase3(h);
 }
