@@ -2406,11 +2406,8 @@ hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, doub
 // separate fr_step_cost_kernel (A/B)
 static bool costs_in_launch_enabled()
 {
-    static const bool on = [] {   // read once: getenv scans the environment on every call
-        const char *e = getenv("MPPI_COSTS_IN_LAUNCH");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+    const char *e = getenv("MPPI_COSTS_IN_LAUNCH");   // per update: tests switch it in-process
+    return !(e && e[0] == '0');
 }
 
 bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
