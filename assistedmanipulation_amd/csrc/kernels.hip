@@ -808,8 +808,10 @@ __device__ __forceinline__ double wave_sum(double v) { return mppi_dev::wave_sum
 // carries four of its sixteen waves lane for lane, so the butterflies pair the same values and
 // every block holds the same bits.  The normaliser is not needed here: blocks (0, s) write e_r of
 // slice s of all R rollouts to wexp and its sum to Status::tsplit[s] (the finish kernel adds them,
-// the host divides for get_weights), so no block evaluates all R exponentials.  The block's eps
-// loads are issued first and land during the reductions.  Block (0, 0) writes the status words.
+// the host divides for get_weights), so no block evaluates all R exponentials; unsharded, slice s
+// is block (0, s)'s own rollout range, so its gradient loop makes those e_r (same order, same
+// bits) and no second pass runs.  The block's eps and cost loads are issued first, together, and
+// land during the reductions.  Block (0, 0) writes the status words.
 constexpr int WV = 16;       // waves of the 1024-thread reduction order
 constexpr int WU = 8;        // costs per (virtual) thread and pass
 constexpr int NV = WV / 4;   // virtual waves per real wave
@@ -913,13 +915,20 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     const int64_t chunk = (a.count + ns - 1) / ns;
     const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
     double ne[GR][C];   // eps of rollouts r0 + t + 256 m (row 0 stands in past r1, unused)
+    double cpre[GR];    // their costs (LARGE: e_r), loaded with the eps: one memory trip, not two
 #pragma unroll
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
         const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C;
 #pragma unroll
         for (int c = 0; c < C; c++) ne[m][c] = n[c];
+        const int64_t gi = a.begin + (r < r1 ? r : 0);
+        if constexpr (LARGE) cpre[m] = a.wexp[gi];
+        else cpre[m] = a.cost[gi];
     }
+    // unsharded, the normaliser slice of block (0, s) is its own rollout range [r0, r1): its e_r come
+    // from the gradient loop below, in the same per-thread order as the separate slice pass
+    const bool own_slice = !LARGE && k == 0 && a.begin == 0 && a.count == R;
     double minimum, maximum, valid, total;
     if constexpr (LARGE) {
         if (rw == 0) {
@@ -1009,7 +1018,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
     if constexpr (LARGE) {   // the normaliser is known: one partial carries it
         if (k == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
-    } else if (k == 0) {   // slice s of [0, R): e_r and its sum
+    } else if (k == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
         const int64_t wc = (R + ns - 1) / ns, w0 = (int64_t)s * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
         double part = 0.0;
         for (int64_t i = w0 + t; i < w1; i += 256) {
@@ -1027,20 +1036,35 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     double acc[C];
 #pragma unroll
     for (int c = 0; c < C; c++) acc[c] = 0.0;
+    double part = 0.0;   // own_slice: this thread's share of the normaliser slice
 #pragma unroll
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
         if (r < r1) {
-            const double wr = wexp(a.begin + r);
+            double wr;
+            if constexpr (LARGE) wr = cpre[m];
+            else wr = expw(cpre[m]);
+            if (own_slice) {
+                a.wexp[r] = wr;
+                part += wr;
+            }
 #pragma unroll
             for (int c = 0; c < C; c++) acc[c] += wr * ne[m][c];
         }
     }
     for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
         const double wr = wexp(a.begin + r);
+        if (own_slice) {
+            a.wexp[r] = wr;
+            part += wr;
+        }
         const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] += wr * n[c];
+    }
+    if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
+        part = wave_sum(part);
+        if (l == 0) ssum[rw] = part;
     }
     // the block's 256 partials: butterflies within each wave, then the four wave sums in order
 #pragma unroll
@@ -1050,6 +1074,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         for (int c = 0; c < C; c++) red[rw * C + c] = acc[c];
     __syncthreads();
     if (t < C) a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[C + t]) + (red[2 * C + t] + red[3 * C + t]);
+    if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
 __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
