@@ -72,7 +72,7 @@ struct mppi_handle {
     // what the last update's rollout launch did (mppi_update_info)
     int64_t info[MPPI_UPDATE_INFO_N] = {};
     int tail_nxb = 0;
-    int64_t tail_xbase = 0;
+    int64_t tail_xbase = 0, tail_row0 = 0;
     // MPPI_HOST_TRACE=1: host-side turnaround stamps, averaged and printed by mppi_destroy:
     // [0] flag seen -> phase 3 returns, [1] return -> next phase 1, [2] phase 1 -> rollout launched
     bool host_trace = false;
@@ -1583,13 +1583,14 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.frec = h->d_rec_opt;
         }
         bool folded = false, costs_done = false, tail = false;
+        CoopTail ct;
         a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
         // the next update's draws in the launch's tail, into the buffer it will write (phase 3 makes
         // the rest with the rank); needs the sampling arguments (fused launch) and no tail switch-off
         a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
-                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry));
+                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry, &ct));
             h->gargs.folded = folded;
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
@@ -1606,12 +1607,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : (fuse ? 1 : 0);
         h->info[MPPI_INFO_ROWS] = h->count + (folded ? 1 : 0);
         h->info[MPPI_INFO_HANDOVER] = h->gargs.x_kernel ? -2 : -1;   // -2: read from the device on request
-        if (tail) {   // the rows the tail left: the fifth wave's and its SIMD-mate's (fr_coop.hip)
-            constexpr int64_t WG_ROWS = 16;
-            const int64_t groups = h->count / WG_ROWS;
-            const int64_t xrows = h->count - groups * WG_ROWS + (folded ? 1 : 0);
-            h->tail_xbase = groups * WG_ROWS;
-            h->tail_nxb = (int)((xrows + 3) / 4);
+        if (tail) {   // the rows the launch left to rank_draw_kernel (fr_coop.hip relay_stage, group_draws)
+            h->tail_row0 = ct.row0;
+            h->tail_xbase = ct.xbase;
+            h->tail_nxb = ct.nxb;
         }
         if (folded) {   // the optimal cost is ready with this update's rollouts; phase 3's host block
                         // carries it back (finish_kernel copies d_opt), on the same stream
@@ -1749,8 +1748,9 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
         for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
         if (h->tail_drawn)
             HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, h->tail_nxb, h->tail_xbase,
-                                      &h->gargs.rd, h->graph_dry));
-        else HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, 0, 0, &h->gargs.rd, h->graph_dry));
+                                      h->tail_row0, &h->gargs.rd, h->graph_dry));
+        else HIP_TRY(launch_draw_ahead(sa, h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream, 0, 0, 0, &h->gargs.rd,
+                                       h->graph_dry));
         h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
         h->ahead_valid = true;
     }
@@ -1845,6 +1845,7 @@ static bool graph_eligible(const mppi_handle *h)
     if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
     if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
     if (h->fc.type != FC_NONE || h->sg_window > 0 || h->S > RANK_TILED_MAX) return false;
+    if (fr_coop_update_split(h->count)) return false;   // two rollout launches: not the four-node graph
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
     return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
            h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
@@ -1913,7 +1914,7 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
         void *a0[] = {&h->gargs.roll};
         void *a1[] = {&h->gargs.wg};
         void *a2[] = {&h->gargs.fin};
-        void *a3[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase};
+        void *a3[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase, &rd.sub_row0};
         void **args[4] = {a0, a1, a2, a3};
         for (int i = 0; i < 4; i++) {
             hipKernelNodeParams p = h->gparams[i];

@@ -2421,25 +2421,102 @@ static bool handover_enabled()
     return !(e && e[0] == '0');
 }
 
-// Whether launch_fr_coop_update runs one round of four-wave groups (the launches that can sample
-// their own rows, a.fuse_sample) for `count` rows.
+// MPPI_SPLIT=0: rows just past two waves per SIMD run as one-wave workgroups (A/B; read per update)
+static bool split_disabled()
+{
+    const char *e = getenv("MPPI_SPLIT");
+    return e && e[0] == '0';
+}
+
+// Whether `count` rows run as two fr_coop_x_kernel launches (launch_fr_coop_update): one-wave
+// workgroups hold two waves per SIMD, 32 rows per CU and round (8192 on 256 CUs), and a count just
+// past that - R = S + 2 at S = 8192, configs[4]'s share per GPU - leaves one wave for a second
+// round that runs alone for the whole horizon (1.49 + 1 lone-wave horizons, plus the separate cost
+// kernel).  Two launches of one wave per SIMD (each 1.06-1.1 lone-wave horizons with the objective
+// beside the loops) take less: the first over one round of full four-wave groups, the second over
+// the rest, whose rows left over and the folded filter() row travel through its relay.
+bool fr_coop_update_split(int64_t count)
+{
+    constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
+    const int64_t round = (int64_t)g_cu_count * WG_ROWS;
+    if (count <= 2 * round || split_disabled()) return false;
+    const int64_t rest = count - round, gb = rest / WG_ROWS, xb = rest - gb * WG_ROWS + 1;   // + a folded filter() row
+    return gb > 0 && gb <= (int64_t)g_cu_count && xb <= gb * ROWS_PER_WAVE;
+}
+
+// Whether launch_fr_coop_update runs rounds of four-wave groups (the launches that can sample
+// their own rows, a.fuse_sample) for `count` rows: one round, or the two launches of the split.
 bool fr_coop_update_fusable(int64_t count)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, xrows = count - groups * WG_ROWS + 1;   // + a folded filter() row
-    return groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE;
+    return (groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count);
+}
+
+static void launch_x_any(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
+{
+    if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, nb, s);
+    else if (a.energy) launch_x<CK_ASSISTED_MANIPULATION, true>(a, nb, s);
+    else launch_x<CK_ASSISTED_MANIPULATION, false>(a, nb, s);
+}
+
+// The arguments of a launch over rows [r0, r0 + n) of `a`'s shard: the row-indexed buffers start at
+// row r0 and the shard at begin + r0, so the kernels' launch-relative row lr is row r0 + lr of the
+// update (global rollout begin + r0 + lr: the Philox counter, the rank, the cost slot).
+static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
+{
+    FrRolloutArgs b = a;
+    b.begin += r0;
+    b.count = n;
+    b.noise += r0 * FR_C;   // [H][Rpad][C]: row lr of step k at (k Rpad + lr) C
+    b.rec += r0 * a.H * FR_NREC;
+    b.samp.begin += r0;
+    b.samp.count = n;
+    b.samp.noise += r0 * FR_C;
+    b.samp.prev += r0 * FR_C;
+    if (b.ahead_noise) b.ahead_noise += r0 * FR_C;
+    return b;
 }
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
-                                 bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry)
+                                 bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry,
+                                 CoopTail *tail)
 {
     *costs_done = false;
     *tail_drawn = false;
     if (x_kernel) *x_kernel = false;
+    if (tail) *tail = CoopTail{};
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
-    const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     *folded = false;
+    if (fr_coop_update_split(a0.count)) {   // two launches: one round of full groups, then the rest
+        if (dry) return hipErrorInvalidValue;   // not the hipGraph's four nodes (graph_eligible)
+        const int64_t n0 = (int64_t)g_cu_count * WG_ROWS, rest = a0.count - n0;
+        FrRolloutArgs a = a0;
+        a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;
+        a.handover = handover_enabled() ? 1 : 0;
+        if (!a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
+        FrRolloutArgs A = row_slice(a, 0, n0), B = row_slice(a, n0, rest);
+        A.fcost = nullptr;   // the previous filter() rides with the rows left over
+        A.xbase = n0;
+        A.xrows = 0;
+        const int64_t gb = rest / WG_ROWS, xb = rest - gb * WG_ROWS;
+        const bool frow = a0.fcost != nullptr;
+        if (!frow) B.fcost = nullptr;
+        B.xbase = gb * WG_ROWS;
+        B.xrows = xb + (frow ? 1 : 0);
+        *folded = frow;
+        *costs_done = a.costs_in_launch != 0;
+        *tail_drawn = a.ahead_noise != nullptr;
+        if (final) *final = a;
+        if (tail) *tail = CoopTail{n0, n0 + B.xbase, (int)((B.xrows + 3) / 4), 2};
+        if (e0) (void)hipEventRecord(e0, s);
+        launch_x_any(A, (unsigned)g_cu_count, s);
+        launch_x_any(B, (unsigned)gb, s);
+        if (e1) (void)hipEventRecord(e1, s);
+        return hipGetLastError();
+    }
+    const int64_t groups = a0.count / WG_ROWS, extra = a0.count - groups * WG_ROWS;
     // the previous update's filter() rides along when there are extra rows anyway (the fifth wave
     // of the first workgroup has room); alone it would add a wave, so then it stays pending
     const bool frow = a0.fcost != nullptr && extra > 0;
@@ -2468,6 +2545,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     *tail_drawn = a.ahead_noise != nullptr;
     if (final) *final = a;
     if (x_kernel) *x_kernel = xrows != 0;
+    if (tail) *tail = CoopTail{0, a.xbase, (int)((xrows + 3) / 4), 1};
     if (dry) return hipSuccess;
     if (e0) (void)hipEventRecord(e0, s);
 #ifdef FORCE_X
@@ -2475,9 +2553,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
 #else
     if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
 #endif
-    else if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, (unsigned)groups, s);
-    else if (a.energy) launch_x<CK_ASSISTED_MANIPULATION, true>(a, (unsigned)groups, s);
-    else launch_x<CK_ASSISTED_MANIPULATION, false>(a, (unsigned)groups, s);
+    else launch_x_any(a, (unsigned)groups, s);
     if (e1) (void)hipEventRecord(e1, s);
     return hipGetLastError();
 }

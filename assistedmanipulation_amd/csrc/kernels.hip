@@ -610,7 +610,8 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a)
 // (rollout, step) (sample_device.hpp philox_index).  The update's rollout launch copies the kept
 // rollouts' shifted columns over these once the shift is known (fr_coop.hip kept_columns).
 template <int C>
-__device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned bx, int k, int sub_nxb, int64_t sub_xbase)
+__device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned bx, int k, int sub_nxb, int64_t sub_xbase,
+                                                 int64_t sub_row0)
 {
     static_assert(C % 4 == 0, "full pieces");
     constexpr int NB = C / 4;
@@ -618,8 +619,13 @@ __device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned b
     int64_t lr = tid / NB;
     const int blk = (int)(tid - lr * NB);
     if (sub_nxb > 0) {   // only the rows the rollout launch's tail left (fr_coop.hip tail_draws)
-        const int64_t nm = 4 * (int64_t)sub_nxb;
-        lr = lr < nm ? 16 * (lr / 4) + (lr % 4) : sub_xbase + (lr - nm);
+        const int64_t nm = 4 * (int64_t)sub_nxb, nx = a.count - sub_xbase;
+        // and, when those rows are not the first launch's, rollouts 0 and 1 (-U*), which no
+        // launch draws (their first wave's rows: tail_draws skips g < 2)
+        const int64_t lead01 = (sub_row0 > 0 && a.begin < 2) ? 2 - a.begin : 0;
+        if (lr < nm) lr = sub_row0 + 16 * (lr / 4) + (lr % 4);
+        else if (lr < nm + nx) lr = sub_xbase + (lr - nm);
+        else lr = lr < nm + nx + lead01 ? lr - nm - nx : a.count;   // past the rows: none
     }
     if (lr >= a.count) return;
     const int64_t g = a.begin + lr;
@@ -648,7 +654,8 @@ __device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned b
 // other's output): blocks [0, nr^2) rank tiles, the rest draw (grid nx x H flattened)
 template <int C>
 __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict__ cost, int64_t S, int *__restrict__ rank,
-                                                        unsigned nr, SampleArgs a, unsigned nx, int sub_nxb, int64_t sub_xbase)
+                                                        unsigned nr, SampleArgs a, unsigned nx, int sub_nxb, int64_t sub_xbase,
+                                                        int64_t sub_row0)
 {
     __shared__ uint64_t kj[RANK_T];
     static_assert(RANK_T == 256, "one block size");
@@ -657,17 +664,20 @@ __global__ __launch_bounds__(256) void rank_draw_kernel(const double *__restrict
     if (b < nrb) rank_tile(cost, S, rank, b % nr, (b / nr) % nr, kj, b / (nr * nr), RANK_JS);
     else {
         const unsigned d = b - nrb;
-        draw_ahead_block<C>(a, d % nx, (int)(d / nx), sub_nxb, sub_xbase);
+        draw_ahead_block<C>(a, d % nx, (int)(d / nx), sub_nxb, sub_xbase, sub_row0);
     }
 }
 
 hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                                       hipStream_t s, int sub_nxb, int64_t sub_xbase, RankDrawLaunch *out, bool dry)
+                                       hipStream_t s, int sub_nxb, int64_t sub_xbase, int64_t sub_row0, RankDrawLaunch *out,
+                                       bool dry)
 {
     if (a.C != FR_C || a.count <= 0) return hipErrorInvalidValue;
-    if (sub_nxb > 0 && (16 * (int64_t)sub_nxb > sub_xbase || sub_xbase > a.count)) return hipErrorInvalidValue;
+    if (sub_nxb > 0 && (sub_row0 < 0 || sub_row0 + 16 * (int64_t)sub_nxb > sub_xbase || sub_xbase > a.count))
+        return hipErrorInvalidValue;
     constexpr int NB = FR_C / 4;
-    const int64_t rows = sub_nxb > 0 ? 4 * (int64_t)sub_nxb + (a.count - sub_xbase) : a.count;
+    const int64_t lead01 = (sub_row0 > 0 && a.begin < 2) ? 2 - a.begin : 0;   // rollouts 0 and 1 (draw_ahead_block)
+    const int64_t rows = sub_nxb > 0 ? 4 * (int64_t)sub_nxb + (a.count - sub_xbase) + lead01 : a.count;
     const unsigned nx = (unsigned)((rows * NB + 255) / 256);
     unsigned nr = (unsigned)((S + RANK_T - 1) / RANK_T);
     if (S > RANK_TILED_MAX) {   // O(S log S) rank in its own launches, then the draws alone
@@ -677,9 +687,10 @@ hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, 
         nr = 0;
     }
     const unsigned grid = nr * nr * RANK_JS + nx * (unsigned)a.H;
-    if (out) *out = RankDrawLaunch{cost, S, rank, nr, nx, a, sub_nxb, sub_xbase, grid};
+    if (out) *out = RankDrawLaunch{cost, S, rank, nr, nx, a, sub_nxb, sub_xbase, sub_row0, grid};
     if (dry) return hipSuccess;
-    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(grid), dim3(256), 0, s, cost, S, rank, nr, a, nx, sub_nxb, sub_xbase);
+    hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(grid), dim3(256), 0, s, cost, S, rank, nr, a, nx, sub_nxb, sub_xbase,
+                       sub_row0);
     return hipGetLastError();
 }
 

@@ -242,7 +242,8 @@ hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s);
 // transform, device Philox): rollout 0 zero, rollout 1 = -U*, the rest Philox by (rollout, step);
 // with the stable rank of this update's costs (one launch when S <= RANK_TILED_MAX; rank[] cleared)
 // sub_nxb > 0: the rollout launch's tail drew the rest, so only the rows it left are drawn - the
-// first wave's rows of its first sub_nxb workgroups (16 b + i, i < 4) and [sub_xbase, count).
+// first wave's rows of its first sub_nxb workgroups (sub_row0 + 16 b + i, i < 4: sub_row0 is the
+// first row of the launch that carries the rows left over) and [sub_xbase, count).
 // The rank_draw_kernel launch's arguments (the hipGraph path updates its node with them).
 struct RankDrawLaunch {
     const double *cost;
@@ -251,13 +252,13 @@ struct RankDrawLaunch {
     unsigned nr, nx;
     SampleArgs a;
     int sub_nxb;
-    int64_t sub_xbase;
+    int64_t sub_xbase, sub_row0;
     unsigned grid;
 };
 // dry: fill *out and launch nothing (the one-launch path only: S <= RANK_TILED_MAX)
 hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
-                             hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0, RankDrawLaunch *out = nullptr,
-                             bool dry = false);
+                             hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0, int64_t sub_row0 = 0,
+                             RankDrawLaunch *out = nullptr, bool dry = false);
 hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
@@ -287,10 +288,20 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // *tail_drawn: the launch made the next update's draws for its main waves' rows (a.ahead_noise).
 // final (may be null): the arguments the launch used; *x_kernel: it was fr_coop_x_kernel (one round
 // of four-wave workgroups with a fifth wave); dry: decide and fill them, launch nothing.
+// Rows past one round of workgroups by less than a workgroup's (fr_coop_update_split) run as two
+// launches of fr_coop_x_kernel, the first over one round of full groups; *tail (may be null) then
+// tells rank_draw_kernel where the second launch's rows left for it are.
+struct CoopTail {
+    int64_t row0 = 0;    // first row of the launch with the rows left over
+    int64_t xbase = 0;   // the rows left over start here (launch rows)
+    int nxb = 0;         // workgroups of that launch whose first wave's rows rank_draw_kernel draws
+    int launches = 1;
+};
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final = nullptr, bool *x_kernel = nullptr,
-                                 bool dry = false);
+                                 bool dry = false, CoopTail *tail = nullptr);
 bool fr_coop_update_fusable(int64_t count);
+bool fr_coop_update_split(int64_t count);   // the two-launch case of launch_fr_coop_update
 bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed

@@ -7,6 +7,9 @@
   without rows left over (4096 rollouts: a relay; 4094: none, the four-wave launch).
 - A horizon past the launch's step-cost buffer (HC_MAX = 128 steps) moves the objective to
   fr_step_cost_kernel: parity against the oracle at 100 x 136.
+- Rows just past two waves per SIMD (R = S + 2 at S = 8192, configs[4]'s share per GPU) run as
+  two fr_coop_x_kernel launches (fr_coop_update_split) instead of one-wave workgroups whose last
+  wave runs alone (MPPI_SPLIT=0): bit-identical noise, costs, U*, weights and filter() cost.
 """
 import numpy as np
 import pytest
@@ -54,3 +57,40 @@ def test_long_horizon_objective_outside_launch():
         step_both(dev, orc, x, 0.05 * j, rng, sd)
         assert dev.update_info()["objective_in_launch"] == 0
         assert_update_parity(dev, orc, "H136 upd %d" % j)
+
+
+@pytest.mark.parametrize("rollouts,horison,window", [(8192, 0.64, 0), (8192, 1.28, 10), (8200, 0.32, 0)])
+def test_split_launch_equals_one_wave_launch(rollouts, horison, window, monkeypatch):
+    """The two-launch split against the one-wave launch: the same dynamics code (coop_rows), the
+    objective's step costs summed in step order by both (cost_work / fr_step_cost_kernel), draws
+    ahead against sampling at update time (bit-identical by construction, test_gpu_parity), the
+    min / max from the objective's atomics against a pass (exact).  Device Philox, keep-best 20,
+    shifts of 5, 2, 5 and 0 steps; 8192 x 128 with the Savitzky-Golay filter is configs[4]'s share
+    per GPU."""
+    sg = am.Smoothing(window, 1) if window else None
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
+                                            smoothing=sg)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12]
+    out = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("MPPI_SPLIT", split)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for j, tm in enumerate(times):
+            t.update(x, tm)
+            info = t.update_info()
+            assert info["wait_timeouts"] == 0, info
+            if split == "1":
+                assert info["objective_in_launch"] == 1, info
+                if j > 0:   # drawn ahead; the previous filter() rides in the second launch's relay
+                    assert info["sampling"] == 2 and info["tail_draws"] == 1 and info["folded_filter"] == 1, info
+            else:
+                assert info["objective_in_launch"] == 0 and info["sampling"] == 0, info
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[split] = rec + [(np.float64(t.get_optimal_total_cost()),) * 4]
+    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
