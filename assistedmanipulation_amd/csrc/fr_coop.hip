@@ -2267,6 +2267,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
                             Lmodel, Lx0);
     if constexpr (WPB == 4) {
         if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel);
+    } else if constexpr (WPB == 1) {
+        // past one round (two waves per SIMD, several rounds): the wave's own rows' objective after
+        // its loop, while the launch's other waves still run, instead of fr_step_cost_kernel after it
+        if (a.costs_in_launch) {
+            __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+            for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
+        }
     }
 }
 
@@ -2526,6 +2535,8 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
         if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
+        a.costs_in_launch = groups > 0 && costs_in_launch_enabled() ? 1 : 0;   // each wave its own rows'
+        *costs_done = a.costs_in_launch != 0;
         if (final) *final = a;
         if (dry) return hipSuccess;
         if (e0) (void)hipEventRecord(e0, s);

@@ -4,7 +4,8 @@
   fr_step_cost_kernel (MPPI_COSTS_IN_LAUNCH=0): both evaluate every step cost with the same code
   and sum each rollout's costs in step order (mppi.cpp:322-337), so costs, weights and U* are
   bit-identical, for the default objective, the energy-tank variant and TrackPoint, with and
-  without rows left over (4096 rollouts: a relay; 4094: none, the four-wave launch).
+  without rows left over (4096 rollouts: a relay; 4094: none, the four-wave launch), and past one
+  round (20000: one-wave workgroups, each evaluating its own rows after its loop).
 - A horizon past the launch's step-cost buffer (HC_MAX = 128 steps) moves the objective to
   fr_step_cost_kernel: parity against the oracle at 100 x 136.
 - Rows just past two waves per SIMD (R = S + 2 at S = 8192, configs[4]'s share per GPU) run as
@@ -23,7 +24,8 @@ from test_gpu_parity import _track_point_all_terms
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("rollouts,objective", [(4096, "am"), (4094, "am"), (1000, "energy"), (1000, "track_point")])
+@pytest.mark.parametrize("rollouts,objective", [(4096, "am"), (4094, "am"), (1000, "energy"), (1000, "track_point"),
+                                                (20000, "am"), (20000, "energy")])
 def test_objective_in_launch_equals_cost_kernel(rollouts, objective, monkeypatch):
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.64, keep_best_rollouts=20, threads=8)
     make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
@@ -88,7 +90,7 @@ def test_split_launch_equals_one_wave_launch(rollouts, horison, window, monkeypa
                 if j > 0:   # drawn ahead; the previous filter() rides in the second launch's relay
                     assert info["sampling"] == 2 and info["tail_draws"] == 1 and info["folded_filter"] == 1, info
             else:
-                assert info["objective_in_launch"] == 0 and info["sampling"] == 0, info
+                assert info["sampling"] == 0 and info["folded_filter"] == 0, info   # one-wave workgroups
             rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
         out[split] = rec + [(np.float64(t.get_optimal_total_cost()),) * 4]
     for j, (a, b) in enumerate(zip(out["0"], out["1"])):

@@ -8,7 +8,7 @@
   phase-split ABI (host all-reduces) against the unsharded handle;
 - configs[4]'s per-GPU (8192 x 128) and total (65536 x 128) workloads with the Savitzky-Golay
   filter (window 10, order 1) against the oracle (mppi.cpp:344-448, filter.cpp:35-110).
-Past one round of workgroups the engine switches paths (one-wave workgroups, fr_step_cost_kernel,
+Past one round of workgroups the engine switches paths (the two-launch split, one-wave workgroups,
 the large-R softmin launches, the chunk + merge rank, sg_finish_kernel's LDS windows at H = 128):
 these sizes are where those run.  The oracle runs with 16 threads (the GPU box's CPU share).
 """
@@ -56,15 +56,15 @@ def test_bench_mode_replay_4096x64():
 
 
 def test_config3_total_unsharded_32768x64():
-    """configs[3]'s 32768 x 64 on one handle: one-wave workgroups, fr_step_cost_kernel, the
-    large-R softmin (R > 16384) and the chunk + merge rank (S > 8192)."""
+    """configs[3]'s 32768 x 64 on one handle: one-wave workgroups (each evaluating its own rows'
+    objective after its loop), the large-R softmin (R > 16384) and the chunk + merge rank (S > 8192)."""
     conf, dev, orc, sd = fr_pair(S=32768, horison=0.64, threads=THREADS)
     rng = np.random.default_rng(33)
     x = am.huddled_state()
     stats = []
     for j in range(3):
         step_both(dev, orc, x, 0.05 * j, rng, sd)
-        assert dev.update_info()["objective_in_launch"] == 0
+        assert dev.update_info()["objective_in_launch"] == 1   # each one-wave workgroup's own rows
         assert_update_parity(dev, orc, "32768x64 upd %d" % j, stats=stats)
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
 
@@ -76,12 +76,16 @@ def _hip():
     return L
 
 
-def test_config3_eight_shards_equal_unsharded():
-    """configs[3]'s partition on one GPU: eight phase-split handles of 4096 or 4097
-    rollouts each (the reference's ThreadPool split, mppi.cpp:277-302), with the two all-reduces
-    done on the host between the phases, against one handle of all 32770 rollouts (device Philox:
-    draws are keyed by global rollout, so every rank draws what the single handle draws)."""
-    conf = am.frankaridgeback_configuration(rollouts=32768, horison=0.64, keep_best_rollouts=20, threads=8)
+@pytest.mark.parametrize("S,horison,window", [(32768, 0.64, 0), (65536, 1.28, 10)])
+def test_eight_shards_equal_unsharded(S, horison, window):
+    """configs[3]'s and configs[4]'s partition on one GPU: eight phase-split handles
+    (the reference's ThreadPool split, mppi.cpp:277-302: 4096 or 4097 rollouts each for configs[3];
+    8192 or 8193 for configs[4], whose first two ranks run the two-launch split and the rest one
+    round of one-wave workgroups), with the two all-reduces done on the host between the phases,
+    against one handle of all S + 2 rollouts (device Philox: draws are keyed by global rollout, so
+    every rank draws what the single handle draws).  configs[4] with the Savitzky-Golay filter."""
+    sg = am.Smoothing(window, 1) if window else None
+    conf = am.frankaridgeback_configuration(rollouts=S, horison=horison, keep_best_rollouts=20, threads=8, smoothing=sg)
     mk = lambda: am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
     world = 8
     single, shards = mk(), [mk() for _ in range(world)]
@@ -93,6 +97,8 @@ def test_config3_eight_shards_equal_unsharded():
     hip = _hip()
     R, HC = single.R, single.H * single.C
     x = am.huddled_state()
+    loose = 1.0 if single.H <= 64 else 10.0
+    worst = (0.0, 0.0, 0.0)
 
     def allreduce(ptrs, n):
         bufs = [np.zeros(n) for _ in ptrs]
@@ -124,22 +130,27 @@ def test_config3_eight_shards_equal_unsharded():
             d = max(2 - b, 0)   # rollout 1 carries -U*, which differs in the last bits (gradient order)
             np.testing.assert_array_equal(mine[d:], ref[d:], err_msg="update %d shard %d noise" % (j, r))
             np.testing.assert_allclose(mine[:d], ref[:d], rtol=0, atol=1e-12)
-            if j > 0:   # 4096-4097 rollouts per shard: one round of workgroups, draws ahead
+            if j > 0 and (e - b) % 8192 != 0:   # rounds of four-wave groups (or the split): draws ahead
                 assert sh.update_info()["sampling"] == 2
         for sh in shards:
             # update 0 starts from U* = 0 on both sides: identical bits.  After it, U* carries the
             # last bits of the gradient's summation order (eight partial sums all-reduced against
             # one), and every rollout rolls out U*_shifted + eps: measured up to 4.3e-12 relative
             # (rollout 31767, update 2), so the Delta bar of assert_update_parity
+            # H = 128 compounds the last bits over twice the steps (as in the oracle parity at H = 128)
             cs, cu = sh.costs(), single.costs()
             if j == 0:
                 np.testing.assert_array_equal(cs, cu)
-            bar = 1e-11 * (np.nanmax(cu) - np.nanmin(cu)) + 1e-11 * np.abs(cu)
+            delta = np.nanmax(cu) - np.nanmin(cu)
+            bar = loose * 1e-11 * (delta + np.abs(cu))
             bad = np.abs(cs - cu) > bar
             assert not bad.any(), "rollout %d: %r vs %r" % (int(np.argmax(bad)), cs[np.argmax(bad)], cu[np.argmax(bad)])
-            np.testing.assert_allclose(sh.get_optimal_rollout(), single.get_optimal_rollout(), rtol=0, atol=1e-12)
-            np.testing.assert_allclose(sh.get_weights(), single.get_weights(), rtol=0, atol=1e-15)
+            du = np.max(np.abs(sh.get_optimal_rollout() - single.get_optimal_rollout()))
+            dw = np.max(np.abs(sh.get_weights() - single.get_weights()))
+            worst = tuple(max(w, v) for w, v in zip(worst, (np.nanmax(np.abs(cs - cu)) / delta, du, dw)))
+            assert du <= loose * 1e-12 and dw <= loose * 1e-15, (du, dw)
             assert sh.argmin() == single.argmin()
+    print("worst (cost error / Delta, U* abs, weights abs):", worst)
 
 
 @pytest.mark.parametrize("S,updates", [(8192, 3), (65536, 2)])

@@ -33,5 +33,5 @@ size() {   # name args...
 }
 size pm --workload point_mass --steps 200 --warmup 10
 size s32k --steps 20 --warmup 3 --samples-per-gpu 32768
-size s8k_h128_sg --steps 20 --warmup 3 --samples-per-gpu 8192 --horizon-steps 128 --smoothing 10
+size s8k_h128_sg --steps 40 --warmup 3 --samples-per-gpu 8192 --horizon-steps 128 --smoothing 10
 size s64k_h128_sg --steps 8 --warmup 2 --samples-per-gpu 65536 --horizon-steps 128 --smoothing 10
