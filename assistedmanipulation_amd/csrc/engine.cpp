@@ -1844,7 +1844,7 @@ static bool graph_eligible(const mppi_handle *h)
 {
     if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
     if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
-    if (h->fc.type != FC_NONE || h->sg_window > 0 || h->S > RANK_TILED_MAX) return false;
+    if (h->fc.type != FC_NONE || h->S > RANK_TILED_MAX) return false;   // SG: sg_finish_kernel is the finish node
     if (fr_coop_update_split(h->count)) return false;   // two rollout launches: not the four-node graph
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
     return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&

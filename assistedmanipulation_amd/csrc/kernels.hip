@@ -915,31 +915,37 @@ __global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
     if (t == 0) a.wpart[3 * SM_NB + blockIdx.x] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
+#ifndef GRAD_CSPLIT
+#define GRAD_CSPLIT 1   // control components split over blockIdx.z (A/B builds: 2)
+#endif
 template <int C, bool LARGE>
 __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
-    __shared__ double red[4 * C];
+    constexpr int CSP = (C > 3 && C % GRAD_CSPLIT == 0) ? GRAD_CSPLIT : 1;
+    constexpr int CP = C / CSP;   // this block's components [c0, c0 + CP)
+    const int zc = CSP > 1 ? (int)blockIdx.z : 0, c0 = zc * CP;
+    __shared__ double red[4 * CP];
     __shared__ double smn[WV], smx[WV], ssum[WV];
     const int t = threadIdx.x, rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
     const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
     const int64_t chunk = (a.count + ns - 1) / ns;
     const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
-    double ne[GR][C];   // eps of rollouts r0 + t + 256 m (row 0 stands in past r1, unused)
+    double ne[GR][CP];   // eps of rollouts r0 + t + 256 m (row 0 stands in past r1, unused)
     double cpre[GR];    // their costs (LARGE: e_r), loaded with the eps: one memory trip, not two
 #pragma unroll
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
-        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C + c0;
 #pragma unroll
-        for (int c = 0; c < C; c++) ne[m][c] = n[c];
+        for (int c = 0; c < CP; c++) ne[m][c] = n[c];
         const int64_t gi = a.begin + (r < r1 ? r : 0);
         if constexpr (LARGE) cpre[m] = a.wexp[gi];
         else cpre[m] = a.cost[gi];
     }
     // unsharded, the normaliser slice of block (0, s) is its own rollout range [r0, r1): its e_r come
     // from the gradient loop below, in the same per-thread order as the separate slice pass
-    const bool own_slice = !LARGE && k == 0 && a.begin == 0 && a.count == R;
+    const bool own_slice = !LARGE && k == 0 && zc == 0 && a.begin == 0 && a.count == R;
     double minimum, maximum, valid, total;
     if constexpr (LARGE) {
         if (rw == 0) {
@@ -1013,7 +1019,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     __syncthreads();
     total = 0.0;
     }
-    const bool lead = k == 0 && s == 0 && t == 0;
+    const bool lead = k == 0 && s == 0 && zc == 0 && t == 0;
     Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
         if (lead) { st->all_nan = 1; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
@@ -1028,8 +1034,8 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     // e_r of global rollout i: recomputed, or (LARGE) written by softmin_exp_kernel
     auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
     if constexpr (LARGE) {   // the normaliser is known: one partial carries it
-        if (k == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
-    } else if (k == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
+        if (k == 0 && zc == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
+    } else if (k == 0 && zc == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
         const int64_t wc = (R + ns - 1) / ns, w0 = (int64_t)s * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
         double part = 0.0;
         for (int64_t i = w0 + t; i < w1; i += 256) {
@@ -1044,9 +1050,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         if (t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
     }
     if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; }
-    double acc[C];
+    double acc[CP];
 #pragma unroll
-    for (int c = 0; c < C; c++) acc[c] = 0.0;
+    for (int c = 0; c < CP; c++) acc[c] = 0.0;
     double part = 0.0;   // own_slice: this thread's share of the normaliser slice
 #pragma unroll
     for (int m = 0; m < GR; m++) {
@@ -1060,7 +1066,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
                 part += wr;
             }
 #pragma unroll
-            for (int c = 0; c < C; c++) acc[c] += wr * ne[m][c];
+            for (int c = 0; c < CP; c++) acc[c] += wr * ne[m][c];
         }
     }
     for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
@@ -1069,9 +1075,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
             a.wexp[r] = wr;
             part += wr;
         }
-        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C + c0;
 #pragma unroll
-        for (int c = 0; c < C; c++) acc[c] += wr * n[c];
+        for (int c = 0; c < CP; c++) acc[c] += wr * n[c];
     }
     if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
         part = wave_sum(part);
@@ -1079,12 +1085,13 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     }
     // the block's 256 partials: butterflies within each wave, then the four wave sums in order
 #pragma unroll
-    for (int c = 0; c < C; c++) acc[c] = wave_sum(acc[c]);
+    for (int c = 0; c < CP; c++) acc[c] = wave_sum(acc[c]);
     if (l == 0)
 #pragma unroll
-        for (int c = 0; c < C; c++) red[rw * C + c] = acc[c];
+        for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
     __syncthreads();
-    if (t < C) a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[C + t]) + (red[2 * C + t] + red[3 * C + t]);
+    if (t < CP)
+        a.gsplit[((int64_t)s * a.H + k) * C + c0 + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
     if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
@@ -1555,8 +1562,9 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s)
 {
-    const dim3 grid((unsigned)a.H, GRAD_SPLIT);
+    const dim3 grid((unsigned)a.H, GRAD_SPLIT, a.C == FR_C ? GRAD_CSPLIT : 1);
     if (a.C != FR_C && a.C != 3) return hipErrorInvalidValue;
+    static_assert(FR_C % GRAD_CSPLIT == 0, "whole component splits");
     if (a.R > SM_LARGE_R) {
         hipLaunchKernelGGL(softmin_minmax_kernel, dim3(SM_NB), dim3(256), 0, s, a);
         hipLaunchKernelGGL(softmin_exp_kernel, dim3(SM_NB), dim3(256), 0, s, a);

@@ -175,13 +175,17 @@ def test_config4_savitzky_golay_h128(S, updates):
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
 
 
-@pytest.mark.parametrize("rollouts", [4096, 1000])
-def test_graph_path_equals_eager_launches(rollouts):
+@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10)])
+def test_graph_path_equals_eager_launches(rollouts, horison, window):
     """The hipGraph path of update() (mppi_set_graph: the steady-state update captured once and
     replayed with each update's arguments written into its kernel nodes) gives the eager launches'
     bits over updates with varying shifts (5, 2, 5, 0 steps), including a state change and an
-    interruption (reading the optimal cost runs filter() by itself, so the next update is eager)."""
-    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.64, keep_best_rollouts=20, threads=8)
+    interruption (reading the optimal cost runs filter() by itself, so the next update is eager).
+    4096 x 128 with the Savitzky-Golay filter (window 10): configs[4]'s filter, sg_finish_kernel as
+    the graph's finish node."""
+    sg = am.Smoothing(window, 1) if window else None
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
+                                            smoothing=sg)
     times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17, 0.22, 0.27, 0.32]
     out = {}
     for graph in (0, 1):

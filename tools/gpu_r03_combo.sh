@@ -10,4 +10,12 @@ grep -E "PASSED|FAILED|ERROR" gpurun_out/r03g/pytest.log | grep -v "^tests.*PASS
 tail -3 gpurun_out/r03g/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 SKIP_TESTS=1 bash tools/gpu_r03_owcost.sh || exit 1
-bash tools/gpu_r03_profile.sh
+bash tools/gpu_r03_profile.sh || exit 1
+bash tools/gpu_r03_cs_ab.sh
+mkdir -p gpurun_out/r03gsg
+for i in 1 2; do
+  for g in 0 1; do
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --graph $g --horizon-steps 128 --smoothing 10 --steps 100 > gpurun_out/r03gsg/g${g}_$i.json 2>&1 || exit 1
+    python3 -c "import json; d=json.loads(open('gpurun_out/r03gsg/g${g}_$i.json').read().strip().split('\n')[-1]); print('4096x128 SG graph=$g ms/update %.4f launch %.4f graph_updates %d' % (d['ms_per_step'], d['kernel_ms']['rollout_launch'], d['engine']['graph_updates_timed']))"
+  done
+done
