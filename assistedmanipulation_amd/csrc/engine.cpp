@@ -170,7 +170,8 @@ struct mppi_handle {
     int graph_mode = 0;
     bool graph_dry = false;             // phases fill `gargs` instead of launching
     struct GraphArgs {
-        FrRolloutArgs roll;
+        FrRolloutArgs roll, roll2;   // the rollout launch (the split's two: roll, roll2)
+        int nroll = 1;
         WGradArgs wg;
         FinishArgs fin;
         RankDrawLaunch rd;
@@ -178,8 +179,8 @@ struct mppi_handle {
     } gargs;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    hipGraphNode_t gnode[4] = {};
-    hipKernelNodeParams gparams[4] = {};
+    hipGraphNode_t gnode[5] = {};   // rollout launch(es), weights + gradient, finish, rank + draws
+    hipKernelNodeParams gparams[5] = {};
     int64_t graph_updates = 0;          // updates that ran as the graph (diagnostics)
     // per-update phase state
     bool phase_open = false;
@@ -1590,8 +1591,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
         if (use_coop(h)) {
             HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
-                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry, &ct));
+                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry, &ct,
+                                          &h->gargs.roll2));
             h->gargs.folded = folded;
+            h->gargs.nroll = ct.launches;
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
             if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
@@ -1845,7 +1848,6 @@ static bool graph_eligible(const mppi_handle *h)
     if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
     if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
     if (h->fc.type != FC_NONE || h->S > RANK_TILED_MAX) return false;   // SG: sg_finish_kernel is the finish node
-    if (fr_coop_update_split(h->count)) return false;   // two rollout launches: not the four-node graph
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
     return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
            h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
@@ -1854,17 +1856,19 @@ static bool graph_eligible(const mppi_handle *h)
 static mppi_status graph_nodes(mppi_handle *h)
 {
     size_t n = 0;
+    const size_t want = 3 + (size_t)h->gargs.nroll;   // the split's two rollout launches (fr_coop.hip)
     HIP_TRY(hipGraphGetNodes(h->graph, nullptr, &n));
-    if (n != 4) return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(n) + " nodes, expected 4");
-    hipGraphNode_t nodes[4];
+    if (n != want || want > 5)
+        return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(n) + " nodes, expected " + std::to_string(want));
+    hipGraphNode_t nodes[5];
     HIP_TRY(hipGraphGetNodes(h->graph, nodes, &n));
     hipGraphNode_t cur = nullptr;
-    for (hipGraphNode_t nd : nodes) {   // the chain's root
+    for (size_t i = 0; i < n; i++) {   // the chain's root
         size_t deps = 0;
-        HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &deps));
-        if (deps == 0) cur = nd;
+        HIP_TRY(hipGraphNodeGetDependencies(nodes[i], nullptr, &deps));
+        if (deps == 0) cur = nodes[i];
     }
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < (int)n; i++) {
         if (!cur) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a kernel chain");
         hipGraphNodeType ty;
         HIP_TRY(hipGraphNodeGetType(cur, &ty));
@@ -1873,7 +1877,7 @@ static mppi_status graph_nodes(mppi_handle *h)
         HIP_TRY(hipGraphKernelNodeGetParams(cur, &h->gparams[i]));
         size_t nd = 0;
         HIP_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd));
-        if (i < 3 && nd != 1) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a chain");
+        if (i + 1 < (int)n && nd != 1) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a chain");
         hipGraphNode_t next = nullptr;
         if (nd == 1) HIP_TRY(hipGraphNodeGetDependentNodes(cur, &next, &nd));
         cur = next;
@@ -1912,15 +1916,19 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
         if (!h->gargs.x_kernel || !h->gargs.folded) return fail(h, MPPI_ERR_DEVICE, "graph update took another launch path");
         RankDrawLaunch &rd = h->gargs.rd;
         void *a0[] = {&h->gargs.roll};
+        void *a0b[] = {&h->gargs.roll2};
         void *a1[] = {&h->gargs.wg};
         void *a2[] = {&h->gargs.fin};
         void *a3[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase, &rd.sub_row0};
-        void **args[4] = {a0, a1, a2, a3};
-        for (int i = 0; i < 4; i++) {
+        void **args1[4] = {a0, a1, a2, a3};
+        void **args2[5] = {a0, a0b, a1, a2, a3};
+        const int nn = 3 + h->gargs.nroll;
+        void ***args = h->gargs.nroll == 2 ? args2 : args1;
+        for (int i = 0; i < nn; i++) {
             hipKernelNodeParams p = h->gparams[i];
             p.kernelParams = args[i];
             p.extra = nullptr;
-            if (i == 3) p.gridDim = dim3(rd.grid);
+            if (i == nn - 1) p.gridDim = dim3(rd.grid);
             HIP_TRY(hipGraphExecKernelNodeSetParams(h->graph_exec, h->gnode[i], &p));
         }
     }

@@ -2490,7 +2490,7 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry,
-                                 CoopTail *tail)
+                                 CoopTail *tail, FrRolloutArgs *final2)
 {
     *costs_done = false;
     *tail_drawn = false;
@@ -2499,7 +2499,6 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     *folded = false;
     if (fr_coop_update_split(a0.count)) {   // two launches: one round of full groups, then the rest
-        if (dry) return hipErrorInvalidValue;   // not the hipGraph's four nodes (graph_eligible)
         const int64_t n0 = (int64_t)g_cu_count * WG_ROWS, rest = a0.count - n0;
         FrRolloutArgs a = a0;
         a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;
@@ -2517,8 +2516,11 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
         *folded = frow;
         *costs_done = a.costs_in_launch != 0;
         *tail_drawn = a.ahead_noise != nullptr;
-        if (final) *final = a;
+        if (final) *final = A;
+        if (final2) *final2 = B;
+        if (x_kernel) *x_kernel = true;
         if (tail) *tail = CoopTail{n0, n0 + B.xbase, (int)((B.xrows + 3) / 4), 2};
+        if (dry) return hipSuccess;
         if (e0) (void)hipEventRecord(e0, s);
         launch_x_any(A, (unsigned)g_cu_count, s);
         launch_x_any(B, (unsigned)gb, s);

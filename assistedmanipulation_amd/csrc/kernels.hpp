@@ -289,8 +289,9 @@ void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split lea
 // final (may be null): the arguments the launch used; *x_kernel: it was fr_coop_x_kernel (one round
 // of four-wave workgroups with a fifth wave); dry: decide and fill them, launch nothing.
 // Rows past one round of workgroups by less than a workgroup's (fr_coop_update_split) run as two
-// launches of fr_coop_x_kernel, the first over one round of full groups; *tail (may be null) then
-// tells rank_draw_kernel where the second launch's rows left for it are.
+// launches of fr_coop_x_kernel, the first over one round of full groups (its arguments in *final),
+// the second over the rest (*final2); *tail (may be null) tells rank_draw_kernel where the second
+// launch's rows left for it are.
 struct CoopTail {
     int64_t row0 = 0;    // first row of the launch with the rows left over
     int64_t xbase = 0;   // the rows left over start here (launch rows)
@@ -299,7 +300,7 @@ struct CoopTail {
 };
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final = nullptr, bool *x_kernel = nullptr,
-                                 bool dry = false, CoopTail *tail = nullptr);
+                                 bool dry = false, CoopTail *tail = nullptr, FrRolloutArgs *final2 = nullptr);
 bool fr_coop_update_fusable(int64_t count);
 bool fr_coop_update_split(int64_t count);   // the two-launch case of launch_fr_coop_update
 bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)

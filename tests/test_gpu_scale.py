@@ -175,14 +175,15 @@ def test_config4_savitzky_golay_h128(S, updates):
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
 
 
-@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10)])
+@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10), (8192, 1.28, 10)])
 def test_graph_path_equals_eager_launches(rollouts, horison, window):
     """The hipGraph path of update() (mppi_set_graph: the steady-state update captured once and
     replayed with each update's arguments written into its kernel nodes) gives the eager launches'
     bits over updates with varying shifts (5, 2, 5, 0 steps), including a state change and an
     interruption (reading the optimal cost runs filter() by itself, so the next update is eager).
     4096 x 128 with the Savitzky-Golay filter (window 10): configs[4]'s filter, sg_finish_kernel as
-    the graph's finish node."""
+    the graph's finish node; 8192 x 128 with it is configs[4]'s share per GPU, whose rollouts are
+    the two-launch split (five kernel nodes)."""
     sg = am.Smoothing(window, 1) if window else None
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
                                             smoothing=sg)
