@@ -762,6 +762,52 @@ __global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
 // ---------------------------------------------------------------------------------------------
 // Point-mass rollouts (config 2).  State (p, v), control = force.
 // ---------------------------------------------------------------------------------------------
+// One lane per rollout: the horizon is a chain of dependent steps whose loads (the rollout's eps,
+// U*_shifted and the step's discount) used to be issued inside it, one memory latency per step
+// (19.6 us for 32 steps at 1024 x 32).  The loads now run PM_PF steps ahead: the next block's are
+// issued before the current block's arithmetic (the same operations in the same order).
+constexpr int PM_PF = 16;
+struct PmBlock {
+    double e[PM_PF][3], u[PM_PF][3], gm[PM_PF];
+};
+__device__ __forceinline__ void pm_load(const PmRolloutArgs &a, int64_t lr, int k0, PmBlock &b)
+{
+#pragma unroll
+    for (int j = 0; j < PM_PF; j++) {
+        const int k = k0 + j < a.H ? k0 + j : a.H - 1;   // past the horizon: loaded, unused
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            b.e[j][c] = a.optimal ? 0.0 : a.noise[((int64_t)k * a.Rpad + lr) * 3 + c];
+            b.u[j][c] = a.Ushift[k * 3 + c];
+        }
+        b.gm[j] = a.steps[k].gamma_k;
+    }
+}
+__device__ __forceinline__ void pm_steps(const PmRolloutArgs &a, const DevPointMass &P, int k0, const PmBlock &b, double *x,
+                                         double &J, bool &alive)
+{
+#pragma unroll
+    for (int j = 0; j < PM_PF; j++) {
+        if (k0 + j >= a.H || !alive) return;
+        double u[3];
+        for (int c = 0; c < 3; c++) u[c] = b.u[j][c] + b.e[j][c];
+        double cost = 0.0;
+        for (int i = 0; i < 3; i++) {
+            const double d = x[i] - P.target[i];
+            cost += P.q[i] * (d * d);
+        }
+        for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
+        const double sc = b.gm[j] * cost;
+        if (!a.optimal && isnan(sc)) {
+            J = NAN;
+            alive = false;
+            return;
+        }
+        J += sc;
+        for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
+        for (int i = 0; i < 3; i++) x[i] = x[i] + x[3 + i] * a.dt;
+    }
+}
 __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
 {
     const int64_t lr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -773,27 +819,14 @@ __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)
     for (int i = 0; i < 6; i++) x[i] = a.x0[i];
     double J = 0.0;
     bool alive = true;
-    for (int k = 0; k < a.H; k++) {
-        double eps[3];
-        for (int c = 0; c < 3; c++) eps[c] = a.optimal ? 0.0 : a.noise[((int64_t)k * a.Rpad + lr) * 3 + c];
-        if (!alive) continue;
-        double u[3];
-        for (int c = 0; c < 3; c++) u[c] = a.Ushift[k * 3 + c] + eps[c];
-        double cost = 0.0;
-        for (int i = 0; i < 3; i++) {
-            const double d = x[i] - P.target[i];
-            cost += P.q[i] * (d * d);
-        }
-        for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
-        const double sc = a.steps[k].gamma_k * cost;
-        if (!a.optimal && isnan(sc)) {
-            J = NAN;
-            alive = false;
-            continue;
-        }
-        J += sc;
-        for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
-        for (int i = 0; i < 3; i++) x[i] = x[i] + x[3 + i] * a.dt;
+    PmBlock b0, b1;   // ping-pong: one block's loads in flight while the other's steps run
+    pm_load(a, lr, 0, b0);
+    for (int k0 = 0; k0 < a.H; k0 += 2 * PM_PF) {
+        if (k0 + PM_PF < a.H) pm_load(a, lr, k0 + PM_PF, b1);
+        pm_steps(a, P, k0, b0, x, J, alive);
+        if (k0 + PM_PF >= a.H) break;
+        if (k0 + 2 * PM_PF < a.H) pm_load(a, lr, k0 + 2 * PM_PF, b0);
+        pm_steps(a, P, k0 + PM_PF, b1, x, J, alive);
     }
     if (a.optimal) *a.cost_out = J;
     else a.cost_out[g] = J;
