@@ -50,12 +50,13 @@ struct mppi_handle {
     hipEvent_t ev[6] = {};
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
     hipEvent_t ev_dyn = nullptr;   // after the rollout (dynamics) kernel, before the cost kernel
+    hipEvent_t ev_wg = nullptr;    // timing level 2: after weights_gradient_kernel (kernel_ms[6])
     // filter() (the optimal rollout) of the last update: pending (not launched yet: it rides in the
     // next update's remainder launch, or runs alone when something needs it first), launched
     enum { OPT_NONE, OPT_PENDING, OPT_LAUNCHED, OPT_FOLDED } opt_state = OPT_NONE;
     const StepConst *opt_steps = nullptr;   // the step constants its update used
     // sample, rollout (dynamics + cost kernels), reduce, optimal rollout, update, dynamics kernel
-    float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
+    float kernel_ms[7] = {0, 0, 0, 0, 0, 0, 0};
     // HIP-event timing on the update path (mppi_set_timing): 0 none, 1 the rollout kernel alone
     // ([5]), 2 every phase.  Each event record costs the stream a few microseconds between kernels.
     int timing = 0;
@@ -922,6 +923,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_done, hipEventDisableTiming));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_end, hipEventDisableSystemFence));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_dyn, hipEventDisableSystemFence));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_wg, hipEventDisableSystemFence));
     const size_t HC = (size_t)(h->H * h->C);
     CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
@@ -1062,6 +1064,7 @@ void mppi_destroy(mppi_handle *h)
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
     if (h->ev_dyn) (void)hipEventDestroy(h->ev_dyn);
+    if (h->ev_wg) (void)hipEventDestroy(h->ev_wg);
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1707,6 +1710,7 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     if (h->graph_dry) return MPPI_OK;
     // sharded: the partial gradient is summed here and all-reduced before phase 3
     HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
+    if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_wg, h->stream));
     return MPPI_OK;
 }
 
@@ -1796,7 +1800,10 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
         for (int i = 0; i < 3; i++) (void)hipEventElapsedTime(&h->kernel_ms[i], h->ev[i], h->ev[i + 1]);
         (void)hipEventElapsedTime(&h->kernel_ms[4], h->ev[0], h->ev[5]);
     }
-    if (h->timing >= 2) (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
+    if (h->timing >= 2) {
+        (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
+        (void)hipEventElapsedTime(&h->kernel_ms[6], h->ev[2], h->ev_wg);   // the weight reduce alone
+    }
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
     if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
@@ -2184,7 +2191,7 @@ mppi_status mppi_set_timing(mppi_handle *h, int level)
 
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
 {
-    if (!h || !ms || n < 0 || n > 6) return MPPI_ERR_INVALID;
+    if (!h || !ms || n < 0 || n > 7) return MPPI_ERR_INVALID;
     if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
     if (h->ring_unread) {   // level 1: the newest recorded pair

@@ -452,11 +452,12 @@ class Trajectory:
     def kernel_times(self, wait=True, detail=False):
         """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
         wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's).
-        detail=True appends [5], the rollout (dynamics) kernel alone ([1] also spans the cost kernel);
-        it implies wait=False."""
+        detail=True appends [5], the rollout (dynamics) kernel alone ([1] also spans the cost kernel),
+        and [6], the weights + gradient launch alone ([2] also spans the finish kernel; timing level
+        2); it implies wait=False."""
         if detail:
-            out = (C.c_float * 6)()
-            self._check(self._L.mppi_kernel_times_detail(self._h, out, 6))
+            out = (C.c_float * 7)()
+            self._check(self._L.mppi_kernel_times_detail(self._h, out, 7))
             return list(out)
         out = (C.c_float * 5)()
         fn = self._L.mppi_kernel_times if wait else self._L.mppi_kernel_times_nowait

@@ -51,6 +51,7 @@ BYTES_EPS_FR = 96.0
 BYTES_REC = 336.0
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
 PMC_JSON = os.path.join(HERE, "profiles", "r03g_pmc_rollout.json")
+PMC_WG_JSON = os.path.join(HERE, "profiles", "r03g_pmc_weights.json")   # weights_gradient_kernel's traffic
 
 
 def parse():
@@ -230,7 +231,7 @@ def main():
     dyn_ms = sum(dyn_times) / max(len(dyn_times), 1)
     # the per-phase breakdown from a few further updates with every event recorded (untimed)
     traj.set_timing(2)
-    kt = np.zeros(6)
+    kt = np.zeros(7)
     nb = 5
     for _ in range(nb):
         traj.update(x, 0.05 * j)
@@ -294,6 +295,19 @@ def main():
     if not pm:
         hbm["extra_bytes_per_rollout_step"] = {"rollout_eps_read": BYTES_EPS_FR,
                                                "step_record_round_trip": 2 * BYTES_REC if info["objective_in_launch"] else BYTES_REC}
+    # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
+    # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
+    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
+    if kt[6] > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
+        wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
+        wg = {"kernel": "weights_gradient_kernel", "bound": "hbm", "ms": kt[6], "bytes_per_launch": wg_bytes,
+              "achieved_GBs": wg_bytes / (kt[6] * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
+        wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS
+        wg["traffic"] = None
+        if os.path.exists(PMC_WG_JSON) and world == 1 and default_workload and not pm:
+            with open(PMC_WG_JSON) as f:
+                wg["traffic"] = json.load(f)["traffic_bytes"]
+        hbm["weight_reduce"] = wg
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -326,7 +340,8 @@ def main():
                    "parallelism": "samples-dp%d" % world},
         "engine": info,
         "kernel_ms": {"rollout_launch": dyn_ms, "rollout_launch_samples": len(dyn_times), "breakdown_untimed": {
-                      "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "optimal_rollout": kt[3], "update": kt[4]}},
+                      "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "weights_gradient": kt[6],
+                      "optimal_rollout": kt[3], "update": kt[4]}},
         "roofline": roofline,
         "hbm": hbm,
     }

@@ -405,9 +405,10 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
 /* As mppi_kernel_times without waiting for the side stream: [3] is the latest optimal rollout
  * already finished (possibly an earlier update's).  For timing loops that keep filter() overlapped. */
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5);
-/* The first n (<= 6) per-update times of mppi_kernel_times_nowait, where [5] is the rollout
+/* The first n (<= 7) per-update times of mppi_kernel_times_nowait, where [5] is the rollout
  * (dynamics) kernel alone: [1] spans it and the FrankaRidgeback cost kernel that sums the step
- * costs from its records. */
+ * costs from its records; [6] (timing level 2) the weights + gradient launch alone, without the
+ * finish kernel that [2] also spans. */
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n);
 /* The rollout launch's HIP-event times (ms) of every update run at timing level 1 since the last
  * call, oldest first (at most the last 64): *count <- min(recorded, capacity), and the record is
