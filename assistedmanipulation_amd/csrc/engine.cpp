@@ -1432,9 +1432,10 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         a.cost_kind = h->cost_kind;
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.rec = h->d_rec_opt;
-        if (use_coop(h)) {
+        if (use_coop(h)) {   // the row's objective after its loop (fr_coop_kernel's one-wave path)
+            a.costs_in_launch = fr_coop_costs_in_launch() ? 1 : 0;
             HIP_TRY(launch_fr_coop(a, h->stream_opt));
-            HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
+            if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
         } else {
             HIP_TRY(launch_fr_rollout(a, h->stream_opt));
         }
