@@ -183,6 +183,11 @@ struct mppi_handle {
     hipGraphNode_t gnode[5] = {};   // rollout launch(es), weights + gradient, finish, rank + draws
     hipKernelNodeParams gparams[5] = {};
     int64_t graph_updates = 0;          // updates that ran as the graph (diagnostics)
+    // in-launch waits that gave up (fr_coop.hip note_wait_timeout), summed over the updates
+    int64_t wait_timeouts_total = 0;
+    // mppi_debug_inject: fault bits for the next debug_updates rollout launches (tests only)
+    int debug_flags = 0, debug_updates = 0;
+    bool published_once = false;   // an update has published U* (and so has a filter() row)
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -513,7 +518,7 @@ bool fuse_sampling(const mppi_handle *h)
 mppi_status alloc_shard_buffers(mppi_handle *h)
 {
     h->ahead_valid = false;   // the draws ahead live in the buffers freed here
-    if (h->d_costs_local) HIP_TRY(hipMemset(h->d_costs_local, 0, (size_t)h->R * sizeof(double)));   // a new range
+    if (h->d_costs_local) HIP_TRY(hipMemset(h->d_costs_local, 0, (size_t)(h->R + 1) * sizeof(double)));   // a new range
     dfree(h, h->d_noise);
     dfree(h, h->d_noise_prev);
     h->Rpad = std::max<int64_t>(64, (h->count + 63) / 64 * 64);
@@ -929,7 +934,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_U, HC));
     CREATE_TRY(dalloc(h, &h->d_Us, HC));
-    CREATE_TRY(dalloc(h, &h->d_costs, (size_t)h->R));
+    CREATE_TRY(dalloc(h, &h->d_costs, (size_t)h->R + 1));   // + slot R: the all-reduced wait timeouts
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
@@ -1111,7 +1116,7 @@ mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char uniqu
     std::memcpy(&id, unique_id, 128);
     HIP_TRY(hipSetDevice(h->device));
     NCCL_TRY(ncclCommInitRank(&h->comm, world, id, rank));
-    if (!h->d_costs_local) HIP_TRY(dalloc(h, &h->d_costs_local, (size_t)h->R));
+    if (!h->d_costs_local) HIP_TRY(dalloc(h, &h->d_costs_local, (size_t)h->R + 1));   // + the wait-timeout slot
     return MPPI_OK;
 }
 
@@ -1412,6 +1417,10 @@ static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
 // filter() of the last update on the side stream, by itself (mppi.cpp:450-479)
 static mppi_status launch_filter_standalone(mppi_handle *h)
 {
+    // cooperative FrankaRidgeback: phase 3 left filter() pending (it rides in the next rollout
+    // launch) and recorded no event behind the finish kernel, to keep one off the update path; the
+    // row reads the d_U / d_x0_opt that kernel wrote, so order the side stream behind it now
+    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h)) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream_opt, h->ev_pub, 0));
     HIP_TRY(hipEventRecord(h->ev[4], h->stream_opt));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
@@ -1571,6 +1580,11 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
         a.rec = h->d_rec;
+        a.wait_sum = h->comm ? h->d_costs_local + h->R : nullptr;
+        if (h->debug_updates > 0) {   // mppi_debug_inject: this update's launch carries the fault
+            a.debug = h->debug_flags;
+            h->debug_updates--;
+        }
         if (fuse) {   // U*_shifted read from U* with the shift; the state from the launch
             a.fuse_sample = ahead ? 2 : 1;
             a.samp = sa;
@@ -1685,6 +1699,8 @@ static FinishArgs finish_args(mppi_handle *h)
     f.rank_zero = h->d_rank;
     f.rank_n = h->S <= RANK_TILED_MAX ? h->R : 0;
     f.stats_reset = h->d_cstats;
+    f.wait_all = h->comm ? h->d_costs + h->R : nullptr;
+    f.wait_local = h->comm ? h->d_costs_local + h->R : nullptr;
     return f;
 }
 
@@ -1807,6 +1823,11 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
     }
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
+    const int64_t waits = (int64_t)h->h_out[HC + 7];   // in-launch waits that gave up (the finish kernel)
+    h->info[MPPI_INFO_WAIT_TIMEOUTS] = waits;
+    h->wait_timeouts_total += waits;
+    if (waits) return fail(h, MPPI_ERR_DEVICE, "in-launch wait timed out (" + std::to_string(waits) +
+                                                   " waits): rollout costs incomplete, U* not published");
     if (all_nan) return fail(h, MPPI_ERR_ALL_NAN, "all nan rollouts");
     if (sg_error) return fail(h, MPPI_ERR_SMOOTHING, "Savitzky-Golay window: time went backwards");
     {
@@ -1825,6 +1846,7 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
     h->update_duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - h->t_start).count();
     h->update_last = h->rollout_time;
     ++h->update_count;
+    h->published_once = true;   // a filter() row exists from here on (mppi_optimal_terms)
     if (h->host_trace) {
         h->ht_ret = std::chrono::steady_clock::now();
         h->ht_sum[0] += std::chrono::duration<double, std::micro>(h->ht_ret - h->ht_flag).count();
@@ -1857,6 +1879,10 @@ static bool graph_eligible(const mppi_handle *h)
     if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
     if (h->fc.type != FC_NONE || h->S > RANK_TILED_MAX) return false;   // SG: sg_finish_kernel is the finish node
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
+    // the launch path the replayed nodes assume: fr_coop_x_kernel with the filter() row folded and
+    // the objective in the launch (a rollout count that is a multiple of 16 takes fr_coop_kernel<4>
+    // with filter() left pending, a horizon past 128 steps adds the cost kernel)
+    if (!fr_coop_update_folds(h->count, (int)h->H) || h->debug_updates > 0) return false;
     return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
            h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
 }
@@ -1921,7 +1947,10 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
         }
     } else {
         if (st != MPPI_OK) return st;
-        if (!h->gargs.x_kernel || !h->gargs.folded) return fail(h, MPPI_ERR_DEVICE, "graph update took another launch path");
+        if (!h->gargs.x_kernel || !h->gargs.folded) {   // graph_eligible rules this out; never replay a stale chain
+            h->graph_mode = 0;
+            return fail(h, MPPI_ERR_DEVICE, "graph update took another launch path");
+        }
         RankDrawLaunch &rd = h->gargs.rd;
         void *a0[] = {&h->gargs.roll};
         void *a0b[] = {&h->gargs.roll2};
@@ -1945,6 +1974,14 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
     return phase3_wait(h, seq);
 }
 
+mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates)
+{
+    if (!h || fault < 0 || fault > MPPI_DEBUG_RELAY_NO_SIGNAL || updates < 0) return MPPI_ERR_INVALID;
+    h->debug_flags = fault;
+    h->debug_updates = updates;
+    return MPPI_OK;
+}
+
 mppi_status mppi_set_graph(mppi_handle *h, int enable)
 {
     if (!h || enable < 0 || enable > 1) return MPPI_ERR_INVALID;
@@ -1966,7 +2003,9 @@ mppi_status mppi_update(mppi_handle *h, const double *state, double time)
     if (st != MPPI_OK) return st;
     if (sharded(h)) {
         if (!h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
-        NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R, ncclDouble, ncclSum, h->comm, h->stream));
+        // R costs and slot R, every rank's in-launch wait timeouts (the finish kernels fail the
+        // update on all ranks alike when any rank's launch lost rows)
+        NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R + 1, ncclDouble, ncclSum, h->comm, h->stream));
     }
     st = mppi_update_phase2(h);
     if (st != MPPI_OK) return st;
@@ -2076,7 +2115,7 @@ mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
     if (h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || !use_coop(h))
         return fail(h, MPPI_ERR_UNSUPPORTED, "per-term totals: AssistedManipulation on the cooperative kernel only");
     HIP_TRY(hipSetDevice(h->device));
-    if (h->opt_state == mppi_handle::OPT_NONE && !h->opt_steps) {   // before the first update: reset(0)
+    if (!h->published_once) {   // before the first update that published: reset(0), no filter() row yet
         for (int i = 0; i < 7; i++) terms7[i] = 0.0;
         return MPPI_OK;
     }
@@ -2130,13 +2169,13 @@ mppi_status mppi_noise(mppi_handle *h, double *out)
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
 {
     if (!h || !info || n < 0 || n > MPPI_UPDATE_INFO_N) return MPPI_ERR_INVALID;
-    if (n > MPPI_INFO_HANDOVER) {   // Status words of the last rollout launch
-        int w[2] = {-1, 0};
+    if (n > MPPI_INFO_HANDOVER && h->info[MPPI_INFO_HANDOVER] == -2) {   // the last rollout launch's Status word
+        int w = -1;
         HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipMemcpy(w, &h->d_status->handover, sizeof(w), hipMemcpyDeviceToHost));
-        if (h->info[MPPI_INFO_HANDOVER] == -2) h->info[MPPI_INFO_HANDOVER] = w[0];
-        h->info[MPPI_INFO_WAIT_TIMEOUTS] = w[1];
+        HIP_TRY(hipMemcpy(&w, &h->d_status->handover, sizeof(w), hipMemcpyDeviceToHost));
+        h->info[MPPI_INFO_HANDOVER] = w;
     }
+    h->info[MPPI_INFO_WAIT_TIMEOUTS_TOTAL] = h->wait_timeouts_total;
     std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;
 }

@@ -1853,12 +1853,15 @@ __device__ __forceinline__ void signal_records(int *flag)
     __builtin_amdgcn_s_waitcnt(0);
     __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Bounded: a wave that never signals (a bug) costs about a second, not a hung GPU; the timeout is
-// counted in Status::wait_timeouts (mppi_update_info MPPI_INFO_WAIT_TIMEOUTS, asserted 0 by tests).
+// Bounded: a wave that never signals (a bug) costs about a second, not a hung GPU.  The timeout is
+// counted in Status::wait_timeouts (and, sharded over RCCL, in the rank's cost slot R that the
+// engine all-reduces); the finish kernel then fails the update (MPPI_ERR_DEVICE) instead of
+// publishing U* from costs some rows never wrote (kernels.hip update_wait_timeouts).
 constexpr int WAIT_SPINS = 1 << 20;
 __device__ __forceinline__ void note_wait_timeout(const FrRolloutArgs &a)
 {
     if (a.status) atomicAdd(&const_cast<Status *>(a.status)->wait_timeouts, 1);
+    if (a.wait_sum) atomicAdd(a.wait_sum, 1.0);
 }
 __device__ __forceinline__ void wait_records(const FrRolloutArgs &a, int *flag)
 {
@@ -2094,7 +2097,9 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
 #endif
         if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
-            __hip_atomic_store(Lq + Q_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
+            if (!((a.debug & 1) && r == 1))
+                __hip_atomic_store(Lq + Q_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             return true;
         }
     }
@@ -2460,6 +2465,15 @@ bool fr_coop_update_fusable(int64_t count)
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, xrows = count - groups * WG_ROWS + 1;   // + a folded filter() row
     return (groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count);
+}
+
+bool fr_coop_update_folds(int64_t count, int H)
+{
+    if (!costs_in_launch_enabled() || H > HC_MAX) return false;
+    if (fr_coop_update_split(count)) return true;
+    constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
+    const int64_t groups = count / WG_ROWS, extra = count - groups * WG_ROWS;
+    return extra > 0 && groups > 0 && groups <= (int64_t)g_cu_count && extra + 1 <= groups * ROWS_PER_WAVE;
 }
 
 static void launch_x_any(const FrRolloutArgs &a, unsigned nb, hipStream_t s)

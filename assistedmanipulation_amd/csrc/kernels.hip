@@ -1146,6 +1146,10 @@ __device__ __forceinline__ void publish_block(const FinishArgs &a)
 {
     __syncthreads();
     if (threadIdx.x == 0) {
+        // every thread has read this update's wait-timeout count (update_wait_timeouts): reset it
+        // for the next rollout launch (stream-ordered after this kernel)
+        a.status_w->wait_timeouts = 0;
+        if (a.wait_local) *a.wait_local = 0.0;
         __threadfence_system();
         __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1160,15 +1164,25 @@ __device__ __forceinline__ double softmin_total(const Status &st)
     return t;
 }
 
+// In-launch waits of this update's rollout launch that gave up (fr_coop.hip note_wait_timeout):
+// every rank's when sharded over RCCL (the all-reduced cost slot R), else this handle's.  Nonzero
+// means some rows' costs were never written, so the update fails the way a throwing optimise()
+// does (mppi.cpp:369-370): no gradient step, no smoothing, U* not published, no filter().
+__device__ __forceinline__ int update_wait_timeouts(const FinishArgs &a)
+{
+    return a.wait_all ? (int)*a.wait_all : a.status->wait_timeouts;
+}
+
 // U* += step * gradient; Savitzky-Golay; clamp (mppi.cpp:421-447).  One workgroup.
 // SG: one thread per control dimension runs its MovingExtendedWindow (filter.cpp:19-116).
 __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
 {
     const Status &stt = *a.status;
     const int HC = a.H * a.C;
+    const int wt = update_wait_timeouts(a);
     if (threadIdx.x == 0) sg_err = 0;
     __syncthreads();
-    if (!stt.early) {
+    if (!stt.early && !wt) {
     const double total = softmin_total(stt);
     if (threadIdx.x == 0) a.status_w->total = total;
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
@@ -1255,7 +1269,7 @@ __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
     }
     __syncthreads();
     // publish (mppi.cpp:178-182): U* <- U*_shifted unless the update threw
-    const bool ok = !stt.all_nan && !sg_err;
+    const bool ok = !stt.all_nan && !sg_err && !wt;
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
         const double v = ok ? a.Ushift[t] : a.U[t];
         if (ok) a.U[t] = v;
@@ -1264,13 +1278,14 @@ __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
     if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
-        a.status_w->sg_error = sg_err;
+        a.status_w->sg_error = sg_err || wt;   // read by the filter() row as "the update threw"
         a.out[HC + 0] = *a.opt_cost;
         a.out[HC + 1] = (double)stt.all_nan;
         a.out[HC + 2] = (double)stt.early;
         a.out[HC + 3] = (double)sg_err;
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
+        a.out[HC + 7] = (double)wt;
     }
 }
 
@@ -1288,7 +1303,8 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
 {
     const int HC = a.H * a.C;
-    const bool upd = !a.status->early, ok = !a.status->all_nan;   // no filter: no SG error
+    const int wt = update_wait_timeouts(a);
+    const bool upd = !a.status->early && !wt, ok = !a.status->all_nan && !wt;   // no filter: no SG error
     const double oc = threadIdx.x == 0 ? *a.opt_cost : 0.0;
     const int nsp = a.ns > 0 ? a.ns : 1;
     const double *__restrict__ gs = a.ns > 0 ? a.gsplit : a.gpart;
@@ -1320,7 +1336,7 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
         const Status stt = *a.status;
-        a.status_w->sg_error = 0;
+        a.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
         if (upd) a.status_w->total = total;
         a.out[HC + 0] = oc;
         a.out[HC + 1] = (double)stt.all_nan;
@@ -1328,6 +1344,7 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         a.out[HC + 3] = 0.0;
         a.out[HC + 4] = stt.minimum;
         a.out[HC + 5] = stt.maximum;
+        a.out[HC + 7] = (double)wt;
     }
     if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, threadIdx.x);
     publish_block(a);
@@ -1376,7 +1393,8 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
     const Status &stt = *a.status;
     const int H = a.H, C = a.C, HC = H * C, w = a.sg_window, W = H + 2 * w + 1, nw = 2 * w + 1;
     const int t = threadIdx.x, c = t >> 6, l = t & 63;
-    const bool upd = !stt.early;   // optimise() returned before the filter (mppi.cpp:373-375)
+    const int wt = update_wait_timeouts(a);
+    const bool upd = !stt.early && !wt;   // optimise() returned before the filter (mppi.cpp:373-375)
     double *wl = sg_lds + (int64_t)C * (2 * W + H);
     if (t == 0) sg_err = 0;
     if (t < nw) wl[t] = a.sg_weights[t];
@@ -1514,7 +1532,7 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
     __syncthreads();
     // publish (mppi.cpp:178-182): U* <- U*_shifted unless the update threw
     const int err = sg_err;
-    const bool ok = !stt.all_nan && !err;
+    const bool ok = !stt.all_nan && !err && !wt;
     for (int i = t; i < HC; i += blockDim.x) {
         const double v = ok ? a.Ushift[i] : a.U[i];
         if (ok) a.U[i] = v;
@@ -1523,7 +1541,8 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
     if (t < a.X) a.x0_opt[t] = a.x0[t];
     for (int64_t i = t; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (t == 0) {
-        a.status_w->sg_error = err;
+        a.status_w->sg_error = err || wt;   // read by the filter() row as "the update threw"
+        a.out[HC + 7] = (double)wt;
         a.out[HC + 0] = *a.opt_cost;
         a.out[HC + 1] = (double)stt.all_nan;
         a.out[HC + 2] = (double)stt.early;

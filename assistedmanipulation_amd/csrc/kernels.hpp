@@ -19,7 +19,9 @@ struct Status {
     int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
     int handover;    // fr_coop_x_kernel: step at which the fifth wave's rows moved (take_over), or -1
-    int wait_timeouts;   // fr_coop_x_kernel: bounded in-launch waits that gave up (a bug if nonzero)
+    // fr_coop_x_kernel: bounded in-launch waits that gave up in this update's rollout launch (some
+    // rows' costs were then never written): the finish kernels fail the update on it and reset it
+    int wait_timeouts;
     int pad[3];
     double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
     double tsplit[GRAD_SPLIT_DEF];    // its GRAD_SPLIT partial sums (weights_gradient_kernel)
@@ -106,6 +108,12 @@ struct FrRolloutArgs {
     // fr_coop_x_kernel: the fifth wave's rows move to the first of waves 1..3 to end its own rows
     // (fr_coop.hip take_over; MPPI_HANDOVER=0 keeps them on the doubled SIMD)
     int handover;
+    // sharded over RCCL: the rank's slot R of the cost vector the engine all-reduces, to which every
+    // in-launch wait that gives up adds 1 (so every rank's finish kernel sees any rank's), or null
+    double *wait_sum;
+    // MPPI_DEBUG_* fault injection (mppi_debug_inject; 0 in production): bit 0, relay stage 1 of
+    // the workgroup with rows left over never signals stage 2 (tests the wait-timeout failure)
+    int debug;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -186,6 +194,10 @@ struct FinishArgs {
     // the cost statistics, consumed by weights_gradient_kernel ahead of this launch: reset here for
     // the next update's folds (stream-ordered before its rollout launch; may be null)
     CostStats *stats_reset;
+    // the update's in-launch wait timeouts: every rank's (the all-reduced cost slot R) when sharded
+    // over RCCL, else null (Status::wait_timeouts); wait_local: this rank's slot, reset here
+    const double *wait_all;
+    double *wait_local;
 };
 
 
@@ -304,6 +316,9 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent
 bool fr_coop_update_fusable(int64_t count);
 bool fr_coop_update_split(int64_t count);   // the two-launch case of launch_fr_coop_update
 bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
+// Whether a pending filter() folds into the update launch of `count` rows with the objective in
+// the launch (fr_coop_x_kernel, one launch or the split's two): the hipGraph path's launch shape
+bool fr_coop_update_folds(int64_t count, int H);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);

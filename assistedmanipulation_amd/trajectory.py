@@ -419,12 +419,18 @@ class Trajectory:
         """What the last update's rollout launch did (mppi_update_info): dict of the engine's own
         choices (cooperative kernel, folded filter(), objective in the launch, tail draws,
         sampling mode 0/1/2, rows rolled out, the step at which the fifth wave's rows moved off
-        the doubled SIMD or -1, the in-launch waits that gave up since create)."""
+        the doubled SIMD or -1, the in-launch waits that gave up in the last update - which then
+        failed - and summed since create)."""
         out = np.zeros(abi.MPPI_UPDATE_INFO_N, dtype=np.int64)
         self._check(self._L.mppi_update_info(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), out.size))
         keys = ("cooperative", "folded_filter", "objective_in_launch", "tail_draws", "sampling", "rows", "handover",
-                "wait_timeouts")
+                "wait_timeouts", "wait_timeouts_total")
         return {k: int(v) for k, v in zip(keys, out)}
+
+    def debug_inject(self, fault, updates=1):
+        """Fault injection for the failure-detection tests (mppi_debug_inject): the next `updates`
+        rollout launches carry fault bits `fault` (abi.MPPI_DEBUG_*)."""
+        self._check(self._L.mppi_debug_inject(self._h, int(fault), int(updates)))
 
     def smoothing_windows(self):
         """(uu, tt, start_idx) of the per-dimension SG windows (SavitzkyGolayFilter::get_windows)."""

@@ -13,11 +13,19 @@ Workloads (BASELINE.json configs):
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload point_mass]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N rank processes
+itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) before anything imports the
+engine or touches HIP, and exits with their status; under torch.distributed.run WORLD_SIZE must
+equal --gpus.  Each rank rolls out its contiguous share of the rollouts (mppi.cpp:272-307's
+partition, mppi_shard_range) and the engine all-reduces the costs and the partial gradient over
+RCCL; rank 0 prints the one JSON line.
 """
 import argparse
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -26,8 +34,7 @@ sys.path.insert(0, HERE)
 
 import numpy as np  # noqa: E402
 
-import assistedmanipulation_amd as am  # noqa: E402  (engine's ROCm runtime loads first)
-from assistedmanipulation_amd import abi  # noqa: E402
+am = abi = None   # the engine package, imported by run() - after the rank processes exist
 
 SAMPLES_PER_GPU = 4096
 HORIZON_STEPS = 64        # 0.64 s at dt = 0.01
@@ -54,6 +61,17 @@ PMC_JSON = os.path.join(HERE, "profiles", "r03g_pmc_rollout.json")
 PMC_WG_JSON = os.path.join(HERE, "profiles", "r03g_pmc_weights.json")   # weights_gradient_kernel's traffic
 
 
+def recorded_label(path):
+    """The PMC traffic beside the live timings is recorded, not measured in this run: name the
+    profile file and the kernel build it was collected on (its 'recorded' field)."""
+    try:
+        with open(path) as f:
+            rec = json.load(f).get("recorded", "")
+    except (OSError, ValueError):
+        rec = ""
+    return "recorded (not this run): %s%s" % (os.path.relpath(path, HERE), ", " + rec if rec else "")
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -69,7 +87,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the CPU baseline (0: the CPU share this process may use)")
-    p.add_argument("--cpu-updates", type=int, default=20, help="timed CPU updates (median / p90)")
+    p.add_argument("--cpu-updates", type=int, default=50, help="timed CPU updates (median / p90), BASELINE.md §2")
+    p.add_argument("--cpu-warmup", type=int, default=5, help="untimed CPU warm-up updates, BASELINE.md §2")
     p.add_argument("--graph", type=int, default=-1,
                    help="1: the hipGraph update path (mppi_set_graph), 0: eager launches, -1: the engine's default")
     a = p.parse_args()
@@ -102,9 +121,9 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def time_oracle(libpath, conf, dyn, cost, updates, compat_uint8=0, forecast=True):
+def time_oracle(libpath, conf, dyn, cost, updates, warmup, compat_uint8=0, forecast=True):
     """Median / p90 seconds per Trajectory::update of the oracle (its own steady_clock boundary,
-    mppi.cpp:161-184) over `updates` timed updates after one warm-up, t = 0.05 j."""
+    mppi.cpp:161-184) over `updates` timed updates after `warmup` untimed ones, t = 0.05 j."""
     from oracle import oracle as O
     cc, keep = conf.to_c()
     orc = O.OracleTrajectory(cc, dyn.descriptor(), cost.descriptor(), lib_path=libpath, compat_uint8=compat_uint8)
@@ -112,9 +131,10 @@ def time_oracle(libpath, conf, dyn, cost, updates, compat_uint8=0, forecast=True
     if forecast:
         orc.set_forecast(am.constant_forecast(orc.H))
     x = np.asarray(conf.initial_state, dtype=np.float64)
-    orc.update(x, 0.0)   # warm-up
+    for j in range(warmup):
+        orc.update(x, 0.05 * j)
     durs = []
-    for j in range(1, updates + 1):
+    for j in range(warmup, warmup + updates):
         orc.update(x, 0.05 * j)
         durs.append(orc.update_duration())
     return float(np.median(durs)), float(np.percentile(durs, 90)), orc.H
@@ -141,33 +161,100 @@ def cpu_baseline(args, pm):
         conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=KEEP_BEST,
                                                 threads=threads)
         dyn, cost = am.FrankaRidgebackDynamics(), am.AssistedManipulation()
-    med, p90, Ho = time_oracle(libpath, conf, dyn, cost, args.cpu_updates, forecast=not pm)
+    med, p90, Ho = time_oracle(libpath, conf, dyn, cost, args.cpu_updates, args.cpu_warmup, forecast=not pm)
+    nproc = os.cpu_count() or 0
     out = {"value": S * Ho / med, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
-           "median_s_per_update": med, "p90_s_per_update": p90,
-           "sample": "%d timed updates of the %dx%d %s workload, oracle/mppi_oracle.cpp fp64, %d threads "
-                     "(the process's CPU share; host %s, %d logical CPUs), -march=native" % (
-                         args.cpu_updates, S, Ho, "point-mass" if pm else "FrankaRidgeback", threads, cpu_model(),
-                         os.cpu_count() or 0)}
+           "median_s_per_update": med, "p90_s_per_update": p90, "warmup_updates": args.cpu_warmup,
+           "timed_updates": args.cpu_updates, "process_cpu_share": cpu_share(), "host_nproc": nproc,
+           "cpu_model": cpu_model(),
+           "sample": "%d warm-up + %d timed updates of the %dx%d %s workload (BASELINE.md §2), "
+                     "oracle/mppi_oracle.cpp fp64, g++ -O3 -march=native, %d threads: the process's CPU share "
+                     "(affinity mask capped by OMP_NUM_THREADS), not the host's nproc %d, which the GPU box "
+                     "shares between its GPUs; host %s" % (
+                         args.cpu_warmup, args.cpu_updates, S, Ho, "point-mass" if pm else "FrankaRidgeback",
+                         threads, nproc, cpu_model())}
     if not pm:   # configs[0]: the reference's own plumbing case, single thread, uint8 indices
         c0 = am.frankaridgeback_configuration(rollouts=128, horison=0.32, keep_best_rollouts=KEEP_BEST, threads=1)
         m0, q0, H0 = time_oracle(libpath, c0, am.FrankaRidgebackDynamics(), am.AssistedManipulation(),
-                                 args.cpu_updates, compat_uint8=1)
+                                 args.cpu_updates, args.cpu_warmup, compat_uint8=1)
         out["configs0"] = {"value": 128 * H0 / m0, "unit": "rollout-steps/s", "cores": 1,
                            "median_s_per_update": m0, "p90_s_per_update": q0,
+                           "warmup_updates": args.cpu_warmup, "timed_updates": args.cpu_updates,
                            "workload": "128 x 32 FrankaRidgeback, single thread, uint8 index semantics (BASELINE configs[0])"}
     return out
 
 
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: start the N rank processes (this script again, one GPU
+    each: LOCAL_RANK = RANK) with the rendezvous on 127.0.0.1, and return the exit status.  This
+    process has imported no engine code and made no HIP call; it only waits.  If one rank fails
+    the others are stopped (their exact PIDs), so a broken rendezvous does not hang the run."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def bootstrap_only(world, rank, local_rank, dist):
+    """MPPI_BENCH_BOOTSTRAP_ONLY=1 (CPU tests): stop after the gloo rendezvous and the broadcast of
+    a stand-in for the RCCL unique id, before the engine loads; rank 0 prints what it saw."""
+    uid = [os.urandom(128) if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": local_rank, "uid": uid[0].hex(), "pid": os.getpid(),
+                                  "engine_loaded": "assistedmanipulation_amd" in sys.modules})
+    if rank == 0:
+        print(json.dumps({"bootstrap_only": True, "n_gpus": world, "ranks": seen}))
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    pm = args.workload == "point_mass"
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d (launch N ranks with --gpus N)" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist  # bootstrap + barrier / max-over-ranks only (gloo)
         dist.init_process_group("gloo")
+        if os.environ.get("MPPI_BENCH_BOOTSTRAP_ONLY") == "1":
+            bootstrap_only(world, rank, local_rank, dist)
+            return
+    run(args, world, rank, local_rank, dist)
+
+
+def run(args, world, rank, local_rank, dist):
+    global am, abi
+    import assistedmanipulation_amd as am_  # the engine's ROCm runtime loads here, in the rank process
+    from assistedmanipulation_amd import abi as abi_
+    am, abi = am_, abi_
+    pm = args.workload == "point_mass"
     S_total = args.samples_per_gpu * world
     horison = args.horizon_steps * 0.01
     sg = am.Smoothing(args.smoothing, 1) if (args.smoothing > 0 and not pm) else None
@@ -279,8 +366,8 @@ def main():
                     "compute": "fp64 VALU, issue-bound at one wave per SIMD (no dense contraction for MFMA)",
                     "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
-                    "traffic_unit": "HBM bytes per rollout launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
-                                    os.path.relpath(PMC_JSON, HERE),
+                    "traffic_unit": "HBM bytes per rollout launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_source": recorded_label(PMC_JSON),
                     "flops_per_rollout_step": flops_unit,
                     "launch_bytes_by_design": launch_bytes,
                     "launch_GBs_by_design": launch_bytes / (dyn_ms * 1e-3) / 1e9}
@@ -307,6 +394,7 @@ def main():
         if os.path.exists(PMC_WG_JSON) and world == 1 and default_workload and not pm:
             with open(PMC_WG_JSON) as f:
                 wg["traffic"] = json.load(f)["traffic_bytes"]
+            wg["traffic_source"] = recorded_label(PMC_WG_JSON)
         hbm["weight_reduce"] = wg
     if rank != 0:
         if dist:

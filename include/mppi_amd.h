@@ -386,10 +386,19 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 #define MPPI_INFO_ROWS 5                  /* rows rolled out (local rollouts + a folded filter()) */
 #define MPPI_INFO_HANDOVER 6              /* step at which the fifth wave's rows moved off the doubled
                                              SIMD (take_over), -1 none; read from the device */
-#define MPPI_INFO_WAIT_TIMEOUTS 7         /* in-launch waits that gave up since create (a bug if
-                                             nonzero; the launch went on); read from the device */
-#define MPPI_UPDATE_INFO_N 8
+#define MPPI_INFO_WAIT_TIMEOUTS 7         /* in-launch waits that gave up in the last update's
+                                             rollout launch (a bug if nonzero: that update then
+                                             failed with MPPI_ERR_DEVICE and published nothing) */
+#define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
+#define MPPI_UPDATE_INFO_N 9
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
+
+/* Fault injection for the failure-detection tests (no reference counterpart; never set in
+ * production): the next `updates` rollout launches carry fault bits `fault`.
+ * MPPI_DEBUG_RELAY_NO_SIGNAL: relay stage 1 of the workgroup with rows left over never signals
+ * stage 2, so the bounded in-launch waits give up and the update must fail (MPPI_ERR_DEVICE). */
+#define MPPI_DEBUG_RELAY_NO_SIGNAL 1
+mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates);
 
 /* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control
  * dimension the value and time buffers (C x (H + 2w + 1), row per dimension) and start index. */

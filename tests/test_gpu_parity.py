@@ -645,3 +645,38 @@ def test_optimal_rollout_term_totals(energy):
         assert (td[3] != 0.0) == energy and td[1] > 0.0
         assert abs(td.sum() - dev.get_optimal_total_cost()) <= 1e-12 * abs(dev.get_optimal_total_cost())
         assert_update_parity(dev, orc, "terms upd %d" % j)
+
+
+def test_in_launch_wait_timeout_fails_the_update():
+    """A bounded in-launch wait that gives up (fr_coop.hip: relay stage 1 never signals stage 2,
+    injected with mppi_debug_inject) leaves the relay rows' costs unwritten, so the update fails
+    with MPPI_ERR_DEVICE and publishes nothing, as the reference refuses to go on when optimise()
+    throws (mppi.cpp:369-370).  The oracle cannot lose rows, so its side of the failed update is an
+    all-NaN failure at the same time with the same noise: both leave U* unpublished, no filter(),
+    and the same shift.  keep_best 0 makes the next update independent of the failed update's
+    costs (which differ: the device's are real where the oracle's are NaN), so the updates after
+    the failure must match the oracle again."""
+    conf, dev, orc, sd = fr_pair(S=4096, horison=0.64, K=0, threads=16)
+    rng = np.random.default_rng(31)
+    x = am.huddled_state()
+    step_both(dev, orc, x, 0.0, rng, sd)
+    assert_update_parity(dev, orc, "before", check_optimal=False)
+    u_before = dev.get_optimal_rollout().copy()
+    n = orc.noise_draws(0.05)
+    eps = rng.standard_normal((n, 12)) * sd
+    dev.inject_noise(eps)
+    orc.inject_noise(eps)
+    bad = x.copy()
+    bad[12:24] = np.nan
+    with pytest.raises(RuntimeError, match="ALL_NAN"):
+        orc.update(bad, 0.05)
+    dev.debug_inject(abi.MPPI_DEBUG_RELAY_NO_SIGNAL, 1)
+    with pytest.raises(am.EngineError, match="wait timed out"):
+        dev.update(x, 0.05)
+    info = dev.update_info()
+    assert info["wait_timeouts"] > 0 and info["wait_timeouts_total"] == info["wait_timeouts"], info
+    np.testing.assert_array_equal(dev.get_optimal_rollout(), u_before)   # nothing published
+    for j in (2, 3, 4):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        assert dev.update_info()["wait_timeouts"] == 0
+        assert_update_parity(dev, orc, "after timeout %d" % j)

@@ -1,0 +1,140 @@
+#!/bin/bash
+# The one GPU-box launcher (run through gpurun from the repo root): every step under its own time
+# limit, steps chained so that the first failure ends the call.  Replaces rounds 1-3's one-off
+# tools/gpu_*.sh scripts (in git history before round 4).
+#
+#   TAG=r04a bash tools/gpu_run.sh STEP [STEP ...]
+#
+# STEP is one of
+#   smoke              __graft_entry__.smoke()
+#   tests[:EXPR]       the whole -m gpu suite in one pytest process (or -k EXPR)
+#   bench              the default bench line (N = 1, with the CPU baseline)
+#   trace              rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
+#   pmc                rocprofv3 PMC passes (one counter set per run) -> pmc summaries + traffic JSON
+#   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
+#                      65536x128 SG)
+#   ab:V1,V2,..:N      N interleaved rounds of bench over kernel variants (gpurun_variants/<V>/,
+#                      built by tools/ab_build.sh; "tree" = the in-tree library); BENCH_ARGS and
+#                      AB_ENV_<V> (extra env for variant V, e.g. AB_ENV_tree0="MPPI_HANDOVER=0") apply
+#   wtrace:VARIANT     per-wave trace of VARIANT's COOP_TRACE build (tools/wave_trace_r03.py)
+# Output: gpurun_out/$TAG/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-run}
+O=gpurun_out/$TAG
+mkdir -p $O
+BENCH_ARGS=${BENCH_ARGS:-}
+
+summary() {   # file label
+    python3 - "$1" "$2" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().split('\n')[-1])
+k = d.get("kernel_ms", {})
+r = d.get("roofline", {})
+print("%-16s ms/update %.4f value %.4e launch %s frac %s" % (sys.argv[2], d["ms_per_step"], d["value"],
+      k.get("rollout_launch"), r.get("frac")))
+PY
+}
+
+step_smoke() {
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+        || { echo "smoke rc=$?"; tail -30 $O/smoke.log; return 1; }
+    echo "smoke ok"
+}
+
+step_tests() {   # [expr]
+    local k=()
+    [ -n "$1" ] && k=(-k "$1")
+    timeout -k 10 1000 python -u -m pytest tests -m gpu "${k[@]}" -v -s --timeout 240 --timeout-method thread \
+        > $O/pytest.log 2>&1
+    local rc=$?
+    grep -E "FAILED|ERROR|passed|failed" $O/pytest.log | tail -20
+    return $rc
+}
+
+step_bench() {
+    timeout -k 10 300 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err \
+        || { echo "bench rc=$?"; tail -20 $O/bench.err; return 1; }
+    summary $O/bench.json bench
+}
+
+step_trace() {
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
+        python3 bench.py --no-cpu-baseline $BENCH_ARGS > $O/bench_traced.json 2> $O/trace.err \
+        || { echo "trace rc=$?"; tail -20 $O/trace.err; return 1; }
+    summary $O/bench_traced.json traced
+    local st
+    st=$(find $O/trace -name "run_kernel_stats.csv" | head -n 1)
+    [ -n "$st" ] && cp "$st" $O/kernel_stats.csv && head -8 $O/kernel_stats.csv
+    return 0
+}
+
+step_pmc() {
+    local B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline $BENCH_ARGS" D=$O/pmc
+    mkdir -p $D
+    run() {   # name counters...
+        local n=$1; shift
+        timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace -d $D -o $n --output-format csv -- $B > $D/$n.log 2>&1
+    }
+    run sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY && echo "pmc sq ok" && \
+    run lat SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && echo "pmc lat ok" && \
+    run flops SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_UNALIGNED_STALL && echo "pmc flops ok" && \
+    run fetch FETCH_SIZE GRBM_GUI_ACTIVE && echo "pmc fetch ok" && \
+    run write WRITE_SIZE && echo "pmc write ok" || return 1
+    for n in sq lat flops fetch write; do python3 tools/pmc_summary.py $D/${n}_counter_collection.csv > $D/${n}_summary.txt; done
+    python3 tools/pmc_traffic.py $D $O/pmc_rollout.json && cat $O/pmc_rollout.json
+}
+
+step_sizes() {
+    size() {   # name args...
+        local n=$1; shift
+        timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > $O/size_$n.json 2> $O/size_$n.err \
+            || { echo "size $n rc=$?"; tail -5 $O/size_$n.err; return 1; }
+        summary $O/size_$n.json $n
+    }
+    size pm --workload point_mass --steps 200 --warmup 10 && \
+    size s32k --steps 20 --warmup 3 --samples-per-gpu 32768 && \
+    size s8k_h128_sg --steps 40 --warmup 3 --samples-per-gpu 8192 --horizon-steps 128 --smoothing 10 && \
+    size s64k_h128_sg --steps 8 --warmup 2 --samples-per-gpu 65536 --horizon-steps 128 --smoothing 10
+}
+
+step_ab() {   # V1,V2,..  rounds
+    local vs rounds=${2:-3}
+    IFS=, read -ra vs <<< "$1"
+    for i in $(seq 1 $rounds); do
+        for v in "${vs[@]}"; do
+            local lib=$PWD/assistedmanipulation_amd/lib/libmppi_amd.so
+            case $v in tree*) ;; *) lib=$PWD/gpurun_variants/$v/libmppi_amd.so;; esac
+            local envv="AB_ENV_$v" f=$O/ab_${v}_$i.json
+            env MPPI_AMD_LIB=$lib ${!envv} timeout -k 10 200 python -u bench.py --no-cpu-baseline $BENCH_ARGS \
+                > $f 2> $O/ab_${v}_$i.err || { echo "ab $v rc=$?"; tail -20 $O/ab_${v}_$i.err; return 1; }
+            summary $f "$v/$i"
+        done
+    done
+}
+
+step_wtrace() {   # variant
+    local lib=$PWD/gpurun_variants/$1/libmppi_amd.so
+    MPPI_WAVE_TRACE=$PWD/$O/wt.bin MPPI_AMD_LIB=$lib timeout -k 10 120 python bench.py --steps 5 --warmup 2 \
+        --no-cpu-baseline $BENCH_ARGS > $O/wt.json 2> $O/wt.err || { echo "wtrace rc=$?"; tail $O/wt.err; return 1; }
+    python3 tools/wave_trace_r03.py $O/wt.bin 1026 relay
+}
+
+for s in "$@"; do
+    name=${s%%:*}
+    arg=${s#*:}
+    [ "$arg" = "$s" ] && arg=""
+    case $name in
+        smoke) step_smoke ;;
+        tests) step_tests "$arg" ;;
+        bench) step_bench ;;
+        trace) step_trace ;;
+        pmc) step_pmc ;;
+        sizes) step_sizes ;;
+        ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
+        wtrace) step_wtrace "$arg" ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac || { echo "step $s failed"; exit 1; }
+done
+exit 0
