@@ -1096,6 +1096,9 @@ struct LaneConst {
     int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
+#ifndef CI_SCAN
+    double desc[10];   // composite_dpp: 1.0 when body i + 2 is in the subtree of body j (lanes 0, 1: all)
+#endif
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
 };
@@ -1371,6 +1374,115 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 }
 
 
+// Composite inertia (h, Ib) of the lane's subtree as broadcast FMAs: v_c = sum over the source
+// lanes i = 2..11 of x_c[lane i] desc_i, desc_i = 1.0 when body i is in the lane's subtree (i >= j
+// on the chain 2..9, itself on the fingers 10 and 11).  Bodies 0 and 1 (the base's prismatic
+// joints) are in no subtree but their own and need no composite: their columns of M are the
+// constant composite mass on the diagonal (S_0, S_1 unit translations), whatever h and Ib hold.
+// Ninety v_fmac_f64_dpp in nine interleaved chains replace the four-level suffix scan (72 DPP
+// moves, 36 adds) and finger 10's select (18).  (r04)
+__device__ __forceinline__ void composite_dpp(const double *x, const double *desc, double *v)
+{
+#pragma unroll
+    for (int c = 0; c < 9; c++) v[c] = 0.0;
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %9, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        : "+&v"(v[0]), "+&v"(v[1]), "+&v"(v[2]), "+&v"(v[3]), "+&v"(v[4]), "+&v"(v[5]), "+&v"(v[6]), "+&v"(v[7]), "+&v"(v[8])
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]), "v"(desc[0]), "v"(desc[1]), "v"(desc[2]), "v"(desc[3]), "v"(desc[4]));
+    asm(""
+        "v_fmac_f64_dpp %0, %9, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %9, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %11, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %12, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %13, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %14, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %15, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %17, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        : "+&v"(v[0]), "+&v"(v[1]), "+&v"(v[2]), "+&v"(v[3]), "+&v"(v[4]), "+&v"(v[5]), "+&v"(v[6]), "+&v"(v[7]), "+&v"(v[8])
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]), "v"(desc[5]), "v"(desc[6]), "v"(desc[7]), "v"(desc[8]), "v"(desc[9]));
+}
+
 // Mass-matrix solve for the rollouts without the energy tank: qdd = M(q)^-1 tau_u, M by the
 // composite-rigid-body algorithm in world coordinates and eliminated by Gauss-Jordan, one column
 // per lane.  Equal to the zero-bias articulated-body pass in exact arithmetic; its serial chain is
@@ -1386,8 +1498,14 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const CoopBody &bd, double tau_l, double *Lk,
                                              uint64_t &t_mid)
 {
-    // (h, Ib) scanned; the subtree's mass is a per-lane constant of the body table (T_MC)
+    // (h, Ib) summed over the subtree; the subtree's mass is a per-lane constant of the body table (T_MC)
     double v[9] = {bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
+#ifndef CI_SCAN
+    {
+        const double x[9] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
+        composite_dpp(x, L.desc, v);
+    }
+#else   // round 3: suffix scan over the lanes (row_shl 1, 2, 4, 8), finger 10 its own subtree
     double own[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) own[k] = v[k];
@@ -1402,6 +1520,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     for (int k = 0; k < 9; k++) v[k] += shl<8>(v[k]);
 #pragma unroll
     for (int k = 0; k < 9; k++) v[k] = msel(L.m_j10, v[k], own[k]);
+#endif
 #endif
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
@@ -1674,6 +1793,15 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
             L.ancd[i] = d;
         }
+#ifndef CI_SCAN
+#pragma unroll
+        for (int i = 2; i < FR_NB; i++) {
+            const bool in = j < 2 || (j < FR_NB - 2 && i >= j) || i == j;   // fingers: themselves
+            double d = in ? 1.0 : 0.0;
+            asm volatile("" : "+v"(d));
+            L.desc[i - 2] = d;
+        }
+#endif
     }
     L.mc = M[T_MC];
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)

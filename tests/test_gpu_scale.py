@@ -175,7 +175,8 @@ def test_config4_savitzky_golay_h128(S, updates):
     print("cost errors (rel, /Delta, (J-Jmin)/Delta):", stats)
 
 
-@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10), (8192, 1.28, 10)])
+@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10), (8192, 1.28, 10),
+                                                     (4094, 0.64, 0)])
 def test_graph_path_equals_eager_launches(rollouts, horison, window):
     """The hipGraph path of update() (mppi_set_graph: the steady-state update captured once and
     replayed with each update's arguments written into its kernel nodes) gives the eager launches'
@@ -183,7 +184,9 @@ def test_graph_path_equals_eager_launches(rollouts, horison, window):
     interruption (reading the optimal cost runs filter() by itself, so the next update is eager).
     4096 x 128 with the Savitzky-Golay filter (window 10): configs[4]'s filter, sg_finish_kernel as
     the graph's finish node; 8192 x 128 with it is configs[4]'s share per GPU, whose rollouts are
-    the two-launch split (five kernel nodes)."""
+    the two-launch split (five kernel nodes).  4094 rollouts (R = 4096, a multiple of 16 rows)
+    leave filter() pending in a four-wave launch, a shape the graph does not replay: every update
+    runs eagerly (such a handle once failed every other update)."""
     sg = am.Smoothing(window, 1) if window else None
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
                                             smoothing=sg)
@@ -205,7 +208,8 @@ def test_graph_path_equals_eager_launches(rollouts, horison, window):
             if j == 6:
                 rec.append(t.get_optimal_total_cost())
         out[graph] = (rec, t.graph_updates())
-    assert out[0][1] == 0 and out[1][1] >= 5, out[1][1]
+    graphable = (rollouts + 2) % 16 != 0
+    assert out[0][1] == 0 and (out[1][1] >= 5 if graphable else out[1][1] == 0), out[1][1]
     for j, (a, b) in enumerate(zip(out[0][0], out[1][0])):
         if isinstance(a, float):
             assert a == b

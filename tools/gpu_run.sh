@@ -9,7 +9,9 @@
 #   smoke              __graft_entry__.smoke()
 #   tests[:EXPR]       the whole -m gpu suite in one pytest process (or -k EXPR)
 #   bench              the default bench line (N = 1, with the CPU baseline)
-#   trace              rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
+#   trace[:NAME]       rocprofv3 --kernel-trace --stats of the bench (no CPU baseline; BENCH_ARGS apply;
+#                      NAME names the output, default "trace")
+#   tracepm            trace of the point-mass workload (configs[1]), 200 updates
 #   pmc                rocprofv3 PMC passes (one counter set per run) -> pmc summaries + traffic JSON
 #   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
 #                      65536x128 SG)
@@ -59,14 +61,18 @@ step_bench() {
     summary $O/bench.json bench
 }
 
-step_trace() {
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
-        python3 bench.py --no-cpu-baseline $BENCH_ARGS > $O/bench_traced.json 2> $O/trace.err \
-        || { echo "trace rc=$?"; tail -20 $O/trace.err; return 1; }
-    summary $O/bench_traced.json traced
+step_trace() {   # [name] [extra bench args...]
+    local n=${1:-trace}; shift
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$n -o run --output-format csv -- \
+        python3 bench.py --no-cpu-baseline $BENCH_ARGS "$@" > $O/${n}_bench.json 2> $O/$n.err \
+        || { echo "trace rc=$?"; tail -20 $O/$n.err; return 1; }
+    summary $O/${n}_bench.json $n
     local st
-    st=$(find $O/trace -name "run_kernel_stats.csv" | head -n 1)
-    [ -n "$st" ] && cp "$st" $O/kernel_stats.csv && head -8 $O/kernel_stats.csv
+    st=$(find $O/$n -name "run_kernel_stats.csv" | head -n 1)
+    [ -n "$st" ] && cp "$st" $O/${n}_kernel_stats.csv && head -8 $O/${n}_kernel_stats.csv
+    local tr
+    tr=$(find $O/$n -name "run_kernel_trace.csv" | head -n 1)
+    [ -n "$tr" ] && python3 tools/trace_seq.py "$tr" > $O/${n}_seq.txt 2>&1
     return 0
 }
 
@@ -129,7 +135,8 @@ for s in "$@"; do
         smoke) step_smoke ;;
         tests) step_tests "$arg" ;;
         bench) step_bench ;;
-        trace) step_trace ;;
+        trace) step_trace "$arg" ;;
+        tracepm) step_trace tracepm --workload point_mass --steps 200 ;;
         pmc) step_pmc ;;
         sizes) step_sizes ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;

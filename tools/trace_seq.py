@@ -11,7 +11,9 @@ def main(path, label=""):
     seq = [(r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0], int(r["Start_Timestamp"]),
             int(r["End_Timestamp"])) for r in rows]
     gap, dur = collections.defaultdict(list), collections.defaultdict(list)
-    starts = [s for n, s, e in seq if n == "fr_coop_x_kernel"]
+    lead = next((k for k in ("fr_coop_x_kernel", "pm_update_kernel", "pm_rollout_kernel", "fr_coop_kernel")
+                 if any(n == k for n, _, _ in seq)), seq[0][0])
+    starts = [s for n, s, e in seq if n == lead]
     for i in range(1, len(seq)):
         n, s, e = seq[i]
         if n.startswith("__amd") or seq[i - 1][0].startswith("__amd"):
@@ -20,7 +22,7 @@ def main(path, label=""):
         gap[key].append((s - seq[i - 1][2]) / 1e3)
         dur[n].append((e - s) / 1e3)
     h = len(starts) // 2   # second half of the updates (past warm-up)
-    period = (starts[-1] - starts[h]) / 1e3 / max(1, len(starts) - 1 - h)
+    period = (starts[-1] - starts[h]) / 1e3 / max(1, len(starts) - 1 - h) if len(starts) > 2 else 0.0
     print("%s update period %.1f us" % (label, period))
     for k, v in gap.items():
         v = v[len(v) // 2:]
