@@ -188,6 +188,11 @@ struct mppi_handle {
     // mppi_debug_inject: fault bits for the next debug_updates rollout launches (tests only)
     int debug_flags = 0, debug_updates = 0;
     bool published_once = false;   // an update has published U* (and so has a filter() row)
+    // the point mass in one launch per update (pm_fused.hip, launch_pm_update)
+    DevPointMass pm_host{};
+    unsigned *d_pm_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
+    double *d_pm_part = nullptr;     // [nblocks][H C] partial gradients, then [nblocks] normalisers
+    unsigned pm_epoch = 0, pm_nblocks = 0;
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -1015,6 +1020,12 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         }
         CREATE_TRY(dalloc(h, &h->d_pm, 1));
         CREATE_TRY(hipMemcpy(h->d_pm, &p, sizeof(p), hipMemcpyHostToDevice));
+        h->pm_host = p;
+        if (h->C == 3 && h->X == 6 && pm_fused_fits(h->R, (int)h->H)) {   // the one-launch update's scratch
+            h->pm_nblocks = (unsigned)((h->R + PM_FUSED_ROWS - 1) / PM_FUSED_ROWS);
+            CREATE_TRY(dalloc(h, &h->d_pm_sync, 2));
+            CREATE_TRY(dalloc(h, &h->d_pm_part, (size_t)h->pm_nblocks * (HC + 1)));
+        }
     }
     if (h->sg_window > 0) {
         const int w = h->sg_window;
@@ -1996,8 +2007,110 @@ mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count)
     return MPPI_OK;
 }
 
+// The point mass in one launch per update (pm_fused.hip): device Philox noise with a diagonal
+// transform, unsharded, no smoothing, timing off or level 1 (MPPI_PM_FUSED=0: the five launches)
+static bool pm_fused_eligible(const mppi_handle *h)
+{
+    const char *e = std::getenv("MPPI_PM_FUSED");
+    if (e && e[0] == '0') return false;
+    return h->dyn_kind == MPPI_DYNAMICS_POINT_MASS && h->d_pm_sync && h->noise_source == MPPI_NOISE_DEVICE_PHILOX &&
+           h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->host_trace && !h->d_trace;
+}
+
+static mppi_status update_pm_fused(mppi_handle *h, const double *state, double time)
+{
+    HIP_TRY(hipSetDevice(h->device));
+    h->t_start = std::chrono::steady_clock::now();
+    h->rollout_time = time;
+    h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);   // sample(): shift by truncation (mppi.cpp:194-201)
+    if (h->shift_by > 0) {
+        h->last_shift_time = time;
+        h->shifted = std::max<int64_t>(0, h->H - h->shift_by);
+    }
+    PmFusedArgs a{};
+    a.pm = h->pm_host;
+    a.steps = h->d_steps;
+    a.sp.shift_by = h->shift_by;
+    a.sp.shifted = h->shift_by > 0 ? h->shifted : h->H;
+    a.sp.keep = keep_count(h);
+    a.sp.update_index = h->update_count;
+    a.sp.seed = h->seed;
+    a.sp.tdiag = 1;
+    for (int c = 0; c < 3; c++) a.tdv[c] = h->T[(size_t)(c * h->C + c)];
+    std::memcpy(a.x0v, state, (size_t)h->X * sizeof(double));
+    a.x0_out = h->d_x0;
+    a.X = (int)h->X;
+    a.H = (int)h->H;
+    a.R = h->R;
+    a.Rpad = h->Rpad;
+    a.dt = h->dt;
+    a.rank = h->d_rank;
+    // this update's draws were made ahead by the previous launch's tail when nothing they depend on changed
+    a.ahead = h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
+              h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
+    h->ahead_valid = false;
+    std::swap(h->d_noise, h->d_noise_prev);   // this update's eps into the other buffer
+    a.prev = h->d_noise_prev;
+    a.noise = h->d_noise;
+    a.ahead_noise = h->d_noise_prev;          // free once the kept columns are copied (grid barrier)
+    a.cost = h->d_costs;
+    a.wexp = h->d_wexp;
+    a.stats = h->d_cstats;
+    a.status = h->d_status;
+    a.gpart = h->d_pm_part;
+    a.tpart = h->d_pm_part + (size_t)h->pm_nblocks * (size_t)(h->H * h->C);
+    a.bar = h->d_pm_sync;
+    a.ticket = h->d_pm_sync + 1;
+    a.epoch = ++h->pm_epoch;
+    a.nblocks = h->pm_nblocks;
+    a.cost_scale = h->cost_scale;
+    a.gradient_step = h->gradient_step;
+    a.control_bound = h->control_bound;
+    a.cmin = h->d_cmin;
+    a.cmax = h->d_cmax;
+    a.U = h->d_U;
+    a.Us = h->d_Us;
+    a.gradient = h->d_grad;
+    a.out = h->h_out_dev;
+    a.seq = (double)(++h->publish_seq);
+    a.opt_cost = h->d_opt;
+    a.x0_opt = h->d_x0_opt;
+    // a filter() of the five-launch path still running on the side stream reads d_U / d_x0_opt
+    if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+    hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
+    if (h->timing == 1) {   // the launch's event pair into the ring (mppi_rollout_kernel_times)
+        ev_r0 = h->ev_ring[2 * h->ring_head];
+        ev_r1 = h->ev_ring[2 * h->ring_head + 1];
+        h->ring_head = (h->ring_head + 1) % mppi_handle::EV_RING;
+        h->ring_count = std::min(h->ring_count + 1, (int)mppi_handle::EV_RING);
+        h->ring_unread = true;
+        HIP_TRY(hipEventRecord(ev_r0, h->stream));
+    }
+    HIP_TRY(launch_pm_update(a, h->stream));
+    if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
+    // filter() of this update runs in the same launch, after the publish (OPT_FOLDED: read behind
+    // the stream); the next update's draws are in d_noise_prev
+    h->opt_steps = h->d_steps;
+    h->opt_state = mppi_handle::OPT_FOLDED;
+    h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
+    h->ahead_valid = true;
+    h->info[MPPI_INFO_COOPERATIVE] = 0;
+    h->info[MPPI_INFO_FOLDED_FILTER] = 1;
+    h->info[MPPI_INFO_OBJECTIVE_IN_LAUNCH] = 1;
+    h->info[MPPI_INFO_TAIL_DRAWS] = 1;
+    h->info[MPPI_INFO_SAMPLING] = a.ahead ? 2 : 1;
+    h->info[MPPI_INFO_ROWS] = h->count;
+    h->info[MPPI_INFO_HANDOVER] = -1;
+    h->info[MPPI_INFO_FUSED_UPDATE] = 1;
+    h->updated_once = true;
+    h->phase_open = true;
+    return phase3_wait(h, a.seq);
+}
+
 mppi_status mppi_update(mppi_handle *h, const double *state, double time)
 {
+    if (h && state && pm_fused_eligible(h)) return update_pm_fused(h, state, time);
+    if (h) h->info[MPPI_INFO_FUSED_UPDATE] = 0;
     if (h && state && graph_eligible(h)) return update_graph(h, state, time);
     mppi_status st = mppi_update_phase1(h, state, time);
     if (st != MPPI_OK) return st;

@@ -350,6 +350,49 @@ hipError_t launch_fr_object(const ObjArgs &a, hipStream_t s);
 // forecast(t0 + k dt) for k < steps into out[steps][6] (mppi_forecast_table)
 hipError_t launch_forecast_table(const ForecastArgs &f, double t0, double dt, int64_t steps, double *out, hipStream_t s);
 hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
+
+// One launch per point-mass update (pm_fused.hip): sample, rollouts, optimise, finish, publish,
+// filter() and the next update's rank and draws, with one grid barrier.  Device Philox noise with a
+// diagonal transform, unsharded, no smoothing.
+constexpr int PM_FUSED_THREADS = 256;
+constexpr int PM_FUSED_ROWS = 64;                 // rollouts per block
+constexpr int64_t PM_FUSED_MAX_R = 64 * PM_FUSED_ROWS;
+struct PmFusedArgs {
+    DevPointMass pm;
+    const StepConst *steps;     // [H] gamma_k
+    SampleParams sp;
+    double tdv[3];              // diagonal noise transform
+    double x0v[MAX_X];          // the update's state by value
+    double *x0_out;             // [X] the rollout state (block 0)
+    int X;
+    int H;
+    int64_t R, Rpad;
+    double dt;
+    int *rank;                  // [R] stable order of the previous costs; rewritten for the next update
+    const double *prev;         // [H][Rpad][3] the previous update's eps
+    double *noise;              // [H][Rpad][3] this update's eps (draws made ahead when `ahead`)
+    double *ahead_noise;        // [H][Rpad][3] the next update's draws, or null
+    int ahead;
+    double *cost;               // [R]
+    double *wexp;               // [R] unnormalised weights e_r
+    CostStats *stats;
+    Status *status;
+    double *gpart;              // [nblocks][H C] partial gradients
+    double *tpart;              // [nblocks] partial normalisers
+    unsigned *bar, *ticket;     // monotonic arrival counters (targets epoch * nblocks)
+    unsigned epoch, nblocks;
+    double cost_scale, gradient_step;
+    int control_bound;
+    const double *cmin, *cmax;
+    double *U, *Us, *gradient;  // [H][3]
+    double *out;                // the mapped host block [H C + 8]
+    double seq;                 // its sequence flag value
+    double *opt_cost;           // filter()'s cost of the published U*
+    double *x0_opt;
+};
+bool pm_fused_fits(int64_t R, int H);
+size_t pm_fused_lds_bytes(int64_t R, int H);
+hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);
 // AssistedManipulation's seven per-term totals of one rollout from its [H][FR_NREC] records
 hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s);
 

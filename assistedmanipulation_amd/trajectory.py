@@ -424,7 +424,7 @@ class Trajectory:
         out = np.zeros(abi.MPPI_UPDATE_INFO_N, dtype=np.int64)
         self._check(self._L.mppi_update_info(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), out.size))
         keys = ("cooperative", "folded_filter", "objective_in_launch", "tail_draws", "sampling", "rows", "handover",
-                "wait_timeouts", "wait_timeouts_total")
+                "wait_timeouts", "wait_timeouts_total", "fused_update")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def debug_inject(self, fault, updates=1):

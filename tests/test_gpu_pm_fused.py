@@ -1,0 +1,90 @@
+"""The point mass (BASELINE configs[1]) in one launch per update (pm_fused.hip): against the
+five-launch path (MPPI_PM_FUSED=0) on the same device Philox stream, and against the oracle with
+the device's draws replayed in the reference's draw order (mppi.cpp:242-262)."""
+import numpy as np
+import pytest
+
+import assistedmanipulation_amd as am
+from assistedmanipulation_amd import abi
+from oracle import oracle as O
+
+from helpers import assert_update_parity, replay_device_draws
+
+pytestmark = pytest.mark.gpu
+
+TIMES = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17, 0.22]   # shifts of 5, 2, 5, 0, 5, 5 steps
+
+
+def _pm(S, horison, K=20):
+    conf = am.point_mass_configuration(rollouts=S, horison=horison, keep_best_rollouts=K)
+    t = am.Trajectory.create(conf, am.PointMassDynamics(), am.QuadraticCost())
+    assert t is not None
+    t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    return conf, t
+
+
+@pytest.mark.parametrize("S,horison", [(1024, 0.32), (1000, 0.32), (2046, 0.64), (62, 0.16)])
+def test_fused_update_equals_five_launches(S, horison, monkeypatch):
+    """Noise bit for bit (draws made ahead by the previous launch's tail, kept columns shifted in),
+    costs bit for bit (the same per-rollout arithmetic), weights / gradient / U* and the filter()
+    cost to the gradient's summation order (per-block partials in block order against the
+    weights kernel's eight splits)."""
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MPPI_PM_FUSED", fused)
+        conf, t = _pm(S, horison)
+        x = np.zeros(6)
+        rec = []
+        for j, tm in enumerate(TIMES):
+            t.update(x, tm)
+            info = t.update_info()
+            assert info["fused_update"] == (1 if fused == "1" else 0), info
+            if fused == "1":
+                assert info["sampling"] == (1 if j == 0 else 2), info   # drawn ahead from the second update
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_weights().copy(), t.get_gradient().copy(),
+                        t.get_optimal_rollout().copy(), t.get_optimal_total_cost()))
+            x = x + 0.01
+        out[fused] = rec
+    for j, (a, b) in enumerate(zip(out["1"], out["0"])):
+        np.testing.assert_array_equal(a[0], b[0], err_msg="update %d noise" % j)
+        np.testing.assert_array_equal(a[1], b[1], err_msg="update %d costs" % j)
+        np.testing.assert_allclose(a[2], b[2], rtol=1e-13, atol=1e-16, err_msg="update %d weights" % j)
+        np.testing.assert_allclose(a[3], b[3], rtol=0, atol=1e-12, err_msg="update %d gradient" % j)
+        np.testing.assert_allclose(a[4], b[4], rtol=0, atol=1e-12, err_msg="update %d U*" % j)
+        assert abs(a[5] - b[5]) <= 1e-12 * max(1.0, abs(b[5])), (j, a[5], b[5])
+
+
+@pytest.mark.parametrize("S", [1024, 130])
+def test_fused_update_against_oracle(S):
+    """The fused path's own draws replayed through the oracle: every update's costs, argmin,
+    weights, gradient, U* and filter() cost within the parity bars (tests/helpers.py)."""
+    conf, dev = _pm(S, 0.32)
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, dev.dynamics.descriptor(), dev.cost.descriptor())
+    x = np.zeros(6)
+    prev_costs, prev_noise = np.zeros(dev.R), np.zeros((dev.R, dev.H, dev.C))
+    for j, tm in enumerate(TIMES):
+        costs, noise = replay_device_draws(dev, orc, x, tm, prev_costs, prev_noise, 20)
+        assert dev.update_info()["fused_update"] == 1
+        assert_update_parity(dev, orc, "pm fused upd %d" % j)
+        prev_costs, prev_noise = costs, noise
+        x = x + 0.01
+
+
+def test_fused_update_all_nan_and_recovery():
+    """A NaN state makes every rollout cost NaN: the fused update throws "all nan rollouts"
+    (mppi.cpp:369-370) without publishing, and the next valid updates run fused again."""
+    conf, t = _pm(1024, 0.32)
+    x = np.zeros(6)
+    t.update(x, 0.0)
+    u0 = t.get_optimal_rollout().copy()
+    bad = x.copy()
+    bad[0] = np.nan
+    with pytest.raises(am.EngineError, match="ALL_NAN"):
+        t.update(bad, 0.05)
+    np.testing.assert_array_equal(t.get_optimal_rollout(), u0)
+    for j in (2, 3):
+        t.update(x, 0.05 * j)
+        info = t.update_info()
+        assert info["fused_update"] == 1 and info["wait_timeouts"] == 0, info
+        assert np.all(np.isfinite(t.costs()))
