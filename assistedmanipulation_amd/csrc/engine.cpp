@@ -193,6 +193,10 @@ struct mppi_handle {
     unsigned *d_pm_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
     double *d_pm_part = nullptr;     // [nblocks][H C] partial gradients, then [nblocks] normalisers
     unsigned pm_epoch = 0, pm_nblocks = 0;
+    // optimise() and finish() in the rollout launch's epilogue (fr_coop.hip epilogue)
+    unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
+    unsigned ep_total = 0;           // their value after the last epilogue launch
+    bool ep_ran = false;             // this update's rollout launch ran the epilogue
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -1008,6 +1012,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(dalloc(h, &h->d_cost, 1));
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
+        CREATE_TRY(dalloc(h, &h->d_ep_sync, 2));
         CREATE_TRY(launch_fr_body_table(h->d_model, h->d_cost, h->d_table, nullptr));
         CREATE_TRY(hipDeviceSynchronize());
     } else {
@@ -1481,12 +1486,27 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
     return MPPI_OK;
 }
 
+// optimise() and finish() in the rollout launch's epilogue: unsharded, no smoothing, the eager path
+// (the hipGraph path keeps its captured four-kernel chain), timing below level 2 (whose events
+// separate the kernels); MPPI_EPILOGUE=0 keeps the three launches (A/B)
+static bool epilogue_wanted(const mppi_handle *h)
+{
+    const char *e = std::getenv("MPPI_EPILOGUE");
+    if (e && e[0] == '0') return false;
+    return h->d_ep_sync && !sharded(h) && h->sg_window == 0 && h->timing < 2 && !h->graph_mode && !h->graph_dry &&
+           draw_ahead_possible(h) && !h->d_trace;
+}
+
+static WGradArgs wgrad_args(const mppi_handle *h);
+static FinishArgs finish_args(mppi_handle *h);
+
 mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
 {
     if (!h || !state) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
     h->tail_drawn = false;
+    h->ep_ran = false;
     if (h->host_trace && h->ht_n[0] > h->ht_n[1]) {
         h->ht_sum[1] += std::chrono::duration<double, std::micro>(h->t_start - h->ht_ret).count();
         h->ht_n[1]++;
@@ -1615,6 +1635,18 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         bool folded = false, costs_done = false, tail = false;
         CoopTail ct;
         a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
+        // optimise() and finish() in the launch's epilogue (launch_fr_coop_update takes it where the
+        // launch shape allows: one round of fr_coop_x_kernel with the draws made ahead)
+        a.epilogue = epilogue_wanted(h) ? 1 : 0;
+        if (a.epilogue) {
+            a.ep_sync = h->d_ep_sync;
+            a.ep_target = h->ep_total;
+            a.wg = wgrad_args(h);
+            a.fin = finish_args(h);   // its sequence: publish_seq + 1, as phase 3 publishes it
+            a.fin.rank_n = h->R;      // draw_ahead_possible: S <= RANK_TILED_MAX, rank_draw_kernel's tiles
+            // a filter() launched by itself on the side stream reads the d_U / d_x0_opt the epilogue rewrites
+            if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+        }
         // the next update's draws in the launch's tail, into the buffer it will write (phase 3 makes
         // the rest with the rank); needs the sampling arguments (fused launch) and no tail switch-off
         a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
@@ -1624,6 +1656,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
                                           &h->gargs.roll2));
             h->gargs.folded = folded;
             h->gargs.nroll = ct.launches;
+            h->ep_ran = !h->graph_dry && h->gargs.roll.epilogue != 0;
+            if (h->ep_ran) h->ep_total = h->gargs.roll.ep_target;
             if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
             if (!folded) a.fcost = nullptr;
             if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
@@ -1639,6 +1673,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : (fuse ? 1 : 0);
         h->info[MPPI_INFO_ROWS] = h->count + (folded ? 1 : 0);
         h->info[MPPI_INFO_HANDOVER] = h->gargs.x_kernel ? -2 : -1;   // -2: read from the device on request
+        h->info[MPPI_INFO_FUSED_UPDATE] = h->ep_ran ? 1 : 0;
         if (tail) {   // the rows the launch left to rank_draw_kernel (fr_coop.hip relay_stage, group_draws)
             h->tail_row0 = ct.row0;
             h->tail_xbase = ct.xbase;
@@ -1715,10 +1750,31 @@ static FinishArgs finish_args(mppi_handle *h)
     return f;
 }
 
+static WGradArgs wgrad_args(const mppi_handle *h)
+{
+    WGradArgs w{};
+    w.cost = h->d_costs;
+    w.R = h->R;
+    w.cost_scale = h->cost_scale;
+    w.status = h->d_status;
+    w.noise = h->d_noise;
+    w.begin = h->begin;
+    w.count = h->count;
+    w.Rpad = h->Rpad;
+    w.H = (int)h->H;
+    w.C = (int)h->C;
+    w.gsplit = h->d_gsplit;
+    w.wexp = h->d_wexp;
+    w.wpart = h->d_wpart;
+    w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
+    return w;
+}
+
 mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
+    if (h->ep_ran) return MPPI_OK;   // optimise() ran in the rollout launch's epilogue
     WGradArgs w{};
     w.cost = h->d_costs;
     w.R = h->R;
@@ -1749,7 +1805,7 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     h->gargs.fin = finish_args(h);
-    if (!h->graph_dry) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
+    if (!h->graph_dry && !h->ep_ran) HIP_TRY(launch_finish(h->gargs.fin, h->stream));   // (or in the epilogue)
     const double seq = (double)(++h->publish_seq);
     *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));

@@ -2121,7 +2121,8 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
             if (a.fcost != nullptr && r == a.count) {
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
             } else {
-                a.cost_out[a.begin + r] = J;
+                if (a.epilogue) __hip_atomic_store(a.cost_out + a.begin + r, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else a.cost_out[a.begin + r] = J;
                 mppi_cost::fold_cost_stats(a.stats, J, r);
             }
         }
@@ -2231,7 +2232,9 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
             return true;
         }
     }
-    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(1, H) : -1;
+    if (blockIdx.x == 0 && lane == 0)   // write-through: the epilogue's finisher reads this line (sc1)
+        __hip_atomic_store(&const_cast<Status *>(a.status)->handover, a.handover ? relay_step(1, H) : -1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
     return true;
 }
@@ -2327,9 +2330,16 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
 #pragma unroll
             for (int u = 0; u < UN; u++) {
                 if (k0 + 4 * u >= kend) break;
-                double2 *dst = reinterpret_cast<double2 *>(sa.noise + ((int64_t)(k0 + 4 * u) * sa.Rpad + lr) * FR_C + 4 * blk);
-                dst[0] = v[u][0];
-                dst[1] = v[u][1];
+                double *dst = sa.noise + ((int64_t)(k0 + 4 * u) * sa.Rpad + lr) * FR_C + 4 * blk;
+                if (a.epilogue) {   // write-through (sc1): the epilogue reads them from other XCDs in this launch
+                    __hip_atomic_store(dst + 0, v[u][0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(dst + 1, v[u][0].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(dst + 2, v[u][1].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(dst + 3, v[u][1].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    reinterpret_cast<double2 *>(dst)[0] = v[u][0];
+                    reinterpret_cast<double2 *>(dst)[1] = v[u][1];
+                }
             }
         }
     }
@@ -2344,7 +2354,7 @@ template <int NT>
 __device__ __forceinline__ void block0_sample_writes(const FrRolloutArgs &a, int t)
 {
     const SampleArgs &sa = a.samp;
-    if (sa.sp.shift_by > 0)
+    if (sa.sp.shift_by > 0 && !a.epilogue)   // (the epilogue's finisher writes U*_shifted itself)
         for (int i = t; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
     if (t < sa.X) sa.x0_out[t] = sa.x0v[t];
 }
@@ -2410,6 +2420,257 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
         }
     }
+}
+
+
+// ---- epilogue: optimise() and finish() inside the update launch (a.epilogue) -------------------
+// After the rows and their objective, every workgroup of the one-round launch meets at a grid
+// barrier (all 256 workgroups are resident: one per CU) and then runs weights_gradient_kernel's
+// (step, split) units, two per workgroup (waves 0..3 and 4..7, each the weights kernel's 256-thread
+// block), and the last workgroup to take the ticket runs finish_flat_kernel's publish.  The unit and
+// the finish are those kernels' arithmetic in the same order (kernels.hip), so every output is
+// bit-identical to the three-launch path; what goes is two launches and their boundaries.
+// Hand-offs inside the launch (MI355X_MICROARCH.md, Workgroup dispatch and visibility): bytes another
+// workgroup reads in this launch are stored write-through (sc1) and loaded sc1 - the costs, the
+// kept rows' eps copies, the units' partials and status words; everything else they read was
+// written by an earlier launch.  The barrier and the ticket are agent-scope adds by one lane per
+// workgroup after every wave drained its stores, polled with sc1 loads, bounded.
+constexpr int EP_GR = 3;   // weights_gradient_kernel's GR: rollouts per thread loaded up front
+constexpr int EP_BAR_SPINS = 1 << 23;
+constexpr int EP_MAXE = 4;   // U* elements per finisher thread: H C <= 4 x 512 (launch_fr_coop_update checks)
+
+__device__ __forceinline__ double ep_ld(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void ep_st(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int ep_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void ep_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// eps of rollout rr (local) at step k as the rollout launch used it: a kept row's columns were
+// copied in this launch (write-through), the rest are the draws made ahead by earlier launches
+__device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, int k, int64_t rr, double *e)
+{
+    const WGradArgs &a = fa.wg;
+    const double *n = a.noise + ((int64_t)k * a.Rpad + rr) * FR_C;
+    const SampleArgs &sa = fa.samp;
+    const int64_t g = a.begin + rr;
+    const bool kept = g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
+    if (kept) {
+#pragma unroll
+        for (int c = 0; c < FR_C; c++) e[c] = ep_ld(n + c);
+    } else {
+#pragma unroll
+        for (int c = 0; c < FR_C; c++) e[c] = n[c];
+    }
+}
+
+// weights_gradient_kernel<FR_C, false> (kernels.hip) block (k, s) = unit u (k = u mod H, s = u / H)
+// on 256 threads t, unsharded with the objective's statistics; u < 0: no unit (the barrier only)
+__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, double *red, double *ssum)
+{
+    const WGradArgs &a = fa.wg;
+    constexpr int CP = FR_C;
+    const int rw = t >> 6, l = t & 63;
+    const int64_t R = a.R;
+    const bool has = u >= 0;
+    const int k = has ? u % a.H : 0, s = has ? u / a.H : 0, ns = GRAD_SPLIT;
+    const int64_t chunk = (a.count + ns - 1) / ns;
+    const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
+    double ne[EP_GR][CP];
+    double cpre[EP_GR];
+#pragma unroll
+    for (int m = 0; m < EP_GR; m++) {
+        const int64_t r = r0 + t + 256 * m;
+        const int64_t rr = (has && r < r1) ? r : 0;
+        ep_eps(fa, k, rr, ne[m]);
+        cpre[m] = ep_ld(a.cost + a.begin + rr);
+    }
+    const bool own_slice = has && k == 0 && a.begin == 0 && a.count == R;
+    static_assert(CS_SLOTS == 64, "one slot per lane");
+    const unsigned long long kn = mppi_dev::wave_umin64_dpp(
+        __hip_atomic_load(&a.stats->kmin[16 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned long long kx = mppi_dev::wave_umax64_dpp(
+        __hip_atomic_load(&a.stats->kmax[16 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const unsigned int n = (unsigned int)mppi_dev::wave_sum_dpp(
+        (double)__hip_atomic_load(&a.stats->count[32 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double minimum = n ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
+    const double maximum = n ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
+    const double valid = (double)n;
+    const bool lead = has && k == 0 && s == 0 && t == 0;
+    Status *st = a.status;
+    if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
+        if (lead) {
+            ep_sti(&st->all_nan, 1);
+            ep_sti(&st->early, 1);
+            ep_st(&st->minimum, minimum);
+            ep_st(&st->maximum, maximum);
+        }
+        return;
+    }
+    const double difference = maximum - minimum;
+    if (difference < 1e-6) {   // early return, weights/gradient stale (mppi.cpp:373-375)
+        if (lead) {
+            ep_sti(&st->all_nan, 0);
+            ep_sti(&st->early, 1);
+            ep_st(&st->minimum, minimum);
+            ep_st(&st->maximum, maximum);
+        }
+        return;
+    }
+    auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
+    if (lead) {
+        ep_sti(&st->all_nan, 0);
+        ep_sti(&st->early, 0);
+        ep_st(&st->minimum, minimum);
+        ep_st(&st->maximum, maximum);
+    }
+    double acc[CP];
+#pragma unroll
+    for (int c = 0; c < CP; c++) acc[c] = 0.0;
+    double part = 0.0;
+#pragma unroll
+    for (int m = 0; m < EP_GR; m++) {
+        const int64_t r = r0 + t + 256 * m;
+        if (has && r < r1) {
+            const double wr = expw(cpre[m]);
+            if (own_slice) {
+                a.wexp[r] = wr;
+                part += wr;
+            }
+#pragma unroll
+            for (int c = 0; c < CP; c++) acc[c] += wr * ne[m][c];
+        }
+    }
+    for (int64_t r = r0 + t + 256 * EP_GR; has && r < r1; r += 256) {
+        const double wr = expw(ep_ld(a.cost + a.begin + r));
+        if (own_slice) {
+            a.wexp[r] = wr;
+            part += wr;
+        }
+        double e[CP];
+        ep_eps(fa, k, r, e);
+#pragma unroll
+        for (int c = 0; c < CP; c++) acc[c] += wr * e[c];
+    }
+    if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
+        part = mppi_dev::wave_sum_dpp(part);
+        if (l == 0) ssum[rw] = part;
+    }
+#pragma unroll
+    for (int c = 0; c < CP; c++) acc[c] = mppi_dev::wave_sum_dpp(acc[c]);
+    if (l == 0)
+#pragma unroll
+        for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
+    __syncthreads();   // both halves of the workgroup reach it (the early returns above are uniform)
+    if (has && t < CP)
+        ep_st(a.gsplit + ((int64_t)s * a.H + k) * FR_C + t, (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]));
+    if (own_slice && t == 0) ep_st(&st->tsplit[s], (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]));
+}
+
+// finish_flat_kernel (kernels.hip) by the last workgroup, NT threads: the units' partials and status
+// words loaded sc1; U*_shifted from U* (block 0 did not write it in this launch) and the state by value
+template <int NT>
+__device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
+{
+    const FinishArgs &a = fa.fin;
+    const SampleArgs &sa = fa.samp;
+    const int HC = a.H * a.C;
+    Status *st = const_cast<Status *>(a.status);
+    const int wt = __hip_atomic_load(&st->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int early = ep_ldi(&st->early), all_nan = ep_ldi(&st->all_nan);
+    const bool upd = !early && !wt, ok = !all_nan && !wt;
+    double tsp[GRAD_SPLIT];
+#pragma unroll
+    for (int i = 0; i < GRAD_SPLIT; i++) tsp[i] = ep_ld(&st->tsplit[i]);
+    double total = tsp[0];
+#pragma unroll
+    for (int i = 1; i < GRAD_SPLIT; i++) total += tsp[i];
+    const double *__restrict__ gs = a.gsplit;
+    double *__restrict__ U = a.U;
+    // U*_shifted reads U* at shifted positions: every element's inputs are read before any U* store
+    double us[EP_MAXE], uos[EP_MAXE];
+#pragma unroll
+    for (int e = 0; e < EP_MAXE; e++) {
+        const int t = tid + e * NT;
+        if (t < HC) {
+            us[e] = sa.sp.shift_by > 0 ? mppi_sample::shifted_u(sa, t / a.C, t % a.C) : a.Ushift[t];
+            uos[e] = U[t];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EP_MAXE; e++) {
+        const int t = tid + e * NT;
+        if (t >= HC) break;
+        const int c = t % a.C;
+        double g = ep_ld(gs + t);
+        for (int i = 1; i < GRAD_SPLIT; i++) g += ep_ld(gs + (int64_t)i * HC + t);
+        g /= total;   // sum_r e_r eps_r / sum_r e_r
+        double u = us[e];
+        const double uo = uos[e];
+        const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
+        if (upd) {
+            a.gradient[t] = g;
+            u += g * a.gradient_step;
+            if (a.control_bound) {
+                u = smin(u, hi);
+                u = smax(u, lo);
+            }
+        }
+        a.Ushift[t] = u;   // U*_shifted as sample() and the gradient step leave it
+        const double v = ok ? u : uo;
+        if (ok) U[t] = v;
+        a.out[t] = v;
+    }
+    if (tid < a.X) a.x0_opt[tid] = sa.x0v[tid];
+    for (int64_t i = tid; i < a.rank_n; i += NT) a.rank_zero[i] = 0;   // for rank_draw_kernel's tiles
+    if (tid == 0) {
+        st->sg_error = wt != 0;   // read by the next filter() row as "the update threw"
+        if (upd) st->total = total;
+        a.out[HC + 0] = 0.0;      // (the folded filter() cost is read behind the stream)
+        a.out[HC + 1] = (double)all_nan;
+        a.out[HC + 2] = (double)early;
+        a.out[HC + 3] = 0.0;
+        a.out[HC + 4] = ep_ld(&st->minimum);
+        a.out[HC + 5] = ep_ld(&st->maximum);
+        a.out[HC + 7] = (double)wt;
+    }
+    if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, tid);
+    __syncthreads();
+    if (tid == 0) {
+        st->wait_timeouts = 0;
+        __threadfence_system();
+        __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// the epilogue of fr_coop_x_kernel (NT = 64 XW threads): barrier, units, ticket, finish
+template <int NT>
+__device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, int *Lint)
+{
+    const int t = threadIdx.x;
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's cost stores, atomics and eps copies have left it
+    __syncthreads();
+    if (t == 0) {   // every workgroup's costs and statistics are final
+        __hip_atomic_fetch_add(a.ep_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int i = 0;
+        while (__hip_atomic_load(a.ep_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.ep_target && i < EP_BAR_SPINS) {
+            __builtin_amdgcn_s_sleep(2);
+            i++;
+        }
+        if (i == EP_BAR_SPINS) note_wait_timeout(a);   // the update then fails
+    }
+    __syncthreads();
+    const int groups = gridDim.x, half = t >> 8, ht = t & 255;
+    const int nunits = a.wg.H * GRAD_SPLIT, per = 2 * groups;
+    for (int base = 0; base < nunits; base += per) {
+        const int u = base + half * groups + (int)blockIdx.x;
+        ep_unit(a, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8);
+        __syncthreads();   // the halves' LDS is reused by the next pass
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // every wave's unit stores have left it
+    __syncthreads();
+    if (t == 0) Lint[0] = __hip_atomic_fetch_add(a.ep_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == a.ep_target;
+    __syncthreads();
+    if (Lint[0]) ep_finish<NT>(a, t);
 }
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and four more
@@ -2481,12 +2742,13 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const int s = wv - 4;   // this wave's SIMD
         const bool relay = xr && (s == 0 || a.handover);
         if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
-        if (!cil) return;
+        if (!cil) return;   // (no epilogue without the objective in the launch)
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
         if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
         cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
+    if (a.epilogue) epilogue<64 * XW>(a, Lcs, Lflag);   // every wave; Lcs and Lflag are free now
 }
 
 namespace mppi_eng {
@@ -2646,6 +2908,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
         a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;
         a.handover = handover_enabled() ? 1 : 0;
         if (!a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
+        a.epilogue = 0;   // (two launches: optimise and finish stay separate launches)
         FrRolloutArgs A = row_slice(a, 0, n0), B = row_slice(a, n0, rest);
         A.fcost = nullptr;   // the previous filter() rides with the rows left over
         A.xbase = n0;
@@ -2677,6 +2940,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     FrRolloutArgs a = a0;
     if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
         if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
+        a.epilogue = 0;
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
         a.costs_in_launch = groups > 0 && costs_in_launch_enabled() ? 1 : 0;   // each wave its own rows'
@@ -2697,6 +2961,11 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
     if (xrows == 0 || !a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
+    // the epilogue: fr_coop_x_kernel with the objective in the launch and the draws made ahead (the
+    // finisher reads the state and U* by value / from U*), at most EP_MAXE U* elements per thread
+    a.epilogue = (a0.epilogue && xrows != 0 && a.costs_in_launch && a.fuse_sample == 2 && a.H * FR_C <= EP_MAXE * 64 * XW &&
+                  a.ep_sync != nullptr) ? 1 : 0;
+    a.ep_target = a0.ep_target + (a.epilogue ? (unsigned)groups : 0u);
     *tail_drawn = a.ahead_noise != nullptr;
     if (final) *final = a;
     if (x_kernel) *x_kernel = xrows != 0;

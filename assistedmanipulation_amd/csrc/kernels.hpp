@@ -62,6 +62,61 @@ struct SampleArgs {
     double tdv[FR_C];   // diagonal noise transform by value (tdiag launches: no loads of T)
 };
 
+// optimise() and the partial gradient in one launch (kernels.hip weights_gradient_kernel)
+struct WGradArgs {
+    const double *cost;    // [R], global rollout index
+    int64_t R;
+    double cost_scale;
+    Status *status;
+    const double *noise;   // [H][Rpad][C]
+    int64_t begin, count, Rpad;
+    int H, C;
+    double *gsplit;        // [GRAD_SPLIT][H][C]
+    double *wexp;          // [R] unnormalised weights e_r (weights = e_r / Status::total)
+    double *wpart;         // [4 * 64] scratch: per-chunk min / max / count / sum (R > SM_LARGE_R)
+    const CostStats *stats;   // min / max / count from the cost kernel (unsharded), or null: a pass
+};
+
+struct FinishArgs {
+    const Status *status;
+    Status *status_w;
+    const double *gsplit;       // [ns][H][C] gradient stage-1 partials (ns > 0: summed here)
+    int ns;
+    const double *gpart;        // [H][C] summed (all-reduced when sharded) gradient, ns == 0
+    double *gradient;
+    double *Ushift;
+    const double *cmin, *cmax;
+    double gradient_step;
+    int control_bound;
+    int H, C;
+    double t0, dt;
+    // Savitzky-Golay state (window 0 = disabled)
+    int sg_window;
+    const double *sg_weights;   // [2w+1]
+    double *sg_uu, *sg_tt;      // [C][H + 2w + 1]
+    int64_t *sg_start;          // [C]
+    double *sg_last_trim;       // [C]
+    // publish: U* <- U*_shifted and the host-visible block [U (H*C), optimal cost, status]
+    double *U;
+    const double *opt_cost;
+    double *out;                // host block [HC + 8]: U*, then status words, then the sequence flag
+    double seq;                 // written to out[HC + 6] last, system-scope release (host polls it)
+    // filter()'s state: the update's x0 copied for the optimal rollout that runs after it
+    const double *x0;
+    double *x0_opt;
+    int X;
+    // the next rank launch accumulates into rank[]: zeroed here when it is the tiled kernel
+    int *rank_zero;
+    int64_t rank_n;
+    // the cost statistics, consumed by weights_gradient_kernel ahead of this launch: reset here for
+    // the next update's folds (stream-ordered before its rollout launch; may be null)
+    CostStats *stats_reset;
+    // the update's in-launch wait timeouts: every rank's (the all-reduced cost slot R) when sharded
+    // over RCCL, else null (Status::wait_timeouts); wait_local: this rank's slot, reset here
+    const double *wait_all;
+    double *wait_local;
+};
+
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;
@@ -114,6 +169,14 @@ struct FrRolloutArgs {
     // MPPI_DEBUG_* fault injection (mppi_debug_inject; 0 in production): bit 0, relay stage 1 of
     // the workgroup with rows left over never signals stage 2 (tests the wait-timeout failure)
     int debug;
+    // epilogue (fr_coop_x_kernel, one round, draws ahead, no smoothing, unsharded): after an
+    // in-launch grid barrier the workgroups run weights_gradient_kernel's (step, split) units and
+    // the last to arrive runs finish_flat_kernel's publish, in place of those two launches
+    int epilogue;
+    unsigned *ep_sync;            // [2] barrier and ticket counters (monotonic)
+    unsigned ep_target;           // their value once every workgroup of this launch has added 1
+    WGradArgs wg;
+    FinishArgs fin;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -160,45 +223,7 @@ struct PmRolloutArgs {
     int optimal;
 };
 
-struct FinishArgs {
-    const Status *status;
-    Status *status_w;
-    const double *gsplit;       // [ns][H][C] gradient stage-1 partials (ns > 0: summed here)
-    int ns;
-    const double *gpart;        // [H][C] summed (all-reduced when sharded) gradient, ns == 0
-    double *gradient;
-    double *Ushift;
-    const double *cmin, *cmax;
-    double gradient_step;
-    int control_bound;
-    int H, C;
-    double t0, dt;
-    // Savitzky-Golay state (window 0 = disabled)
-    int sg_window;
-    const double *sg_weights;   // [2w+1]
-    double *sg_uu, *sg_tt;      // [C][H + 2w + 1]
-    int64_t *sg_start;          // [C]
-    double *sg_last_trim;       // [C]
-    // publish: U* <- U*_shifted and the host-visible block [U (H*C), optimal cost, status]
-    double *U;
-    const double *opt_cost;
-    double *out;                // host block [HC + 8]: U*, then status words, then the sequence flag
-    double seq;                 // written to out[HC + 6] last, system-scope release (host polls it)
-    // filter()'s state: the update's x0 copied for the optimal rollout that runs after it
-    const double *x0;
-    double *x0_opt;
-    int X;
-    // the next rank launch accumulates into rank[]: zeroed here when it is the tiled kernel
-    int *rank_zero;
-    int64_t rank_n;
-    // the cost statistics, consumed by weights_gradient_kernel ahead of this launch: reset here for
-    // the next update's folds (stream-ordered before its rollout launch; may be null)
-    CostStats *stats_reset;
-    // the update's in-launch wait timeouts: every rank's (the all-reduced cost slot R) when sharded
-    // over RCCL, else null (Status::wait_timeouts); wait_local: this rank's slot, reset here
-    const double *wait_all;
-    double *wait_local;
-};
+
 
 
 // stable rank of rollouts 2..S+1 by cost; `sorted` is scratch of rank_scratch(S) keys
@@ -275,20 +300,7 @@ hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
 constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
 static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser partials");
-// optimise() and the partial gradient in one launch (kernels.hip weights_gradient_kernel)
-struct WGradArgs {
-    const double *cost;    // [R], global rollout index
-    int64_t R;
-    double cost_scale;
-    Status *status;
-    const double *noise;   // [H][Rpad][C]
-    int64_t begin, count, Rpad;
-    int H, C;
-    double *gsplit;        // [GRAD_SPLIT][H][C]
-    double *wexp;          // [R] unnormalised weights e_r (weights = e_r / Status::total)
-    double *wpart;         // [4 * 64] scratch: per-chunk min / max / count / sum (R > SM_LARGE_R)
-    const CostStats *stats;   // min / max / count from the cost kernel (unsharded), or null: a pass
-};
+
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
