@@ -193,6 +193,9 @@ struct mppi_handle {
     unsigned *d_pm_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
     double *d_pm_part = nullptr;     // [nblocks][H C] partial gradients, then [nblocks] normalisers
     unsigned pm_epoch = 0, pm_nblocks = 0;
+    uint64_t *d_pm_stamps = nullptr;   // MPPI_PM_STAMPS=1: the launch's phase stamps per block
+    std::vector<double> pm_stamp_sum; // their per-phase sums (us after the block's entry), printed at destroy
+    int64_t pm_stamp_n = 0;
     // optimise() and finish() in the rollout launch's epilogue (fr_coop.hip epilogue)
     unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
     unsigned ep_total = 0;           // their value after the last epilogue launch
@@ -1030,6 +1033,11 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
             h->pm_nblocks = (unsigned)((h->R + PM_FUSED_ROWS - 1) / PM_FUSED_ROWS);
             CREATE_TRY(dalloc(h, &h->d_pm_sync, 2));
             CREATE_TRY(dalloc(h, &h->d_pm_part, (size_t)h->pm_nblocks * (HC + 1)));
+            const char *ps = std::getenv("MPPI_PM_STAMPS");
+            if (ps && ps[0] == '1') {
+                CREATE_TRY(dalloc(h, &h->d_pm_stamps, (size_t)h->pm_nblocks * PM_STAMPS));
+                h->pm_stamp_sum.assign(PM_STAMPS, 0.0);
+            }
         }
     }
     if (h->sg_window > 0) {
@@ -1068,6 +1076,13 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 void mppi_destroy(mppi_handle *h)
 {
     if (!h) return;
+    if (h->pm_stamp_n > 0) {
+        std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
+                     (long long)h->pm_stamp_n);
+        static const char *names[PM_STAMPS] = {"entry", "sampled", "rolled", "barrier", "partials", "published", "ranked", "end"};
+        for (int i = 0; i < PM_STAMPS; i++) std::fprintf(stderr, " %s %.2f", names[i], h->pm_stamp_sum[(size_t)i] / (double)h->pm_stamp_n);
+        std::fprintf(stderr, "\n");
+    }
     if (h->host_trace && h->ht_n[2] > 0)
         std::fprintf(stderr, "mppi host turnaround (us): flag->return %.2f  return->phase1 %.2f  phase1->launched %.2f  (n=%lld)\n",
                      h->ht_sum[0] / (double)std::max<int64_t>(1, h->ht_n[0]), h->ht_sum[1] / (double)std::max<int64_t>(1, h->ht_n[1]),
@@ -2131,6 +2146,7 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     a.seq = (double)(++h->publish_seq);
     a.opt_cost = h->d_opt;
     a.x0_opt = h->d_x0_opt;
+    a.stamps = h->d_pm_stamps;
     // a filter() of the five-launch path still running on the side stream reads d_U / d_x0_opt
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
@@ -2160,7 +2176,27 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     h->info[MPPI_INFO_FUSED_UPDATE] = 1;
     h->updated_once = true;
     h->phase_open = true;
-    return phase3_wait(h, a.seq);
+    mppi_status st = phase3_wait(h, a.seq);
+    if (h->d_pm_stamps && st == MPPI_OK) {   // diagnostics: each phase's end after the block's entry
+        std::vector<uint64_t> sv((size_t)h->pm_nblocks * PM_STAMPS);
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipMemcpy(sv.data(), h->d_pm_stamps, sv.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        uint64_t t0 = ~0ull;
+        for (unsigned b = 0; b < h->pm_nblocks; b++) t0 = std::min(t0, sv[(size_t)b * PM_STAMPS]);
+        for (int i = 0; i < PM_STAMPS; i++) {
+            uint64_t mx = 0;   // the phase's last block (s_memrealtime: 100 MHz)
+            for (unsigned b = 0; b < h->pm_nblocks; b++) mx = std::max(mx, sv[(size_t)b * PM_STAMPS + i]);
+            if (i == 5) {   // the publish: only the finishing block stamps it
+                mx = 0;
+                for (unsigned b = 0; b < h->pm_nblocks; b++)
+                    if (sv[(size_t)b * PM_STAMPS + 5] > t0) mx = std::max(mx, sv[(size_t)b * PM_STAMPS + 5]);
+            }
+            h->pm_stamp_sum[(size_t)i] += (double)(mx - t0) * 0.01;
+        }
+        h->pm_stamp_n++;
+        HIP_TRY(hipMemset(h->d_pm_stamps, 0, sv.size() * sizeof(uint64_t)));
+    }
+    return st;
 }
 
 mppi_status mppi_update(mppi_handle *h, const double *state, double time)

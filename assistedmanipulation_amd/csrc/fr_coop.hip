@@ -2445,15 +2445,22 @@ __device__ __forceinline__ int ep_ldi(const int *p) { return __hip_atomic_load(p
 __device__ __forceinline__ void ep_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // eps of rollout rr (local) at step k as the rollout launch used it: a kept row's columns were
-// copied in this launch (write-through), the rest are the draws made ahead by earlier launches
+// copied in this launch (write-through: loaded sc1, after the barrier), the rest are the draws
+// made ahead by earlier launches (plain loads, issued before the barrier)
+__device__ __forceinline__ bool ep_kept(const FrRolloutArgs &fa, int k, int64_t rr)
+{
+    const SampleArgs &sa = fa.samp;
+    const int64_t g = fa.wg.begin + rr;
+    return g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
+}
+__device__ __forceinline__ const double *ep_eps_ptr(const FrRolloutArgs &fa, int k, int64_t rr)
+{
+    return fa.wg.noise + ((int64_t)k * fa.wg.Rpad + rr) * FR_C;
+}
 __device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, int k, int64_t rr, double *e)
 {
-    const WGradArgs &a = fa.wg;
-    const double *n = a.noise + ((int64_t)k * a.Rpad + rr) * FR_C;
-    const SampleArgs &sa = fa.samp;
-    const int64_t g = a.begin + rr;
-    const bool kept = g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
-    if (kept) {
+    const double *n = ep_eps_ptr(fa, k, rr);
+    if (ep_kept(fa, k, rr)) {
 #pragma unroll
         for (int c = 0; c < FR_C; c++) e[c] = ep_ld(n + c);
     } else {
@@ -2461,26 +2468,61 @@ __device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, int k, int64_t r
         for (int c = 0; c < FR_C; c++) e[c] = n[c];
     }
 }
+// A unit's eps, loaded ahead of the barrier where it can be (rows not kept)
+struct EpPre {
+    double ne[EP_GR][FR_C];
+    bool kept[EP_GR];
+};
+__device__ __forceinline__ void ep_unit_range(const FrRolloutArgs &fa, int u, int64_t &r0, int64_t &r1, int &k, int &s)
+{
+    const WGradArgs &a = fa.wg;
+    const bool has = u >= 0;
+    k = has ? u % a.H : 0;
+    s = has ? u / a.H : 0;
+    const int64_t chunk = (a.count + GRAD_SPLIT - 1) / GRAD_SPLIT;
+    r0 = (int64_t)s * chunk;
+    r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
+}
+__device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, int u, int t, EpPre &p)
+{
+    int64_t r0, r1;
+    int k, s;
+    ep_unit_range(fa, u, r0, r1, k, s);
+#pragma unroll
+    for (int m = 0; m < EP_GR; m++) {
+        const int64_t r = r0 + t + 256 * m;
+        const int64_t rr = (u >= 0 && r < r1) ? r : 0;
+        p.kept[m] = ep_kept(fa, k, rr);
+        const double *n = ep_eps_ptr(fa, k, rr);
+        if (!p.kept[m])
+#pragma unroll
+            for (int c = 0; c < FR_C; c++) p.ne[m][c] = n[c];
+    }
+}
 
 // weights_gradient_kernel<FR_C, false> (kernels.hip) block (k, s) = unit u (k = u mod H, s = u / H)
 // on 256 threads t, unsharded with the objective's statistics; u < 0: no unit (the barrier only)
-__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, double *red, double *ssum)
+__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, double *red, double *ssum, EpPre &p)
 {
     const WGradArgs &a = fa.wg;
     constexpr int CP = FR_C;
     const int rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
     const bool has = u >= 0;
-    const int k = has ? u % a.H : 0, s = has ? u / a.H : 0, ns = GRAD_SPLIT;
-    const int64_t chunk = (a.count + ns - 1) / ns;
-    const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
-    double ne[EP_GR][CP];
+    int64_t r0, r1;
+    int k, s;
+    ep_unit_range(fa, u, r0, r1, k, s);
+    double (&ne)[EP_GR][CP] = p.ne;
     double cpre[EP_GR];
 #pragma unroll
-    for (int m = 0; m < EP_GR; m++) {
+    for (int m = 0; m < EP_GR; m++) {   // the kept rows' eps (sc1) and the costs, after the barrier
         const int64_t r = r0 + t + 256 * m;
         const int64_t rr = (has && r < r1) ? r : 0;
-        ep_eps(fa, k, rr, ne[m]);
+        if (p.kept[m]) {
+            const double *n = ep_eps_ptr(fa, k, rr);
+#pragma unroll
+            for (int c = 0; c < CP; c++) ne[m][c] = ep_ld(n + c);
+        }
         cpre[m] = ep_ld(a.cost + a.begin + rr);
     }
     const bool own_slice = has && k == 0 && a.begin == 0 && a.count == R;
@@ -2647,6 +2689,13 @@ template <int NT>
 __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, int *Lint)
 {
     const int t = threadIdx.x;
+    const int groups = gridDim.x, half = t >> 8, ht = t & 255;
+    const int nunits = a.wg.H * GRAD_SPLIT, per = 2 * groups;
+    EpPre pre;   // the first pass's eps, loaded while the barrier waits
+    {
+        const int u = half * groups + (int)blockIdx.x;
+        ep_preload(a, u < nunits ? u : -1, ht, pre);
+    }
     __builtin_amdgcn_s_waitcnt(0);   // this wave's cost stores, atomics and eps copies have left it
     __syncthreads();
     if (t == 0) {   // every workgroup's costs and statistics are final
@@ -2659,11 +2708,10 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
         if (i == EP_BAR_SPINS) note_wait_timeout(a);   // the update then fails
     }
     __syncthreads();
-    const int groups = gridDim.x, half = t >> 8, ht = t & 255;
-    const int nunits = a.wg.H * GRAD_SPLIT, per = 2 * groups;
     for (int base = 0; base < nunits; base += per) {
         const int u = base + half * groups + (int)blockIdx.x;
-        ep_unit(a, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8);
+        if (base > 0) ep_preload(a, u < nunits ? u : -1, ht, pre);
+        ep_unit(a, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8, pre);
         __syncthreads();   // the halves' LDS is reused by the next pass
     }
     __builtin_amdgcn_s_waitcnt(0);   // every wave's unit stores have left it

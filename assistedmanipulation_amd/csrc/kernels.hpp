@@ -401,7 +401,9 @@ struct PmFusedArgs {
     double seq;                 // its sequence flag value
     double *opt_cost;           // filter()'s cost of the published U*
     double *x0_opt;
+    uint64_t *stamps;           // diagnostics (MPPI_PM_STAMPS=1): [nblocks][PM_STAMPS] s_memrealtime, or null
 };
+constexpr int PM_STAMPS = 8;   // entry, sampled, rolled out, barrier passed, partials stored, published, ranked, end
 bool pm_fused_fits(int64_t R, int H);
 size_t pm_fused_lds_bytes(int64_t R, int H);
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);

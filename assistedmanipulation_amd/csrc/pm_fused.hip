@@ -80,6 +80,7 @@ __device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double 
 #pragma unroll
     for (int i = 0; i < 6; i++) x[i] = a.x0v[i];
     double J = 0.0;
+#pragma unroll 4
     for (int k = 0; k < a.H; k++) {
         double u[3];
 #pragma unroll
@@ -126,6 +127,10 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     const SampleParams &P = a.sp;
     const double *Uprev = a.U;   // U* as the previous update published it
     const unsigned target = a.epoch * (unsigned)nb;
+    auto stamp = [&](int i) {   // diagnostics: one clock stamp per block and phase
+        if (a.stamps && t == 0) a.stamps[b * PM_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
     // ---- phase A: sample (mppi.cpp:189-270) ----
     for (int i = t; i < HC; i += PT) {   // U*_shifted (mppi.cpp:197-207); unshifted, as last left
@@ -134,38 +139,78 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     }
     for (int k = t; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
     if (t == 0) s_last = 0;
-    for (int i = t; i < PR * H; i += PT) {   // item (step k, rollout): consecutive threads, consecutive rollouts
-        const int k = i / PR, rl = i - k * PR;
-        const int64_t g = r0 + rl;   // unsharded: local = global
-        if (g >= a.R) continue;
-        double e[PC];
-        const int64_t rank = g >= 2 ? a.rank[g] : 0;
-        if (g == 0) {
+    // the block's ranks once (LDS; Lcnt's room, used again only by the tail's rank)
+    int *Lrank = Lcnt;
+    if (t < PR) {
+        const int64_t g = r0 + t;
+        Lrank[t] = (g >= 2 && g < a.R) ? a.rank[g] : 0x7FFFFFFF;
+    }
+    __syncthreads();
+    // items (step k, rollout): consecutive threads, consecutive rollouts; IB items per thread per pass
+    // with their loads issued together (one memory trip per pass, not one per item)
+    constexpr int IB = 4;
+    for (int base = t; base < PR * H; base += PT * IB) {
+        const double *src[IB];
+        double sgn[IB], e[IB][PC];
+        bool draw[IB], store[IB], live[IB];
+        int kk[IB], rr[IB];
 #pragma unroll
-            for (int c = 0; c < PC; c++) e[c] = 0.0;
-        } else if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
-#pragma unroll
-            for (int c = 0; c < PC; c++) e[c] = -Uprev[k * PC + c];
-        } else if (rank < P.keep && (P.shift_by <= 0 || k < P.shifted)) {   // kept: the previous eps, shifted
-            const double *s = a.prev + (((int64_t)k + (P.shift_by > 0 ? P.shift_by : 0)) * a.Rpad + g) * PC;
-#pragma unroll
-            for (int c = 0; c < PC; c++) e[c] = s[c];
-        } else if (a.ahead) {   // the previous launch's tail drew it into this update's buffer
-            const double *s = a.noise + ((int64_t)k * a.Rpad + g) * PC;
-#pragma unroll
-            for (int c = 0; c < PC; c++) e[c] = s[c];
-        } else {
-            philox_eps(a, g, k, P.update_index, e);
+        for (int u = 0; u < IB; u++) {
+            const int i = base + u * PT;
+            const int k = i / PR, rl = i - k * PR;
+            const int64_t g = r0 + rl;   // unsharded: local = global
+            kk[u] = k;
+            rr[u] = rl;
+            live[u] = i < PR * H && g < a.R;
+            src[u] = Uprev;   // any valid address
+            sgn[u] = 1.0;
+            draw[u] = false;
+            store[u] = true;
+            if (!live[u]) continue;
+            const int rank = Lrank[rl];
+            if (g == 0) {
+                sgn[u] = 0.0;
+            } else if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
+                src[u] = Uprev + k * PC;
+                sgn[u] = -1.0;
+            } else if (rank < P.keep && (P.shift_by <= 0 || k < P.shifted)) {   // kept: the previous eps, shifted
+                src[u] = a.prev + (((int64_t)k + (P.shift_by > 0 ? P.shift_by : 0)) * a.Rpad + g) * PC;
+            } else if (a.ahead) {   // the previous launch's tail drew it into this update's buffer: in place
+                src[u] = a.noise + ((int64_t)k * a.Rpad + g) * PC;
+                store[u] = false;
+            } else {
+                draw[u] = true;
+            }
         }
-        double *o = a.noise + ((int64_t)k * a.Rpad + g) * PC;
 #pragma unroll
-        for (int c = 0; c < PC; c++) {
-            Leps[rl * ES + k * PC + c] = e[c];
-            o[c] = e[c];
+        for (int u = 0; u < IB; u++)
+#pragma unroll
+            for (int c = 0; c < PC; c++) e[u][c] = src[u][c];
+#pragma unroll
+        for (int u = 0; u < IB; u++) {
+            const int i = base + u * PT;
+            if (i >= PR * H) break;
+            const int k = kk[u], rl = rr[u];
+            if (!live[u]) {   // rows past R: zeros, which the gradient's fixed 64-row sum multiplies by 0
+#pragma unroll
+                for (int c = 0; c < PC; c++) Leps[rl * ES + k * PC + c] = 0.0;
+                continue;
+            }
+            if (draw[u]) philox_eps(a, r0 + rl, k, P.update_index, e[u]);
+            else if (sgn[u] != 1.0)
+#pragma unroll
+                for (int c = 0; c < PC; c++) e[u][c] = sgn[u] == 0.0 ? 0.0 : sgn[u] * e[u][c];   // rollout 0: +0
+            double *o = a.noise + ((int64_t)k * a.Rpad + r0 + rl) * PC;
+#pragma unroll
+            for (int c = 0; c < PC; c++) {
+                Leps[rl * ES + k * PC + c] = e[u][c];
+                if (store[u]) o[c] = e[u][c];
+            }
         }
     }
     if (b == 0 && t < a.X) a.x0_out[t] = a.x0v[t];
     __syncthreads();
+    stamp(1);
     if (w == 0) {   // rollouts (mppi.cpp:272-342): one lane per rollout
         const int64_t g = r0 + l;
         double J = NAN;
@@ -189,6 +234,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         __builtin_amdgcn_s_waitcnt(0);   // the cost stores and the atomics have left this wave
     }
     __syncthreads();
+    stamp(2);
     // ---- grid barrier: every block's costs and statistics are final (bounded) ----
     if (t == 0) {
         __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -200,6 +246,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         if (i == BAR_SPINS) atomicAdd(&a.status->wait_timeouts, 1);   // the update then fails
     }
     __syncthreads();
+    stamp(3);
     // ---- phase B: optimise (mppi.cpp:344-418) ----
     static_assert(CS_SLOTS == 64, "one slot per lane");
     const unsigned long long kn = mppi_dev::wave_umin64_dpp(
@@ -232,6 +279,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     }
     __builtin_amdgcn_s_waitcnt(0);   // every wave's partial stores have left it
     __syncthreads();
+    stamp(4);
     if (t == 0) {   // the last block to arrive finishes the update
         const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old + 1 == target;
@@ -288,6 +336,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             st->wait_timeouts = 0;
             __threadfence_system();
             __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            stamp(5);
             // filter() (mppi.cpp:450-479): the cost of the published U* from this update's state,
             // while the host takes the result; none when the update threw
             if (ok) *a.opt_cost = pm_rollout(a, Lus, Lgm, nullptr, true);
@@ -306,7 +355,8 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         if (i >= 0 && i < S) {
             const uint64_t ki = Lkey[i];
             const int64_t j0 = (S * qd) / 4, j1 = (S * (qd + 1)) / 4;
-            for (int64_t j = j0; j < j1; j++) {
+#pragma unroll 8
+            for (int64_t j = j0; j < j1; j++) {   // unrolled: the LDS reads of eight keys in flight
                 const uint64_t kj = Lkey[j];
                 cnt += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
             }
@@ -315,6 +365,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         __syncthreads();
         if (qd == 0 && i >= 0 && i < S) a.rank[i + 2] = cnt + Lcnt[rl] + Lcnt[PR + rl] + Lcnt[2 * PR + rl];
     }
+    stamp(6);
     // the next update's draws (Philox by (rollout, step), its update index) into the buffer it will
     // sample from: rollouts >= 2 (rollout 0 is zero and rollout 1 -U* at sampling time)
     if (a.ahead_noise) {
@@ -329,6 +380,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             for (int c = 0; c < PC; c++) o[c] = e[c];
         }
     }
+    stamp(7);
 }
 
 namespace mppi_eng {
@@ -341,7 +393,7 @@ size_t pm_fused_lds_bytes(int64_t R, int H)
 
 bool pm_fused_fits(int64_t R, int H)
 {
-    return R >= 4 && H >= 1 && R <= PM_FUSED_MAX_R && (int64_t)H * PC <= 4 * PT && pm_fused_lds_bytes(R, H) <= 96 * 1024;
+    return R >= 4 && H >= 1 && R <= PM_FUSED_MAX_R && (int64_t)H * PC <= 4 * PT && pm_fused_lds_bytes(R, H) <= 150 * 1024;
 }
 
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s)

@@ -338,12 +338,21 @@ def run(args, world, rank, local_rank, dist):
     units = count_local * traj.H            # rollout-steps of this rank's rollout launch
     units_all = traj.R * traj.H             # of the whole update
     if pm:
-        # pm_rollout_kernel: one lane per rollout, reads its 24-B eps column per step (fp64)
-        kernel = "pm_rollout_kernel"
-        rollout_bytes = 24.0 * units
-        roofline = {"bound": "hbm", "kernel": kernel, "achieved": rollout_bytes / (dyn_ms * 1e-3) / 1e9,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "bytes_per_launch": rollout_bytes, "bytes_per_rollout_step": 24.0}
+        # the point mass is latency-bound, not HBM-bound: 0.8 MB of eps per update against a chain of
+        # H dependent steps per rollout, one grid barrier and the publish (pm_update_kernel: the whole
+        # update in one launch), or five dependent launches (MPPI_PM_FUSED=0).  The HBM view (the eps
+        # written once and read once, fp64) is reported beside the latency, as the fraction of 8 TB/s
+        # the launch's bytes reach.
+        fused = bool(info.get("fused_update"))
+        kernel = "pm_update_kernel (sample + rollouts + optimise + finish + filter + next rank/draws)" if fused \
+            else "pm_rollout_kernel"
+        rollout_bytes = 2 * 24.0 * units if fused else 24.0 * units
+        roofline = {"bound": "latency", "kernel": kernel,
+                    "critical_chain": "%d dependent rollout steps + a grid barrier + the publish, %s" % (
+                        traj.H, "one launch per update" if fused else "five dependent launches per update"),
+                    "achieved": rollout_bytes / (dyn_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "bytes_per_launch": rollout_bytes, "bytes_per_rollout_step": rollout_bytes / units,
+                    "launch_us": dyn_ms * 1e3}
         roofline["frac"] = roofline["achieved"] / roofline["peak"]
         roofline["traffic"] = None
         survey_bytes = BYTES_SURVEY_PM
@@ -362,7 +371,8 @@ def run(args, world, rank, local_rank, dist):
         launch_bytes = ((BYTES_EPS_FR + BYTES_REC * (2 if in_launch else 1)) * rows_units
                         + (BYTES_EPS_FR * units if info["tail_draws"] else 0.0)) if not lane else BYTES_EPS_FR * units
         roofline = {"bound": "valu", "kernel": "fr_rollout_kernel" if lane else (
-                        "fr_coop_x_kernel (dynamics + objective)" if in_launch else "fr_coop_kernel"),
+                        ("fr_coop_x_kernel (dynamics + objective + optimise/finish epilogue)" if info.get("fused_update")
+                         else "fr_coop_x_kernel (dynamics + objective)") if in_launch else "fr_coop_kernel"),
                     "compute": "fp64 VALU, issue-bound at one wave per SIMD (no dense contraction for MFMA)",
                     "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,

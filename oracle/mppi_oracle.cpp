@@ -1532,6 +1532,10 @@ void oracle_dims(void *h, int64_t *R, int64_t *H, int64_t *C, int64_t *X)
     *R = t->R; *H = t->H; *C = t->C; *X = t->X;
 }
 void oracle_costs(void *h, double *out) { Trajectory *t = (Trajectory *)h; std::copy(t->cost.begin(), t->cost.end(), out); }
+// Test hook: the previous update's rollout costs, which the next sample() sorts (mppi.cpp:222-231).
+// Used after an engine failure that has no reference counterpart (an in-launch wait timing out),
+// so that the oracle's next update starts from the engine's state.
+void oracle_set_costs(void *h, const double *in) { Trajectory *t = (Trajectory *)h; std::copy(in, in + t->R, t->cost.begin()); }
 void oracle_weights(void *h, double *out) { Trajectory *t = (Trajectory *)h; std::copy(t->weights.begin(), t->weights.end(), out); }
 void oracle_gradient(void *h, double *out) { Trajectory *t = (Trajectory *)h; std::copy(t->gradient.begin(), t->gradient.end(), out); }
 void oracle_optimal_control(void *h, double *out) { Trajectory *t = (Trajectory *)h; std::copy(t->U.begin(), t->U.end(), out); }

@@ -53,7 +53,7 @@ def lib(path=None):
     L.oracle_get.argtypes = [vp, C.c_double, dp]
     L.oracle_dims.argtypes = [vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]
     for n in ("oracle_costs", "oracle_weights", "oracle_gradient", "oracle_optimal_control",
-              "oracle_noise", "oracle_optimal_terms"):
+              "oracle_noise", "oracle_optimal_terms", "oracle_set_costs"):
         getattr(L, n).argtypes = [vp, dp]
     L.oracle_optimal_cost.restype = C.c_double
     L.oracle_optimal_cost.argtypes = [vp]
@@ -226,6 +226,12 @@ class OracleTrajectory:
 
     def costs(self):
         return self._vec("oracle_costs", self.R)
+
+    def set_costs(self, costs):
+        """Test hook: the previous costs the next sample() sorts (oracle_set_costs)."""
+        c = np.ascontiguousarray(costs, dtype=np.float64)
+        assert c.size == self.R
+        self._L.oracle_set_costs(self._h, _p(c))
 
     def weights(self):
         return self._vec("oracle_weights", self.R)

@@ -653,10 +653,11 @@ def test_in_launch_wait_timeout_fails_the_update():
     with MPPI_ERR_DEVICE and publishes nothing, as the reference refuses to go on when optimise()
     throws (mppi.cpp:369-370).  The oracle cannot lose rows, so its side of the failed update is an
     all-NaN failure at the same time with the same noise: both leave U* unpublished, no filter(),
-    and the same shift.  keep_best 0 makes the next update independent of the failed update's
-    costs (which differ: the device's are real where the oracle's are NaN), so the updates after
-    the failure must match the oracle again."""
-    conf, dev, orc, sd = fr_pair(S=4096, horison=0.64, K=0, threads=16)
+    and the same shift.  The next sample() sorts the failed update's costs (the keep-best set and
+    the injected stream's order, mppi.cpp:222-262), which differ - the device's are real where the
+    oracle's are NaN - so the oracle takes the device's (oracle_set_costs); the updates after the
+    failure must then match the oracle again."""
+    conf, dev, orc, sd = fr_pair(S=4096, horison=0.64, K=20, threads=16)
     rng = np.random.default_rng(31)
     x = am.huddled_state()
     step_both(dev, orc, x, 0.0, rng, sd)
@@ -676,6 +677,7 @@ def test_in_launch_wait_timeout_fails_the_update():
     info = dev.update_info()
     assert info["wait_timeouts"] > 0 and info["wait_timeouts_total"] == info["wait_timeouts"], info
     np.testing.assert_array_equal(dev.get_optimal_rollout(), u_before)   # nothing published
+    orc.set_costs(dev.costs())
     for j in (2, 3, 4):
         step_both(dev, orc, x, 0.05 * j, rng, sd)
         assert dev.update_info()["wait_timeouts"] == 0

@@ -46,8 +46,13 @@ def test_fused_update_equals_five_launches(S, horison, monkeypatch):
             x = x + 0.01
         out[fused] = rec
     for j, (a, b) in enumerate(zip(out["1"], out["0"])):
-        np.testing.assert_array_equal(a[0], b[0], err_msg="update %d noise" % j)
-        np.testing.assert_array_equal(a[1], b[1], err_msg="update %d costs" % j)
+        np.testing.assert_array_equal(a[0][0], b[0][0], err_msg="update %d noise" % j)
+        np.testing.assert_array_equal(a[0][2:], b[0][2:], err_msg="update %d noise" % j)
+        # rollout 1 = -U*, which the two paths round differently (the gradient's summation order)
+        np.testing.assert_allclose(a[0][1], b[0][1], rtol=0, atol=1e-12, err_msg="update %d noise" % j)
+        np.testing.assert_array_equal(a[1][0], b[1][0], err_msg="update %d costs" % j)
+        np.testing.assert_array_equal(a[1][2:], b[1][2:], err_msg="update %d costs" % j)
+        np.testing.assert_allclose(a[1][1], b[1][1], rtol=1e-12, err_msg="update %d costs" % j)
         np.testing.assert_allclose(a[2], b[2], rtol=1e-13, atol=1e-16, err_msg="update %d weights" % j)
         np.testing.assert_allclose(a[3], b[3], rtol=0, atol=1e-12, err_msg="update %d gradient" % j)
         np.testing.assert_allclose(a[4], b[4], rtol=0, atol=1e-12, err_msg="update %d U*" % j)
