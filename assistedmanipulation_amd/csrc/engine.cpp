@@ -200,6 +200,10 @@ struct mppi_handle {
     unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
     unsigned ep_total = 0;           // their value after the last epilogue launch
     bool ep_ran = false;             // this update's rollout launch ran the epilogue
+    uint64_t *d_ep_stamps = nullptr; // MPPI_EP_STAMPS=1: the epilogue's phase stamps per workgroup
+    unsigned ep_stamp_groups = 0;
+    std::vector<double> ep_stamp_sum;   // us: last arrival -> barrier passed (last), -> units stored (last), -> published
+    int64_t ep_stamp_n = 0;
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -1016,6 +1020,12 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
         CREATE_TRY(dalloc(h, &h->d_ep_sync, 2));
+        const char *es = std::getenv("MPPI_EP_STAMPS");
+        if (es && es[0] == '1') {
+            h->ep_stamp_groups = (unsigned)std::max<int64_t>(1, (h->R + 15) / 16);
+            CREATE_TRY(dalloc(h, &h->d_ep_stamps, (size_t)h->ep_stamp_groups * EP_STAMPS));
+            h->ep_stamp_sum.assign(4, 0.0);
+        }
         CREATE_TRY(launch_fr_body_table(h->d_model, h->d_cost, h->d_table, nullptr));
         CREATE_TRY(hipDeviceSynchronize());
     } else {
@@ -1076,6 +1086,10 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 void mppi_destroy(mppi_handle *h)
 {
     if (!h) return;
+    if (h->ep_stamp_n > 0)
+        std::fprintf(stderr, "epilogue phases (us, mean of %lld): arrivals spread %.2f  barrier release %.2f  units %.2f  "
+                             "ticket+finish+publish %.2f\n", (long long)h->ep_stamp_n, h->ep_stamp_sum[0] / h->ep_stamp_n,
+                     h->ep_stamp_sum[1] / h->ep_stamp_n, h->ep_stamp_sum[2] / h->ep_stamp_n, h->ep_stamp_sum[3] / h->ep_stamp_n);
     if (h->pm_stamp_n > 0) {
         std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
                      (long long)h->pm_stamp_n);
@@ -1656,6 +1670,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         if (a.epilogue) {
             a.ep_sync = h->d_ep_sync;
             a.ep_target = h->ep_total;
+            a.ep_stamps = h->d_ep_stamps;
             a.wg = wgrad_args(h);
             a.fin = finish_args(h);   // its sequence: publish_seq + 1, as phase 3 publishes it
             a.fin.rank_n = h->R;      // draw_ahead_possible: S <= RANK_TILED_MAX, rank_draw_kernel's tiles
@@ -1929,6 +1944,29 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
     h->update_last = h->rollout_time;
     ++h->update_count;
     h->published_once = true;   // a filter() row exists from here on (mppi_optimal_terms)
+    if (h->d_ep_stamps && h->ep_ran) {   // diagnostics: the epilogue's phases (s_memrealtime, 100 MHz)
+        std::vector<uint64_t> sv((size_t)h->ep_stamp_groups * EP_STAMPS);
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipMemcpy(sv.data(), h->d_ep_stamps, sv.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        uint64_t first = ~0ull, last_arr = 0, pass = 0, stored = 0, pub = 0;
+        for (unsigned b = 0; b < h->ep_stamp_groups; b++) {
+            const uint64_t *v = &sv[(size_t)b * EP_STAMPS];
+            if (!v[0]) continue;
+            first = std::min(first, v[0]);
+            last_arr = std::max(last_arr, v[0]);
+            pass = std::max(pass, v[1]);
+            stored = std::max(stored, v[2]);
+            pub = std::max(pub, v[3]);
+        }
+        if (last_arr) {
+            h->ep_stamp_sum[0] += (double)(last_arr - first) * 0.01;   // spread of the arrivals
+            h->ep_stamp_sum[1] += (double)(pass - last_arr) * 0.01;    // barrier release
+            h->ep_stamp_sum[2] += (double)(stored - pass) * 0.01;      // units (the weight reduce)
+            h->ep_stamp_sum[3] += (double)(pub - stored) * 0.01;       // ticket + finish + publish
+            h->ep_stamp_n++;
+        }
+        HIP_TRY(hipMemset(h->d_ep_stamps, 0, sv.size() * sizeof(uint64_t)));
+    }
     if (h->host_trace) {
         h->ht_ret = std::chrono::steady_clock::now();
         h->ht_sum[0] += std::chrono::duration<double, std::micro>(h->ht_ret - h->ht_flag).count();

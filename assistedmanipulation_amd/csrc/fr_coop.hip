@@ -2696,8 +2696,12 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
         const int u = half * groups + (int)blockIdx.x;
         ep_preload(a, u < nunits ? u : -1, ht, pre);
     }
+    auto stamp = [&](int i) {   // diagnostics: one clock stamp per workgroup and phase
+        if (a.ep_stamps && t == 0) a.ep_stamps[blockIdx.x * EP_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
+    };
     __builtin_amdgcn_s_waitcnt(0);   // this wave's cost stores, atomics and eps copies have left it
     __syncthreads();
+    stamp(0);
     if (t == 0) {   // every workgroup's costs and statistics are final
         __hip_atomic_fetch_add(a.ep_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int i = 0;
@@ -2708,6 +2712,7 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
         if (i == EP_BAR_SPINS) note_wait_timeout(a);   // the update then fails
     }
     __syncthreads();
+    stamp(1);
     for (int base = 0; base < nunits; base += per) {
         const int u = base + half * groups + (int)blockIdx.x;
         if (base > 0) ep_preload(a, u < nunits ? u : -1, ht, pre);
@@ -2716,9 +2721,13 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
     }
     __builtin_amdgcn_s_waitcnt(0);   // every wave's unit stores have left it
     __syncthreads();
+    stamp(2);
     if (t == 0) Lint[0] = __hip_atomic_fetch_add(a.ep_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == a.ep_target;
     __syncthreads();
-    if (Lint[0]) ep_finish<NT>(a, t);
+    if (Lint[0]) {
+        ep_finish<NT>(a, t);
+        stamp(3);
+    }
 }
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and four more

@@ -117,6 +117,7 @@ struct FinishArgs {
     double *wait_local;
 };
 
+constexpr int EP_STAMPS = 4;   // epilogue stamps: barrier arrival, barrier passed, units stored, published (finisher)
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;
@@ -175,6 +176,7 @@ struct FrRolloutArgs {
     int epilogue;
     unsigned *ep_sync;            // [2] barrier and ticket counters (monotonic)
     unsigned ep_target;           // their value once every workgroup of this launch has added 1
+    uint64_t *ep_stamps;          // diagnostics (MPPI_EP_STAMPS=1): [groups][EP_STAMPS] s_memrealtime, or null
     WGradArgs wg;
     FinishArgs fin;
 };
