@@ -1040,7 +1040,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(hipMemcpy(h->d_pm, &p, sizeof(p), hipMemcpyHostToDevice));
         h->pm_host = p;
         if (h->C == 3 && h->X == 6 && pm_fused_fits(h->R, (int)h->H)) {   // the one-launch update's scratch
-            h->pm_nblocks = (unsigned)((h->R + PM_FUSED_ROWS - 1) / PM_FUSED_ROWS);
+            const int rows = pm_fused_rows(h->R, (int)h->H);
+            h->pm_nblocks = (unsigned)((h->R + rows - 1) / rows);
             CREATE_TRY(dalloc(h, &h->d_pm_sync, 2));
             CREATE_TRY(dalloc(h, &h->d_pm_part, (size_t)h->pm_nblocks * (HC + 1)));
             const char *ps = std::getenv("MPPI_PM_STAMPS");
@@ -1465,7 +1466,9 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
     // cooperative FrankaRidgeback: phase 3 left filter() pending (it rides in the next rollout
     // launch) and recorded no event behind the finish kernel, to keep one off the update path; the
     // row reads the d_U / d_x0_opt that kernel wrote, so order the side stream behind it now
-    if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h)) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
+    // (the fused point-mass launch leaves it pending the same way; elsewhere phase 3 recorded the
+    // event just before, and recording it again marks the same point of the stream)
+    HIP_TRY(hipEventRecord(h->ev_pub, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream_opt, h->ev_pub, 0));
     HIP_TRY(hipEventRecord(h->ev[4], h->stream_opt));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
@@ -1517,11 +1520,13 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
 
 // optimise() and finish() in the rollout launch's epilogue: unsharded, no smoothing, the eager path
 // (the hipGraph path keeps its captured four-kernel chain), timing below level 2 (whose events
-// separate the kernels); MPPI_EPILOGUE=0 keeps the three launches (A/B)
+// separate the kernels).  Opt-in (MPPI_EPILOGUE=1): on MI355X the in-launch weight reduce and
+// finish cost the launch ~15.6 us against ~14.6 us for the two launches they replace (r04 A/B,
+// DESIGN.md §5), so the default keeps the three launches
 static bool epilogue_wanted(const mppi_handle *h)
 {
     const char *e = std::getenv("MPPI_EPILOGUE");
-    if (e && e[0] == '0') return false;
+    if (!e || e[0] != '1') return false;
     return h->d_ep_sync && !sharded(h) && h->sg_window == 0 && h->timing < 2 && !h->graph_mode && !h->graph_dry &&
            draw_ahead_possible(h) && !h->d_trace;
 }
@@ -2185,6 +2190,10 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     a.opt_cost = h->d_opt;
     a.x0_opt = h->d_x0_opt;
     a.stamps = h->d_pm_stamps;
+    // the previous update's pending filter() rides in this launch (block 0's second wave, beside
+    // its rollouts); this update's stays pending for the next launch, or for a read (wait_optimal)
+    a.fold_filter = h->opt_state == mppi_handle::OPT_PENDING ? 1 : 0;
+    a.fx0 = h->d_x0_opt;
     // a filter() of the five-launch path still running on the side stream reads d_U / d_x0_opt
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
@@ -2198,14 +2207,14 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     }
     HIP_TRY(launch_pm_update(a, h->stream));
     if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
-    // filter() of this update runs in the same launch, after the publish (OPT_FOLDED: read behind
-    // the stream); the next update's draws are in d_noise_prev
+    // filter() of this update is left pending (as phase 3 leaves the cooperative launch's); the next
+    // update's draws are in d_noise_prev
     h->opt_steps = h->d_steps;
-    h->opt_state = mppi_handle::OPT_FOLDED;
+    h->opt_state = mppi_handle::OPT_PENDING;
     h->ahead = {h->update_count + 1, h->seed, h->begin, h->count, h->H, h->C};
     h->ahead_valid = true;
     h->info[MPPI_INFO_COOPERATIVE] = 0;
-    h->info[MPPI_INFO_FOLDED_FILTER] = 1;
+    h->info[MPPI_INFO_FOLDED_FILTER] = a.fold_filter;
     h->info[MPPI_INFO_OBJECTIVE_IN_LAUNCH] = 1;
     h->info[MPPI_INFO_TAIL_DRAWS] = 1;
     h->info[MPPI_INFO_SAMPLING] = a.ahead ? 2 : 1;

@@ -369,8 +369,12 @@ hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s);
 // filter() and the next update's rank and draws, with one grid barrier.  Device Philox noise with a
 // diagonal transform, unsharded, no smoothing.
 constexpr int PM_FUSED_THREADS = 256;
-constexpr int PM_FUSED_ROWS = 64;                 // rollouts per block
-constexpr int64_t PM_FUSED_MAX_R = 64 * PM_FUSED_ROWS;
+constexpr int64_t PM_FUSED_MAX_R = 4096;
+constexpr int PM_FUSED_MAX_BLOCKS = 256;          // one per CU: the grid barrier needs them co-resident
+// rollouts per block: the fewest of 16, 32, 64 whose grid (at most 256 blocks) and LDS (the
+// finisher stages every block's partials) fit, so that the rank and the draws spread over the most
+// CUs; 0 when none does
+int pm_fused_rows(int64_t R, int H);
 struct PmFusedArgs {
     DevPointMass pm;
     const StepConst *steps;     // [H] gamma_k
@@ -402,7 +406,9 @@ struct PmFusedArgs {
     double *out;                // the mapped host block [H C + 8]
     double seq;                 // its sequence flag value
     double *opt_cost;           // filter()'s cost of the published U*
-    double *x0_opt;
+    double *x0_opt;             // the update's state, for its filter()
+    int fold_filter;            // the previous update's filter() is pending: run it in this launch
+    const double *fx0;          // its state (x0_opt as the previous launch left it)
     uint64_t *stamps;           // diagnostics (MPPI_PM_STAMPS=1): [nblocks][PM_STAMPS] s_memrealtime, or null
 };
 constexpr int PM_STAMPS = 8;   // entry, sampled, rolled out, barrier passed, partials stored, published, ranked, end

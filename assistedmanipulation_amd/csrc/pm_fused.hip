@@ -3,30 +3,36 @@
 // The point-mass update (the a16 bring-up plugin: quadratic cost, ~25 flops per rollout-step) has
 // no arithmetic to speak of; in five launches (sample, rollouts, weights + gradient, finish, rank)
 // its time was the launches' fixed costs and their dependent memory trips.  Here one grid of
-// 256-thread workgroups, each owning 64 rollouts, runs the whole of Trajectory::update
-// (mppi.cpp:154-187) with one grid barrier:
+// 256-thread workgroups, each owning PR rollouts (16 up to 1024 rollouts, 64 above), runs the whole
+// of Trajectory::update (mppi.cpp:154-187) with one grid barrier:
 //
 //   phase A  sample (mppi.cpp:189-270): the block's eps columns into LDS (and the eps tensor):
 //            rollout 0 zero, rollout 1 = -U*, kept rollouts the previous eps shifted, the rest
 //            Philox by (rollout, step) - drawn ahead by the previous launch when it could; U*
-//            shifted; then one wave rolls the 64 rollouts out of LDS (mppi.cpp:272-342) and folds
-//            the costs' min / max / count into the CostStats slots (exact key atomics).
+//            shifted.  Every candidate source (kept, drawn ahead) is loaded in one batch with the
+//            rank, so the phase is one memory trip; then one wave rolls the rollouts out of LDS
+//            (mppi.cpp:272-342) and folds the costs' min / max / count into the CostStats slots
+//            (exact key atomics).
 //   barrier  every block's costs and statistics are final.
 //   phase B  optimise (mppi.cpp:344-418): e_r of the block's rollouts and its partial gradient
-//            sum_r e_r eps_r over its 64 rollouts (fixed order), written through to L2 (sc1) for
-//            the last block to arrive (agent-scope ticket), which adds the partials in block order,
-//            steps U*, clamps and publishes the host block (mppi.cpp:421-447, 178-182), then runs
-//            filter() (mppi.cpp:450-479) on one lane.
+//            sum_r e_r eps_r over its PR rollouts (fixed order), written through to L2 (sc1) for
+//            the last block to arrive (agent-scope ticket), which stages every block's partials in
+//            LDS in one batch of loads, adds them in block order, steps U*, clamps and publishes
+//            the host block (mppi.cpp:421-447, 178-182).
 //   tail     while the host turns around: the stable rank of the block's rollouts (the next
 //            update's keep-best) and the next update's Philox draws of its rollouts.
 //
+// filter() (mppi.cpp:450-479) of the published U* is left pending, as the cooperative rollout
+// launch leaves it: the next launch runs it on block 0's second wave beside that block's rollouts
+// (free: a SIMD that was idle), or a read of the optimal cost runs it first (wait_optimal).
+//
 // Cross-block hand-offs follow MI355X_MICROARCH.md's measured forms: payloads stored sc1
 // (write-through) and drained with vmcnt(0) before an agent-scope atomic add; readers poll with
-// sc1 loads and load the payload with sc1 loads.  Every wait is bounded: a block that gives up
-// counts it in Status::wait_timeouts, and the update then fails like the rollout launch's waits.
-// A rollout's arithmetic is pm_rollout_kernel's (kernels.hip) operation for operation, so the
-// costs are bit-identical to the five-launch path; the gradient and the normaliser are summed in
-// another order (rounding only).
+// sc1 loads and load the payload with sc1 loads, issued together.  Every wait is bounded: a block
+// that gives up counts it in Status::wait_timeouts, and the update then fails like the rollout
+// launch's waits.  A rollout's arithmetic is pm_rollout_kernel's (kernels.hip) operation for
+// operation, so the costs are bit-identical to the five-launch path on the same operands; the
+// gradient and the normaliser are summed in another order (rounding only).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -43,9 +49,10 @@ using mppi_dev::smin;
 namespace {
 
 constexpr int PT = PM_FUSED_THREADS;   // threads per block
-constexpr int PR = PM_FUSED_ROWS;      // rollouts per block (one wave rolls them out)
 constexpr int PC = 3;                  // control dimension of the point mass
 constexpr int BAR_SPINS = 1 << 22;     // about a second of s_sleep 1
+constexpr int IB = 8;                  // phase A items per thread per batch of loads
+constexpr int SB = 32;                 // sc1 loads per thread per batch (the finisher's and the rank's staging)
 
 __device__ __forceinline__ double ld_sc1(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -54,6 +61,13 @@ __device__ __forceinline__ void st_sc1(double *p, double v) { __hip_atomic_store
 __device__ __forceinline__ uint64_t rank_key(double c)
 {
     return isnan(c) ? ~0ull : mppi_dev::cost_order_key(c);
+}
+
+// the doubles of the eps rows [PR][H C + 1], which the finisher reuses for every block's partials
+__host__ __device__ inline int64_t pm_region(int PR, int HC, int64_t nb)
+{
+    const int64_t e = (int64_t)PR * (HC + 1), p = nb * HC + nb;
+    return e > p ? e : p;
 }
 
 // Philox eps of (rollout g, step k) for update `upd`: sample_device.hpp's diagonal piece 0, three
@@ -71,14 +85,17 @@ __device__ __forceinline__ void philox_eps(const PmFusedArgs &a, int64_t g, int 
 }
 
 // pm_rollout_kernel's horizon (kernels.hip pm_steps), the same operations in the same order; eps
-// row k at eps[k * PC] (unused when optimal)
-__device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double *Lus, const double *Lgm, const double *eps,
-                                             bool optimal)
+// row k at eps[k * PC] (unused when optimal).  No branch per step: a NaN step cost leaves J NaN
+// to the end, which is the reference's NaN rollout cost (mppi.cpp:331-334); the states it
+// integrates past that point are never read.  (A step cost of +inf followed by -inf, which the
+// reference would sum to NaN and not stop on, is NaN here as well.)
+__device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double *x0, const double *Lus, const double *Lgm,
+                                             const double *eps, bool optimal)
 {
     const DevPointMass &P = a.pm;
     double x[6];
 #pragma unroll
-    for (int i = 0; i < 6; i++) x[i] = a.x0v[i];
+    for (int i = 0; i < 6; i++) x[i] = x0[i];
     double J = 0.0;
 #pragma unroll 4
     for (int k = 0; k < a.H; k++) {
@@ -94,8 +111,10 @@ __device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double 
 #pragma unroll
         for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
         const double sc = Lgm[k] * cost;
-        if (!optimal && isnan(sc)) return NAN;   // rollout cost NaN, stop (mppi.cpp:331-334)
-        J += sc;
+        {
+#pragma clang fp contract(off)
+            J += sc;   // an add of the rounded product, as pm_rollout_kernel's (no fma)
+        }
 #pragma unroll
         for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
 #pragma unroll
@@ -104,25 +123,44 @@ __device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double 
     return J;
 }
 
+// p[0] + p[s] + ... + p[(n - 1) s] from 0.0 in index order (LDS), eight reads in flight at a time
+__device__ __forceinline__ double sum_in_order(const double *p, int n, int s)
+{
+    double acc = 0.0;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = p[(i + u) * s];
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += v[u];
+    }
+    for (; i < n; i++) acc += p[i * s];
+    return acc;
+}
+
 }  // namespace
 
-// LDS (doubles): eps [PR][ES] (ES = H C + 1: the rollout wave's lanes then read distinct banks),
-// U*_shifted [H C], gamma [H], the block's costs [PR] and e_r [PR], the rank's keys [R - 2] and
-// partial counts [3][PR] (ints)
+// LDS (doubles): U*_shifted [H C], gamma [H], the block's costs [PR] and e_r [PR], the rank's keys
+// [R - 2], the eps rows [PR][ES] (ES = H C + 1: the rollout wave's lanes then read distinct banks;
+// the finisher's staged partials after phase B), the rank's partial counts [QD - 1][PR] (ints)
+template <int PR>
 __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
 {
+    static_assert(PT % PR == 0 && PR <= 64, "a thread's phase A items share one rollout; one wave rolls them out");
+    constexpr int QD = PT / PR;   // threads per rollout (phase A items, the rank's key quarters)
     extern __shared__ double lds[];
     const int H = a.H, HC = H * PC, ES = HC + 1, t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int64_t S = a.R - 2;
-    double *Leps = lds;
-    double *Lus = Leps + PR * ES;
+    const int S = (int)(a.R - 2);
+    const int b = blockIdx.x, nb = gridDim.x;
+    double *Lus = lds;
     double *Lgm = Lus + HC;
     double *Lcost = Lgm + H;
     double *Le = Lcost + PR;
     uint64_t *Lkey = reinterpret_cast<uint64_t *>(Le + PR);
-    int *Lcnt = reinterpret_cast<int *>(Lkey + S);
+    double *Leps = reinterpret_cast<double *>(Lkey + S);
+    int *Lcnt = reinterpret_cast<int *>(Leps + pm_region(PR, HC, nb));
     __shared__ int s_last;
-    const int b = blockIdx.x, nb = gridDim.x;
     const int64_t r0 = (int64_t)b * PR;
     const SampleParams &P = a.sp;
     const double *Uprev = a.U;   // U* as the previous update published it
@@ -133,94 +171,99 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     stamp(0);
 
     // ---- phase A: sample (mppi.cpp:189-270) ----
-    for (int i = t; i < HC; i += PT) {   // U*_shifted (mppi.cpp:197-207); unshifted, as last left
+    // every item (step k) of this thread belongs to rollout g = r0 + rl (PT % PR == 0)
+    const int rl = t % PR;
+    const int64_t g = r0 + rl;
+    const bool row = g < a.R;
+    const int64_t gc = row ? g : 0;   // a valid address for the speculative loads of rows past R
+    // loaded unconditionally and first used by the items (rollouts >= 2): its wait falls after the
+    // eps batch is issued
+    const int rank = a.rank[gc];
+    const int keep = P.keep < 0x7FFFFFFF ? (int)P.keep : 0x7FFFFFFF;
+    auto us_at = [&](int i) {   // U*_shifted (mppi.cpp:197-207); unshifted, as last left
         const int k = i / PC, c = i - k * PC;
-        Lus[i] = P.shift_by > 0 ? (k < P.shifted ? Uprev[(k + P.shift_by) * PC + c] : Uprev[(H - 1) * PC + c]) : a.Us[i];
-    }
-    for (int k = t; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
+        return P.shift_by > 0 ? (k < P.shifted ? Uprev[(k + P.shift_by) * PC + c] : Uprev[(H - 1) * PC + c]) : a.Us[i];
+    };
+    // loaded here, stored to LDS after the eps batch: their loads travel with it
+    const double us_t = t < HC ? us_at(t) : 0.0, gm_t = t < H ? a.steps[t].gamma_k : 0.0;
     if (t == 0) s_last = 0;
-    // the block's ranks once (LDS; Lcnt's room, used again only by the tail's rank)
-    int *Lrank = Lcnt;
-    if (t < PR) {
-        const int64_t g = r0 + t;
-        Lrank[t] = (g >= 2 && g < a.R) ? a.rank[g] : 0x7FFFFFFF;
-    }
-    __syncthreads();
-    // items (step k, rollout): consecutive threads, consecutive rollouts; IB items per thread per pass
-    // with their loads issued together (one memory trip per pass, not one per item)
-    constexpr int IB = 4;
-    for (int base = t; base < PR * H; base += PT * IB) {
-        const double *src[IB];
-        double sgn[IB], e[IB][PC];
-        bool draw[IB], store[IB], live[IB];
-        int kk[IB], rr[IB];
+    auto items = [&](int k0) {
+        // both candidate sources of each item (the previous eps shifted, the draw made ahead or -U*)
+        // loaded in one batch with the rank: one memory trip, whichever the rank picks
+        double ep[IB][PC], en[IB][PC];
 #pragma unroll
         for (int u = 0; u < IB; u++) {
-            const int i = base + u * PT;
-            const int k = i / PR, rl = i - k * PR;
-            const int64_t g = r0 + rl;   // unsharded: local = global
-            kk[u] = k;
-            rr[u] = rl;
-            live[u] = i < PR * H && g < a.R;
-            src[u] = Uprev;   // any valid address
-            sgn[u] = 1.0;
-            draw[u] = false;
-            store[u] = true;
-            if (!live[u]) continue;
-            const int rank = Lrank[rl];
-            if (g == 0) {
-                sgn[u] = 0.0;
-            } else if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
-                src[u] = Uprev + k * PC;
-                sgn[u] = -1.0;
-            } else if (rank < P.keep && (P.shift_by <= 0 || k < P.shifted)) {   // kept: the previous eps, shifted
-                src[u] = a.prev + (((int64_t)k + (P.shift_by > 0 ? P.shift_by : 0)) * a.Rpad + g) * PC;
-            } else if (a.ahead) {   // the previous launch's tail drew it into this update's buffer: in place
-                src[u] = a.noise + ((int64_t)k * a.Rpad + g) * PC;
-                store[u] = false;
-            } else {
-                draw[u] = true;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < IB; u++)
-#pragma unroll
-            for (int c = 0; c < PC; c++) e[u][c] = src[u][c];
-#pragma unroll
-        for (int u = 0; u < IB; u++) {
-            const int i = base + u * PT;
-            if (i >= PR * H) break;
-            const int k = kk[u], rl = rr[u];
-            if (!live[u]) {   // rows past R: zeros, which the gradient's fixed 64-row sum multiplies by 0
-#pragma unroll
-                for (int c = 0; c < PC; c++) Leps[rl * ES + k * PC + c] = 0.0;
-                continue;
-            }
-            if (draw[u]) philox_eps(a, r0 + rl, k, P.update_index, e[u]);
-            else if (sgn[u] != 1.0)
-#pragma unroll
-                for (int c = 0; c < PC; c++) e[u][c] = sgn[u] == 0.0 ? 0.0 : sgn[u] * e[u][c];   // rollout 0: +0
-            double *o = a.noise + ((int64_t)k * a.Rpad + r0 + rl) * PC;
+            if (k0 + u * QD >= H) break;
+            const int k = k0 + u * QD;
+            const int kp = (P.shift_by > 0 && k < P.shifted) ? k + P.shift_by : k;
+            const double *pp = a.prev + ((int64_t)kp * a.Rpad + gc) * PC;
+            const double *pn = g == 1 ? Uprev + k * PC : a.noise + ((int64_t)k * a.Rpad + gc) * PC;
 #pragma unroll
             for (int c = 0; c < PC; c++) {
-                Leps[rl * ES + k * PC + c] = e[u][c];
-                if (store[u]) o[c] = e[u][c];
+                ep[u][c] = pp[c];
+                en[u][c] = pn[c];
             }
         }
-    }
+        int rk = rank;
+        asm volatile("" : "+v"(rk));   // the rank's first use here, not hoisted ahead of the batch
+#pragma unroll
+        for (int u = 0; u < IB; u++) {
+            const int k = k0 + u * QD;
+            if (k >= H) break;
+            double *le = Leps + rl * ES + k * PC;
+            if (!row) {   // rows past R: zeros, which the gradient's fixed PR-row sum multiplies by 0
+#pragma unroll
+                for (int c = 0; c < PC; c++) le[c] = 0.0;
+                continue;
+            }
+            double e[PC];
+            bool store = true;
+            if (g == 0) {
+#pragma unroll
+                for (int c = 0; c < PC; c++) e[c] = 0.0;
+            } else if (g == 1) {   // m_rollouts[1].noise = -m_optimal_control
+#pragma unroll
+                for (int c = 0; c < PC; c++) e[c] = -1.0 * en[u][c];
+            } else if (rk < keep && (P.shift_by <= 0 || k < P.shifted)) {   // kept: the previous eps, shifted
+#pragma unroll
+                for (int c = 0; c < PC; c++) e[c] = ep[u][c];
+            } else if (a.ahead) {   // the previous launch's tail drew it into this update's buffer: in place
+#pragma unroll
+                for (int c = 0; c < PC; c++) e[c] = en[u][c];
+                store = false;
+            } else {
+                philox_eps(a, g, k, P.update_index, e);
+            }
+            double *o = a.noise + ((int64_t)k * a.Rpad + g) * PC;
+#pragma unroll
+            for (int c = 0; c < PC; c++) {
+                le[c] = e[c];
+                if (store) o[c] = e[c];
+            }
+        }
+    };
+    if (H <= QD * IB)   // the common case straight-line: no loop header for the waits to merge at
+        items(t / PR);
+    else
+        for (int k0 = t / PR; k0 < H; k0 += QD * IB) items(k0);
+    if (t < HC) Lus[t] = us_t;
+    for (int i = t + PT; i < HC; i += PT) Lus[i] = us_at(i);
+    if (t < H) Lgm[t] = gm_t;
+    for (int k = t + PT; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
     if (b == 0 && t < a.X) a.x0_out[t] = a.x0v[t];
     __syncthreads();
     stamp(1);
+    const int64_t gr = r0 + l;   // the rollout wave's lane l
     if (w == 0) {   // rollouts (mppi.cpp:272-342): one lane per rollout
-        const int64_t g = r0 + l;
+        const bool mine = l < PR && gr < a.R;
         double J = NAN;
-        if (g < a.R) {
-            J = pm_rollout(a, Lus, Lgm, Leps + l * ES, false);
-            st_sc1(a.cost + g, J);   // read by every block's rank (tail)
+        if (mine) {
+            J = pm_rollout(a, a.x0v, Lus, Lgm, Leps + l * ES, false);
+            st_sc1(a.cost + gr, J);   // read by every block's rank (tail)
         }
-        Lcost[l] = J;
+        if (l < PR) Lcost[l] = J;
         // the block's min / max / count, then one exact key atomic each into CostStats slot b % 64
-        const bool ok = g < a.R && !isnan(J);
+        const bool ok = mine && !isnan(J);
         const unsigned long long key = ok ? mppi_dev::cost_order_key(J) : 0ull;
         const unsigned long long kn = mppi_dev::wave_umin64_dpp(ok ? key : ~0ull);
         const unsigned long long kx = mppi_dev::wave_umax64_dpp(ok ? key : 0ull);
@@ -232,6 +275,15 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             atomicAdd(&a.stats->count[32 * slot], (unsigned)n);
         }
         __builtin_amdgcn_s_waitcnt(0);   // the cost stores and the atomics have left this wave
+    } else if (w == 1 && b == 0 && a.fold_filter && l == 0) {
+        // the previous update's filter() (mppi.cpp:450-479), which its launch left pending: the cost
+        // of the U* it published (not yet rewritten: this launch's finisher writes it after the
+        // barrier, which this block reaches after this) from its state; none when it threw
+        const Status *st = a.status;
+        if (!st->all_nan && !st->sg_error) {
+            st_sc1(a.opt_cost, pm_rollout(a, a.fx0, a.U, Lgm, nullptr, true));
+            __builtin_amdgcn_s_waitcnt(0);   // read by the finisher (its host block's optimal cost)
+        }
     }
     __syncthreads();
     stamp(2);
@@ -262,17 +314,18 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     const bool early = all_nan || difference < 1e-6;   // early return, weights / gradient stale (mppi.cpp:373-375)
     if (!early) {
         if (w == 0) {   // e_r of the block's rollouts, their sum in lane order
-            const int64_t g = r0 + l;
-            const double c = Lcost[l];
-            const double e = (g < a.R && !isnan(c)) ? exp(-a.cost_scale * (c - mn) / difference) : 0.0;
-            Le[l] = e;
-            if (g < a.R) a.wexp[g] = e;
+            const bool mine = l < PR && gr < a.R;
+            const double c = mine ? Lcost[l] : 0.0;
+            const double e = (mine && !isnan(c)) ? exp(-a.cost_scale * (c - mn) / difference) : 0.0;
+            if (l < PR) Le[l] = e;
+            if (mine) a.wexp[gr] = e;
             const double s = mppi_dev::wave_sum_dpp(e);
             if (l == 0) st_sc1(a.tpart + b, s);
         }
         __syncthreads();
         for (int o = t; o < HC; o += PT) {   // partial gradient: the block's rollouts in order
             double acc = 0.0;
+#pragma unroll
             for (int r = 0; r < PR; r++) acc = __builtin_fma(Le[r], Leps[r * ES + o], acc);
             st_sc1(a.gpart + (int64_t)b * HC + o, acc);
         }
@@ -285,22 +338,38 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         s_last = old + 1 == target;
     }
     __syncthreads();
+    // the rank's keys (every block's tail), and in the finishing block every block's partials
+    // (gradient [nb][HC], then normalisers [nb]) over the eps rows: one batch of sc1 loads, SB per
+    // thread in flight at once (the other blocks stored them this launch)
+    double *Lst = Leps;
+    const int G = nb * HC, np = (s_last && !early) ? G + nb : 0, n = np + S;
+    for (int base = t; base < n; base += PT * SB) {
+        double v[SB];
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int j = min(base + u * PT, n - 1);
+            v[u] = ld_sc1(j < G && j < np ? a.gpart + j : j < np ? a.tpart + (j - G) : a.cost + 2 + (j - np));
+        }
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+            const int j = base + u * PT;
+            if (j < np) Lst[j] = v[u];
+            else if (j < n) Lkey[j - np] = rank_key(v[u]);
+        }
+    }
+    __syncthreads();
     if (s_last) {
         Status *st = a.status;
         const int wt = __hip_atomic_load(&st->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool upd = !early && !wt, ok = !all_nan && !wt;
-        double total = 0.0;
-        if (upd)
-            for (int i = 0; i < nb; i++) total += ld_sc1(a.tpart + i);
+        const double total = upd ? sum_in_order(Lst + G, nb, 1) : 0.0;
         for (int o = t; o < HC; o += PT) {   // finish (mppi.cpp:421-447) and publish (178-182)
             const int c = o % PC;
             double u = Lus[o];
             if (upd) {
-                double g = 0.0;
-                for (int i = 0; i < nb; i++) g += ld_sc1(a.gpart + (int64_t)i * HC + o);
-                g /= total;   // sum_r e_r eps_r / sum_r e_r
-                a.gradient[o] = g;
-                u += g * a.gradient_step;
+                const double gs = sum_in_order(Lst + o, nb, HC) / total;   // sum_r e_r eps_r / sum_r e_r
+                a.gradient[o] = gs;
+                u += gs * a.gradient_step;
                 if (a.control_bound) u = smax(smin(u, a.cmax[c]), a.cmin[c]);
             }
             Lus[o] = u;
@@ -322,7 +391,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
                 for (int i = 1; i < GRAD_SPLIT; i++) st->tsplit[i] = 0.0;
             }
             st->sg_error = wt != 0;   // "the update threw": no filter() (as the finish kernels)
-            a.out[HC + 0] = *a.opt_cost;
+            a.out[HC + 0] = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
             a.out[HC + 1] = (double)all_nan;
             a.out[HC + 2] = (double)early;
             a.out[HC + 3] = 0.0;
@@ -336,43 +405,38 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             st->wait_timeouts = 0;
             __threadfence_system();
             __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            stamp(5);
-            // filter() (mppi.cpp:450-479): the cost of the published U* from this update's state,
-            // while the host takes the result; none when the update threw
-            if (ok) *a.opt_cost = pm_rollout(a, Lus, Lgm, nullptr, true);
         }
+        stamp(5);
     }
     // ---- tail: the next update's stable order and draws, behind the publish ----
-    // rank (sample(), mppi.cpp:222-231) of the block's rollouts among rollouts 2..R-1: NaN last,
-    // ties by index; four threads per rollout, each over a quarter of the keys (staged in LDS from
-    // sc1 loads: the other blocks stored them this launch)
-    for (int64_t j = t; j < S; j += PT) Lkey[j] = rank_key(ld_sc1(a.cost + 2 + j));
-    __syncthreads();
+    // rank (sample(), mppi.cpp:222-231) of the block's rollouts among rollouts 2..R-1 (keys staged
+    // above): NaN last, ties by index; QD threads per rollout, each over its share of the keys
     {
-        const int rl = t & (PR - 1), qd = t >> 6;
-        const int64_t i = r0 + rl - 2;
+        const int qd = t / PR;
+        const int i = (int)g - 2;
         int cnt = 0;
         if (i >= 0 && i < S) {
             const uint64_t ki = Lkey[i];
-            const int64_t j0 = (S * qd) / 4, j1 = (S * (qd + 1)) / 4;
+            const int j0 = (S * qd) / QD, j1 = (S * (qd + 1)) / QD;
 #pragma unroll 8
-            for (int64_t j = j0; j < j1; j++) {   // unrolled: the LDS reads of eight keys in flight
+            for (int j = j0; j < j1; j++) {   // unrolled: the LDS reads of eight keys in flight
                 const uint64_t kj = Lkey[j];
                 cnt += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
             }
         }
         if (qd > 0) Lcnt[(qd - 1) * PR + rl] = cnt;
         __syncthreads();
-        if (qd == 0 && i >= 0 && i < S) a.rank[i + 2] = cnt + Lcnt[rl] + Lcnt[PR + rl] + Lcnt[2 * PR + rl];
+        if (qd == 0 && i >= 0 && i < S) {
+#pragma unroll
+            for (int q = 1; q < QD; q++) cnt += Lcnt[(q - 1) * PR + rl];
+            a.rank[g] = cnt;
+        }
     }
     stamp(6);
     // the next update's draws (Philox by (rollout, step), its update index) into the buffer it will
     // sample from: rollouts >= 2 (rollout 0 is zero and rollout 1 -U* at sampling time)
-    if (a.ahead_noise) {
-        for (int i = t; i < PR * H; i += PT) {
-            const int k = i / PR, rl = i - k * PR;
-            const int64_t g = r0 + rl;
-            if (g < 2 || g >= a.R) continue;
+    if (a.ahead_noise && row && g >= 2) {
+        for (int k = t / PR; k < H; k += QD) {
             double e[PC];
             philox_eps(a, g, k, P.update_index + 1, e);
             double *o = a.ahead_noise + ((int64_t)k * a.Rpad + g) * PC;
@@ -385,23 +449,42 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
 
 namespace mppi_eng {
 
-size_t pm_fused_lds_bytes(int64_t R, int H)
+static size_t lds_bytes(int PR, int64_t R, int H)
 {
-    const int64_t HC = (int64_t)H * PC;
-    return (size_t)((PR * (HC + 1) + HC + H + 2 * PR + (R - 2)) * 8 + 3 * PR * 4);
+    const int HC = H * PC;
+    const int64_t nb = (R + PR - 1) / PR;
+    return (size_t)((HC + H + 2 * PR + (R - 2) + pm_region(PR, HC, nb)) * 8 + (PT / PR - 1) * PR * 4);
 }
 
-bool pm_fused_fits(int64_t R, int H)
+int pm_fused_rows(int64_t R, int H)
 {
-    return R >= 4 && H >= 1 && R <= PM_FUSED_MAX_R && (int64_t)H * PC <= 4 * PT && pm_fused_lds_bytes(R, H) <= 150 * 1024;
+    if (R < 4 || H < 1 || R > PM_FUSED_MAX_R) return 0;
+    for (int PR = 16; PR <= 64; PR *= 2)
+        if ((R + PR - 1) / PR <= PM_FUSED_MAX_BLOCKS && lds_bytes(PR, R, H) <= 150 * 1024) return PR;
+    return 0;
 }
+
+size_t pm_fused_lds_bytes(int64_t R, int H)
+{
+    const int PR = pm_fused_rows(R, H);
+    return PR ? lds_bytes(PR, R, H) : 0;
+}
+
+bool pm_fused_fits(int64_t R, int H) { return pm_fused_rows(R, H) != 0; }
 
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s)
 {
     if (!pm_fused_fits(a.R, a.H)) return hipErrorInvalidValue;
+    const int PR = pm_fused_rows(a.R, a.H);
     const unsigned nb = (unsigned)((a.R + PR - 1) / PR);
     if (nb != a.nblocks) return hipErrorInvalidValue;   // the barrier and ticket targets assume it
-    hipLaunchKernelGGL(pm_update_kernel, dim3(nb), dim3(PT), pm_fused_lds_bytes(a.R, a.H), s, a);
+    const size_t lds = pm_fused_lds_bytes(a.R, a.H);
+    if (PR == 16)
+        hipLaunchKernelGGL(pm_update_kernel<16>, dim3(nb), dim3(PT), lds, s, a);
+    else if (PR == 32)
+        hipLaunchKernelGGL(pm_update_kernel<32>, dim3(nb), dim3(PT), lds, s, a);
+    else
+        hipLaunchKernelGGL(pm_update_kernel<64>, dim3(nb), dim3(PT), lds, s, a);
     return hipGetLastError();
 }
 

@@ -52,10 +52,11 @@ def test_epilogue_equals_three_launches(rollouts, horison, objective, monkeypatc
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
 
 
-def test_epilogue_wait_timeout_fails_the_update():
+def test_epilogue_wait_timeout_fails_the_update(monkeypatch):
     """A relay stage that never signals (mppi_debug_inject) in a launch with the epilogue: the
     finisher sees the in-launch timeouts, publishes nothing and the update fails; the updates after
     it run the epilogue again and time nothing out."""
+    monkeypatch.setenv("MPPI_EPILOGUE", "1")   # opt-in (engine.cpp epilogue_wanted)
     conf = am.frankaridgeback_configuration(rollouts=4096, horison=0.64, keep_best_rollouts=20, threads=8)
     t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
     t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)

@@ -50,10 +50,12 @@ def test_fused_update_equals_five_launches(S, horison, monkeypatch):
         np.testing.assert_array_equal(a[0][2:], b[0][2:], err_msg="update %d noise" % j)
         # rollout 1 = -U*, which the two paths round differently (the gradient's summation order)
         np.testing.assert_allclose(a[0][1], b[0][1], rtol=0, atol=1e-12, err_msg="update %d noise" % j)
-        np.testing.assert_array_equal(a[1][0], b[1][0], err_msg="update %d costs" % j)
-        np.testing.assert_array_equal(a[1][2:], b[1][2:], err_msg="update %d costs" % j)
-        np.testing.assert_allclose(a[1][1], b[1][1], rtol=1e-12, err_msg="update %d costs" % j)
-        np.testing.assert_allclose(a[2], b[2], rtol=1e-13, atol=1e-16, err_msg="update %d weights" % j)
+        if j == 0:   # the same nominal (zeros): the same arithmetic on the same operands
+            np.testing.assert_array_equal(a[1], b[1], err_msg="update %d costs" % j)
+        else:   # every rollout rides the shifted U*, which carries the gradient's rounding
+            np.testing.assert_allclose(a[1], b[1], rtol=1e-13, atol=0, err_msg="update %d costs" % j)
+        # exp(-s (c - min) / (max - min)) carries the costs' rounding, scaled by s (c - min) / (max - min)
+        np.testing.assert_allclose(a[2], b[2], rtol=1e-13 if j == 0 else 1e-11, atol=1e-16, err_msg="update %d weights" % j)
         np.testing.assert_allclose(a[3], b[3], rtol=0, atol=1e-12, err_msg="update %d gradient" % j)
         np.testing.assert_allclose(a[4], b[4], rtol=0, atol=1e-12, err_msg="update %d U*" % j)
         assert abs(a[5] - b[5]) <= 1e-12 * max(1.0, abs(b[5])), (j, a[5], b[5])

@@ -14,6 +14,7 @@
 #                      NAME names the output, default "trace")
 #   tracepm            trace of the point-mass workload (configs[1]), 200 updates
 #   pmc                rocprofv3 PMC passes (one counter set per run) -> pmc summaries + traffic JSON
+#   pmcpm              the fetch / write / fp64 passes over the fused point-mass launch (configs[1])
 #   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
 #                      65536x128 SG)
 #   ab:V1,V2,..:N      N interleaved rounds of bench over kernel variants (gpurun_variants/<V>/,
@@ -81,20 +82,29 @@ step_trace() {   # [name] [extra bench args...]
     return 0
 }
 
-step_pmc() {
-    local B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline $BENCH_ARGS" D=$O/pmc
+step_pmc() {   # [pm]
+    local B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline $BENCH_ARGS" D=$O/pmc out=$O/pmc_rollout.json prefix=
+    if [ "$1" = pm ]; then
+        B="python3 bench.py --workload point_mass --steps 50 --warmup 5 --no-cpu-baseline"
+        D=$O/pmcpm out=$O/pmc_pm.json prefix=pm_update_kernel
+    fi
     mkdir -p $D
     run() {   # name counters...
         local n=$1; shift
         timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace -d $D -o $n --output-format csv -- $B > $D/$n.log 2>&1
     }
-    run sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY && echo "pmc sq ok" && \
-    run lat SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && echo "pmc lat ok" && \
+    local names="sq lat flops fetch write"
+    if [ "$1" = pm ]; then
+        names="flops fetch write"
+    else
+        run sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY && echo "pmc sq ok" && \
+        run lat SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE && echo "pmc lat ok" || return 1
+    fi
     run flops SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_UNALIGNED_STALL && echo "pmc flops ok" && \
     run fetch FETCH_SIZE GRBM_GUI_ACTIVE && echo "pmc fetch ok" && \
     run write WRITE_SIZE && echo "pmc write ok" || return 1
-    for n in sq lat flops fetch write; do python3 tools/pmc_summary.py $D/${n}_counter_collection.csv > $D/${n}_summary.txt; done
-    python3 tools/pmc_traffic.py $D $O/pmc_rollout.json && cat $O/pmc_rollout.json
+    for n in $names; do python3 tools/pmc_summary.py $D/${n}_counter_collection.csv > $D/${n}_summary.txt; done
+    python3 tools/pmc_traffic.py $D $out $prefix && cat $out
 }
 
 step_sizes() {
@@ -133,7 +143,7 @@ step_pmstamps() {   # the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS
 }
 
 step_epstamps() {   # the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1, printed at destroy)
-    MPPI_EP_STAMPS=1 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline $BENCH_ARGS \
+    MPPI_EPILOGUE=1 MPPI_EP_STAMPS=1 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline $BENCH_ARGS \
         > $O/epstamps.json 2> $O/epstamps.err || { echo "epstamps rc=$?"; tail -20 $O/epstamps.err; return 1; }
     grep "epilogue phases" $O/epstamps.err
     summary $O/epstamps.json epstamps
@@ -158,6 +168,7 @@ for s in "$@"; do
         trace) step_trace "$arg" ;;
         tracepm) step_trace tracepm --workload point_mass --steps 200 ;;
         pmc) step_pmc ;;
+        pmcpm) step_pmc pm ;;
         sizes) step_sizes ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;

@@ -6,7 +6,7 @@ FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled here; the rollout ke
 8-B-per-lane eps loads (a width the guide leaves uncalibrated) - the doubled figure agrees with
 the 25.2 MB eps tensor, which is the check that the correction applies.
 
-usage: pmc_traffic.py <pmc dir> <out.json> [kernel name prefix]   (default: the rollout launch, "[main]")
+usage: pmc_traffic.py <pmc dir> <out.json> [kernel name part]   (default: the rollout launch, "[main]")
 """
 import json
 import sys
@@ -19,7 +19,7 @@ def main(d, out, prefix=None):
     fetch = summarize(d + "/fetch_counter_collection.csv")
     write = summarize(d + "/write_counter_collection.csv")
     flops = summarize(d + "/flops_counter_collection.csv")
-    key = [k for k in fetch if (k.startswith(prefix) if prefix else k.endswith("[main]"))][0]
+    key = [k for k in fetch if ((prefix in k) if prefix else k.endswith("[main]"))][0]
     kib = 1024.0
     f = fetch[key]["FETCH_SIZE"] * kib * 2.0
     w = write[key]["WRITE_SIZE"] * kib
