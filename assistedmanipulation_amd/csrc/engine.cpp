@@ -1094,7 +1094,8 @@ void mppi_destroy(mppi_handle *h)
     if (h->pm_stamp_n > 0) {
         std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
                      (long long)h->pm_stamp_n);
-        static const char *names[PM_STAMPS] = {"entry", "sampled", "rolled", "barrier", "partials", "published", "ranked", "end"};
+        static const char *names[PM_STAMPS] = {"entry", "sampled", "rolled", "barrier", "partials", "ticket",
+                                               "staged", "stored", "published", "ranked", "end"};
         for (int i = 0; i < PM_STAMPS; i++) std::fprintf(stderr, " %s %.2f", names[i], h->pm_stamp_sum[(size_t)i] / (double)h->pm_stamp_n);
         std::fprintf(stderr, "\n");
     }
@@ -2231,13 +2232,9 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
         uint64_t t0 = ~0ull;
         for (unsigned b = 0; b < h->pm_nblocks; b++) t0 = std::min(t0, sv[(size_t)b * PM_STAMPS]);
         for (int i = 0; i < PM_STAMPS; i++) {
-            uint64_t mx = 0;   // the phase's last block (s_memrealtime: 100 MHz)
+            uint64_t mx = t0;   // the phase's last block (s_memrealtime: 100 MHz); the finisher's
+                                // stamps only in its block (the others stay 0)
             for (unsigned b = 0; b < h->pm_nblocks; b++) mx = std::max(mx, sv[(size_t)b * PM_STAMPS + i]);
-            if (i == 5) {   // the publish: only the finishing block stamps it
-                mx = 0;
-                for (unsigned b = 0; b < h->pm_nblocks; b++)
-                    if (sv[(size_t)b * PM_STAMPS + 5] > t0) mx = std::max(mx, sv[(size_t)b * PM_STAMPS + 5]);
-            }
             h->pm_stamp_sum[(size_t)i] += (double)(mx - t0) * 0.01;
         }
         h->pm_stamp_n++;

@@ -2627,14 +2627,18 @@ __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
     for (int i = 1; i < GRAD_SPLIT; i++) total += tsp[i];
     const double *__restrict__ gs = a.gsplit;
     double *__restrict__ U = a.U;
-    // U*_shifted reads U* at shifted positions: every element's inputs are read before any U* store
-    double us[EP_MAXE], uos[EP_MAXE];
+    const double mn = ep_ld(&st->minimum), mx = ep_ld(&st->maximum);
+    // U*_shifted reads U* at shifted positions: every element's inputs are read before any U* store;
+    // the gradient partials with them (one memory trip for the whole finish)
+    double us[EP_MAXE], uos[EP_MAXE], gp[EP_MAXE][GRAD_SPLIT];
 #pragma unroll
     for (int e = 0; e < EP_MAXE; e++) {
         const int t = tid + e * NT;
         if (t < HC) {
             us[e] = sa.sp.shift_by > 0 ? mppi_sample::shifted_u(sa, t / a.C, t % a.C) : a.Ushift[t];
             uos[e] = U[t];
+#pragma unroll
+            for (int i = 0; i < GRAD_SPLIT; i++) gp[e][i] = ep_ld(gs + (int64_t)i * HC + t);
         }
     }
     __syncthreads();
@@ -2643,8 +2647,9 @@ __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
         const int t = tid + e * NT;
         if (t >= HC) break;
         const int c = t % a.C;
-        double g = ep_ld(gs + t);
-        for (int i = 1; i < GRAD_SPLIT; i++) g += ep_ld(gs + (int64_t)i * HC + t);
+        double g = gp[e][0];
+#pragma unroll
+        for (int i = 1; i < GRAD_SPLIT; i++) g += gp[e][i];
         g /= total;   // sum_r e_r eps_r / sum_r e_r
         double u = us[e];
         const double uo = uos[e];
@@ -2671,8 +2676,8 @@ __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
         a.out[HC + 1] = (double)all_nan;
         a.out[HC + 2] = (double)early;
         a.out[HC + 3] = 0.0;
-        a.out[HC + 4] = ep_ld(&st->minimum);
-        a.out[HC + 5] = ep_ld(&st->maximum);
+        a.out[HC + 4] = mn;
+        a.out[HC + 5] = mx;
         a.out[HC + 7] = (double)wt;
     }
     if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, tid);

@@ -1303,22 +1303,36 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
 __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
 {
     const int HC = a.H * a.C;
-    const int wt = update_wait_timeouts(a);
-    const bool upd = !a.status->early && !wt, ok = !a.status->all_nan && !wt;   // no filter: no SG error
+    const Status stt = *a.status;   // the status words, the normaliser partials, min / max: one batch
+    const int wt = a.wait_all ? (int)*a.wait_all : stt.wait_timeouts;   // update_wait_timeouts
+    const bool upd = !stt.early && !wt, ok = !stt.all_nan && !wt;   // no filter: no SG error
     const double oc = threadIdx.x == 0 ? *a.opt_cost : 0.0;
+    const double x0 = (int)threadIdx.x < a.X ? a.x0[threadIdx.x] : 0.0;
     const int nsp = a.ns > 0 ? a.ns : 1;
     const double *__restrict__ gs = a.ns > 0 ? a.gsplit : a.gpart;
     double *__restrict__ Us = a.Ushift;
     double *__restrict__ U = a.U;
-    const double total = softmin_total(*a.status);
+    double total = stt.tsplit[0];   // softmin_total
+#pragma unroll
+    for (int i = 1; i < GRAD_SPLIT; i++) total += stt.tsplit[i];
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
         const int c = t % a.C;
-        double g = gs[t];
-        for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
-        g /= total;   // sum_r e_r eps_r / sum_r e_r
-        double u = Us[t];
+        double u = Us[t];   // loaded first: with the partials in one trip
         const double uo = U[t];
         const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
+        double g;
+        if (nsp == GRAD_SPLIT) {   // the usual split: its partials loaded together, added in order
+            double p[GRAD_SPLIT];
+#pragma unroll
+            for (int i = 0; i < GRAD_SPLIT; i++) p[i] = gs[(int64_t)i * HC + t];
+            g = p[0];
+#pragma unroll
+            for (int i = 1; i < GRAD_SPLIT; i++) g += p[i];
+        } else {
+            g = gs[t];
+            for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
+        }
+        g /= total;   // sum_r e_r eps_r / sum_r e_r
         if (upd) {
             a.gradient[t] = g;
             u += g * a.gradient_step;
@@ -1332,10 +1346,9 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         if (ok) U[t] = v;
         a.out[t] = v;
     }
-    if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
+    if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = x0;
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
-        const Status stt = *a.status;
         a.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
         if (upd) a.status_w->total = total;
         a.out[HC + 0] = oc;

@@ -411,7 +411,9 @@ struct PmFusedArgs {
     const double *fx0;          // its state (x0_opt as the previous launch left it)
     uint64_t *stamps;           // diagnostics (MPPI_PM_STAMPS=1): [nblocks][PM_STAMPS] s_memrealtime, or null
 };
-constexpr int PM_STAMPS = 8;   // entry, sampled, rolled out, barrier passed, partials stored, published, ranked, end
+// entry, sampled, rolled out, barrier passed, partials stored, ticket taken, staged, (finisher:)
+// stored, published, ranked, end
+constexpr int PM_STAMPS = 11;
 bool pm_fused_fits(int64_t R, int H);
 size_t pm_fused_lds_bytes(int64_t R, int H);
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);

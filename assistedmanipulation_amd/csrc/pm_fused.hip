@@ -52,7 +52,10 @@ constexpr int PT = PM_FUSED_THREADS;   // threads per block
 constexpr int PC = 3;                  // control dimension of the point mass
 constexpr int BAR_SPINS = 1 << 22;     // about a second of s_sleep 1
 constexpr int IB = 8;                  // phase A items per thread per batch of loads
-constexpr int SB = 32;                 // sc1 loads per thread per batch (the finisher's and the rank's staging)
+#ifndef PM_SB
+#define PM_SB 32
+#endif
+constexpr int SB = PM_SB;              // sc1 loads per thread per batch (the finisher's and the rank's staging)
 
 __device__ __forceinline__ double ld_sc1(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -338,17 +341,31 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         s_last = old + 1 == target;
     }
     __syncthreads();
+    stamp(5);
     // the rank's keys (every block's tail), and in the finishing block every block's partials
     // (gradient [nb][HC], then normalisers [nb]) over the eps rows: one batch of sc1 loads, SB per
     // thread in flight at once (the other blocks stored them this launch)
+#ifdef PM_STAGE_PLAIN
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (A/B) one invalidate, then plain loads
+#endif
     double *Lst = Leps;
     const int G = nb * HC, np = (s_last && !early) ? G + nb : 0, n = np + S;
+    int wt = 0;
+    double oc = 0.0;
+    if (s_last) {   // issued with the batch (their own trips otherwise)
+        wt = __hip_atomic_load(&a.status->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        oc = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
+    }
     for (int base = t; base < n; base += PT * SB) {
         double v[SB];
 #pragma unroll
         for (int u = 0; u < SB; u++) {
             const int j = min(base + u * PT, n - 1);
+#ifdef PM_STAGE_PLAIN
+            v[u] = *(j < G && j < np ? a.gpart + j : j < np ? a.tpart + (j - G) : a.cost + 2 + (j - np));
+#else
             v[u] = ld_sc1(j < G && j < np ? a.gpart + j : j < np ? a.tpart + (j - G) : a.cost + 2 + (j - np));
+#endif
         }
 #pragma unroll
         for (int u = 0; u < SB; u++) {
@@ -358,9 +375,9 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         }
     }
     __syncthreads();
+    stamp(6);
     if (s_last) {
         Status *st = a.status;
-        const int wt = __hip_atomic_load(&st->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool upd = !early && !wt, ok = !all_nan && !wt;
         const double total = upd ? sum_in_order(Lst + G, nb, 1) : 0.0;
         for (int o = t; o < HC; o += PT) {   // finish (mppi.cpp:421-447) and publish (178-182)
@@ -391,7 +408,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
                 for (int i = 1; i < GRAD_SPLIT; i++) st->tsplit[i] = 0.0;
             }
             st->sg_error = wt != 0;   // "the update threw": no filter() (as the finish kernels)
-            a.out[HC + 0] = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
+            a.out[HC + 0] = oc;
             a.out[HC + 1] = (double)all_nan;
             a.out[HC + 2] = (double)early;
             a.out[HC + 3] = 0.0;
@@ -401,12 +418,13 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         }
         if (t < CS_SLOTS) mppi_sample::reset_cost_stats(a.stats, t);   // every block has read them (ticket)
         __syncthreads();
+        stamp(7);
         if (t == 0) {
             st->wait_timeouts = 0;
             __threadfence_system();
             __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        stamp(5);
+        stamp(8);
     }
     // ---- tail: the next update's stable order and draws, behind the publish ----
     // rank (sample(), mppi.cpp:222-231) of the block's rollouts among rollouts 2..R-1 (keys staged
@@ -432,7 +450,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             a.rank[g] = cnt;
         }
     }
-    stamp(6);
+    stamp(9);
     // the next update's draws (Philox by (rollout, step), its update index) into the buffer it will
     // sample from: rollouts >= 2 (rollout 0 is zero and rollout 1 -U* at sampling time)
     if (a.ahead_noise && row && g >= 2) {
@@ -444,7 +462,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             for (int c = 0; c < PC; c++) o[c] = e[c];
         }
     }
-    stamp(7);
+    stamp(10);
 }
 
 namespace mppi_eng {

@@ -20,7 +20,7 @@
 #   ab:V1,V2,..:N      N interleaved rounds of bench over kernel variants (gpurun_variants/<V>/,
 #                      built by tools/ab_build.sh; "tree" = the in-tree library); BENCH_ARGS and
 #                      AB_ENV_<V> (extra env for variant V, e.g. AB_ENV_tree0="MPPI_HANDOVER=0") apply
-#   pmstamps           the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1)
+#   pmstamps[:VARIANT] the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1), in-tree or a variant
 #   epstamps           the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1)
 #   wtrace:VARIANT     per-wave trace of VARIANT's COOP_TRACE build (tools/wave_trace_r03.py)
 # Output: gpurun_out/$TAG/.
@@ -135,11 +135,13 @@ step_ab() {   # V1,V2,..  rounds
     done
 }
 
-step_pmstamps() {   # the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1, printed at destroy)
-    MPPI_PM_STAMPS=1 timeout -k 10 200 python -u bench.py --workload point_mass --steps 100 --warmup 10 --no-cpu-baseline \
-        > $O/pmstamps.json 2> $O/pmstamps.err || { echo "pmstamps rc=$?"; tail -20 $O/pmstamps.err; return 1; }
-    grep "pm_update_kernel phases" $O/pmstamps.err
-    summary $O/pmstamps.json pmstamps
+step_pmstamps() {   # [variant]: the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1, printed at destroy)
+    local lib=$PWD/assistedmanipulation_amd/lib/libmppi_amd.so n=pmstamps${1:+_$1}
+    [ -n "$1" ] && lib=$PWD/gpurun_variants/$1/libmppi_amd.so
+    MPPI_AMD_LIB=$lib MPPI_PM_STAMPS=1 timeout -k 10 200 python -u bench.py --workload point_mass --steps 100 --warmup 10 \
+        --no-cpu-baseline > $O/$n.json 2> $O/$n.err || { echo "$n rc=$?"; tail -20 $O/$n.err; return 1; }
+    grep "pm_update_kernel phases" $O/$n.err
+    summary $O/$n.json $n
 }
 
 step_epstamps() {   # the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1, printed at destroy)
@@ -172,7 +174,7 @@ for s in "$@"; do
         sizes) step_sizes ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;
-        pmstamps) step_pmstamps ;;
+        pmstamps) step_pmstamps "$arg" ;;
         epstamps) step_epstamps ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac || { echo "step $s failed"; exit 1; }
