@@ -478,6 +478,16 @@ mppi_status check_topology(const mppi_frankaridgeback_desc &d, std::string &why)
                 why = "body " + std::to_string(i) + " (planar base joint) placement must be unrotated";
                 return MPPI_ERR_UNSUPPORTED;
             }
+    // Bodies 2 and 3 (pivot_joint, panda_joint1) turn about z: with z-rotation placements the world
+    // poses of bodies 0..3 are a rotation about z and a translation, which the FK scan's last level
+    // composes in planar form (fr_coop.hip scan_level_planar8).
+    for (int i = 2; i < 4; i++) {
+        const double *r = d.bodies[i].rotation;
+        if (!(r[2] == 0 && r[5] == 0 && r[6] == 0 && r[7] == 0 && r[8] == 1 && r[0] == r[4] && r[1] == -r[3])) {
+            why = "body " + std::to_string(i) + " placement must be a rotation about z";
+            return MPPI_ERR_UNSUPPORTED;
+        }
+    }
     if (d.end_effector.parent != FR_EE_PARENT || d.arm_mount.parent != FR_AM_PARENT) {
         why = "end-effector / arm-mount frame parents do not match the FrankaRidgeback topology";
         return MPPI_ERR_UNSUPPORTED;

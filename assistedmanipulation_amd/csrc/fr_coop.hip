@@ -984,6 +984,28 @@ __device__ __forceinline__ void scan_level2(double *D, double *p)
     }
 }
 
+// The scan's last level (row_shr 8) for this robot: what lanes 8..11 compose with is the world pose of
+// bodies 0..3 (the planar base and panda_joint1), which is a rotation about z and a translation
+// (check_topology rejects any model where it is not).  So only (cos - 1, sin) of that rotation and
+// its translation travel - 5 doubles (10 moves) instead of 9 - and the product takes 19 operations
+// instead of 43: (I + Dw) (I + D) = I + D + Dw + Dw D with Dw = [[dc, -s, 0], [s, dc, 0], [0, 0, 0]].
+// Lanes 0..7 receive zeros, the identity.  (The partner's R11, -R01 are taken as its R00, R10: equal
+// for a z rotation up to the last bit of the scan's rounding.)
+__device__ __forceinline__ void scan_level_planar8(double *D, double *p)
+{
+    const double dc = shr<8>(D[0]), sn = shr<8>(D[3]);
+    const double pw0 = shr<8>(p[0]), pw1 = shr<8>(p[1]), pw2 = shr<8>(p[2]);
+    const double d00 = D[0], d01 = D[1], d10 = D[3], d11 = D[4];
+    D[0] = __builtin_fma(dc, d00, __builtin_fma(-sn, d10, d00 + dc));
+    D[1] = __builtin_fma(dc, d01, __builtin_fma(-sn, d11, d01 - sn));
+    D[3] = __builtin_fma(sn, d00, __builtin_fma(dc, d10, d10 + sn));
+    D[4] = __builtin_fma(sn, d01, __builtin_fma(dc, d11, d11 + dc));
+    const double p0 = p[0], p1 = p[1];
+    p[0] = __builtin_fma(dc, p0, __builtin_fma(-sn, p1, p0 + pw0));
+    p[1] = __builtin_fma(sn, p0, __builtin_fma(dc, p1, p1 + pw1));
+    p[2] = p[2] + pw2;
+}
+
 // Packed upper-triangle index of a symmetric 6x6.
 __host__ __device__ constexpr int pidx(int r, int c)
 {
@@ -1134,7 +1156,11 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     scan_level2<1>(D, p);
     scan_level2<2>(D, p);
     scan_level2<4>(D, p);
+#ifdef FK_SCAN8
     scan_level2<8>(D, p);
+#else
+    scan_level_planar8(D, p);
+#endif
 #endif
     delta_col2(D);
     FKSTAMP(1, p[2])

@@ -350,22 +350,18 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
 #endif
     double *Lst = Leps;
     const int G = nb * HC, np = (s_last && !early) ? G + nb : 0, n = np + S;
-    int wt = 0;
-    double oc = 0.0;
-    if (s_last) {   // issued with the batch (their own trips otherwise)
-        wt = __hip_atomic_load(&a.status->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        oc = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
-    }
-    for (int base = t; base < n; base += PT * SB) {
+    // with the batch, unconditionally (a branch or a loop header here makes their wait a trip)
+    const int wt = __hip_atomic_load(&a.status->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double oc = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
+    // the partials are one array (tpart = gpart + G, launch_pm_update checks), so each load's source
+    // is a select of two bases, not a branch around each load
+    const double *bp = a.gpart, *bk = a.cost + 2 - np;
+    auto stage = [&](int base) {
         double v[SB];
 #pragma unroll
         for (int u = 0; u < SB; u++) {
             const int j = min(base + u * PT, n - 1);
-#ifdef PM_STAGE_PLAIN
-            v[u] = *(j < G && j < np ? a.gpart + j : j < np ? a.tpart + (j - G) : a.cost + 2 + (j - np));
-#else
-            v[u] = ld_sc1(j < G && j < np ? a.gpart + j : j < np ? a.tpart + (j - G) : a.cost + 2 + (j - np));
-#endif
+            v[u] = ld_sc1((j < np ? bp : bk) + j);
         }
 #pragma unroll
         for (int u = 0; u < SB; u++) {
@@ -373,7 +369,9 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             if (j < np) Lst[j] = v[u];
             else if (j < n) Lkey[j - np] = rank_key(v[u]);
         }
-    }
+    };
+    stage(t);   // the usual sizes: one batch, straight-line
+    for (int base = t + PT * SB; base < n; base += PT * SB) stage(base);
     __syncthreads();
     stamp(6);
     if (s_last) {
@@ -496,6 +494,7 @@ hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s)
     const int PR = pm_fused_rows(a.R, a.H);
     const unsigned nb = (unsigned)((a.R + PR - 1) / PR);
     if (nb != a.nblocks) return hipErrorInvalidValue;   // the barrier and ticket targets assume it
+    if (a.tpart != a.gpart + (size_t)nb * a.H * PC) return hipErrorInvalidValue;   // the finisher's staging
     const size_t lds = pm_fused_lds_bytes(a.R, a.H);
     if (PR == 16)
         hipLaunchKernelGGL(pm_update_kernel<16>, dim3(nb), dim3(PT), lds, s, a);
