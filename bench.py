@@ -59,6 +59,7 @@ BYTES_REC = 336.0
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
 PMC_JSON = os.path.join(HERE, "profiles", "r03g_pmc_rollout.json")
 PMC_WG_JSON = os.path.join(HERE, "profiles", "r03g_pmc_weights.json")   # weights_gradient_kernel's traffic
+PMC_PM_JSON = os.path.join(HERE, "profiles", "r04", "pmc_pm.json")      # pm_update_kernel's traffic
 
 
 def recorded_label(path):
@@ -355,6 +356,11 @@ def run(args, world, rank, local_rank, dist):
                     "launch_us": dyn_ms * 1e3}
         roofline["frac"] = roofline["achieved"] / roofline["peak"]
         roofline["traffic"] = None
+        if fused and os.path.exists(PMC_PM_JSON) and world == 1 and default_workload:
+            with open(PMC_PM_JSON) as f:
+                roofline["traffic"] = json.load(f)["traffic_bytes"]
+            roofline["traffic_unit"] = "HBM bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            roofline["traffic_source"] = recorded_label(PMC_PM_JSON)
         survey_bytes = BYTES_SURVEY_PM
     else:
         lane = info["cooperative"] == 0   # MPPI_FR_KERNEL=lane A/B: the fused one-lane-per-rollout kernel
