@@ -129,3 +129,12 @@ def test_create_rejects_unsupported_models():
     dyn = am.FrankaRidgebackDynamics()
     dyn.model.bodies[1].rotation[1] = 1e-3   # the solve takes the base joints' axes as world x / y
     assert _create(dyn=dyn) is None and "must be unrotated" in _err()
+    for i in (2, 3):   # the FK scan's planar last level (fr_coop.hip scan_level_planar8)
+        dyn = am.FrankaRidgebackDynamics()
+        dyn.model.bodies[i].rotation[5] = 1e-3
+        assert _create(dyn=dyn) is None and "rotation about z" in _err()
+    dyn = am.FrankaRidgebackDynamics()   # a rotation about z is accepted
+    c, s = np.cos(0.3), np.sin(0.3)
+    for k, v in enumerate((c, -s, 0.0, s, c, 0.0, 0.0, 0.0, 1.0)):
+        dyn.model.bodies[3].rotation[k] = v
+    assert "rotation about z" not in (_err() if _create(dyn=dyn) is None else "")
