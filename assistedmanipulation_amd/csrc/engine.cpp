@@ -32,6 +32,26 @@
 using namespace mppi_eng;
 
 namespace {
+EnvSwitches g_env;
+}
+
+namespace mppi_eng {
+const EnvSwitches &env_switches() { return g_env; }
+void env_switches_refresh()
+{
+    auto is = [](const char *name, char c) { const char *e = std::getenv(name); return e && e[0] == c; };
+    g_env.draw_ahead_off = is("MPPI_DRAW_AHEAD", '0');
+    g_env.tail_draws_off = is("MPPI_TAIL_DRAWS", '0');
+    g_env.fuse_sample = is("MPPI_FUSE_SAMPLE", '1');
+    g_env.epilogue = is("MPPI_EPILOGUE", '1');
+    g_env.pm_fused_off = is("MPPI_PM_FUSED", '0');
+    g_env.costs_in_launch_off = is("MPPI_COSTS_IN_LAUNCH", '0');
+    g_env.handover_off = is("MPPI_HANDOVER", '0');
+    g_env.split_off = is("MPPI_SPLIT", '0');
+}
+}  // namespace mppi_eng
+
+namespace {
 
 std::string g_last_error;
 
@@ -521,8 +541,7 @@ bool use_coop(const mppi_handle *h)
 // turns it off (A/B).
 static bool draw_ahead_possible(const mppi_handle *h)
 {
-    const char *e = std::getenv("MPPI_DRAW_AHEAD");
-    if (e && e[0] == '0') return false;
+    if (env_switches().draw_ahead_off) return false;
     return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C && h->tdiag &&
            h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count);
 }
@@ -530,14 +549,12 @@ static bool draw_ahead_possible(const mppi_handle *h)
 // MPPI_TAIL_DRAWS=0: the next update's draws all in rank_draw_kernel behind the publish (A/B)
 static bool tail_draws_disabled()
 {
-    const char *e = std::getenv("MPPI_TAIL_DRAWS");   // per update: tests switch it in-process
-    return e && e[0] == '0';
+    return env_switches().tail_draws_off;
 }
 
 bool fuse_sampling(const mppi_handle *h)
 {
-    const char *e = std::getenv("MPPI_FUSE_SAMPLE");   // per update: tests switch it in-process
-    return e && e[0] == '1' && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
+    return env_switches().fuse_sample && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
            fr_coop_update_fusable(h->count);
 }
 
@@ -857,6 +874,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     mppi_handle *h = nullptr;
     if (!cfg || !dyn || !cost || !out) return fail(nullptr, MPPI_ERR_INVALID, "null argument");
     *out = nullptr;
+    env_switches_refresh();   // the A/B switches, as the environment holds them now
     const int64_t Cd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 3 : (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK ? FR_C : -1);
     const int64_t Xd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 6 : FR_X;
     const bool fr_cost = cost->kind == MPPI_COST_ASSISTED_MANIPULATION || cost->kind == MPPI_COST_TRACK_POINT;
@@ -1105,7 +1123,7 @@ void mppi_destroy(mppi_handle *h)
         std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
                      (long long)h->pm_stamp_n);
         static const char *names[PM_STAMPS] = {"entry", "sampled", "rolled", "barrier", "partials", "ticket",
-                                               "staged", "stored", "published", "ranked", "end"};
+                                               "staged", "stored", "published", "ranked", "end", "costs"};
         for (int i = 0; i < PM_STAMPS; i++) std::fprintf(stderr, " %s %.2f", names[i], h->pm_stamp_sum[(size_t)i] / (double)h->pm_stamp_n);
         std::fprintf(stderr, "\n");
     }
@@ -1536,8 +1554,7 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
 // DESIGN.md §5), so the default keeps the three launches
 static bool epilogue_wanted(const mppi_handle *h)
 {
-    const char *e = std::getenv("MPPI_EPILOGUE");
-    if (!e || e[0] != '1') return false;
+    if (!env_switches().epilogue) return false;
     return h->d_ep_sync && !sharded(h) && h->sg_window == 0 && h->timing < 2 && !h->graph_mode && !h->graph_dry &&
            draw_ahead_possible(h) && !h->d_trace;
 }
@@ -2136,8 +2153,7 @@ mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count)
 // transform, unsharded, no smoothing, timing off or level 1 (MPPI_PM_FUSED=0: the five launches)
 static bool pm_fused_eligible(const mppi_handle *h)
 {
-    const char *e = std::getenv("MPPI_PM_FUSED");
-    if (e && e[0] == '0') return false;
+    if (env_switches().pm_fused_off) return false;
     return h->dyn_kind == MPPI_DYNAMICS_POINT_MASS && h->d_pm_sync && h->noise_source == MPPI_NOISE_DEVICE_PHILOX &&
            h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->host_trace && !h->d_trace;
 }

@@ -2836,7 +2836,9 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
         cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
+#ifndef NO_EPILOGUE
     if (a.epilogue) epilogue<64 * XW>(a, Lcs, Lflag);   // every wave; Lcs and Lflag are free now
+#endif
 }
 
 namespace mppi_eng {
@@ -2896,29 +2898,16 @@ hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, doub
 
 // The objective inside the update launch (launch_costs); MPPI_COSTS_IN_LAUNCH=0 keeps the
 // separate fr_step_cost_kernel (A/B)
-static bool costs_in_launch_enabled()
-{
-    const char *e = getenv("MPPI_COSTS_IN_LAUNCH");   // per update: tests switch it in-process
-    return !(e && e[0] == '0');
-}
+static bool costs_in_launch_enabled() { return !env_switches().costs_in_launch_off; }
 
 bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
 
 // The relay in fr_coop_x_kernel (relay_stage, the default); MPPI_HANDOVER=0 leaves the rows left
-// over on wave 4 for the whole horizon, beside main wave 0 (A/B; read per update: tests switch it
-// in-process)
-static bool handover_enabled()
-{
-    const char *e = getenv("MPPI_HANDOVER");
-    return !(e && e[0] == '0');
-}
+// over on wave 4 for the whole horizon, beside main wave 0 (A/B)
+static bool handover_enabled() { return !env_switches().handover_off; }
 
-// MPPI_SPLIT=0: rows just past two waves per SIMD run as one-wave workgroups (A/B; read per update)
-static bool split_disabled()
-{
-    const char *e = getenv("MPPI_SPLIT");
-    return e && e[0] == '0';
-}
+// MPPI_SPLIT=0: rows just past two waves per SIMD run as one-wave workgroups (A/B)
+static bool split_disabled() { return env_switches().split_off; }
 
 // Whether `count` rows run as two fr_coop_x_kernel launches (launch_fr_coop_update): one-wave
 // workgroups hold two waves per SIMD, 32 rows per CU and round (8192 on 256 CUs), and a count just

@@ -330,6 +330,13 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent
 bool fr_coop_update_fusable(int64_t count);
 bool fr_coop_update_split(int64_t count);   // the two-launch case of launch_fr_coop_update
 bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
+// A/B switches from the environment, read once per mppi_create (tests set them before creating a
+// handle) instead of by getenv on every update (~80 ns each on the host's path between updates)
+struct EnvSwitches {
+    bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off;
+};
+const EnvSwitches &env_switches();
+void env_switches_refresh();
 // Whether a pending filter() folds into the update launch of `count` rows with the objective in
 // the launch (fr_coop_x_kernel, one launch or the split's two): the hipGraph path's launch shape
 bool fr_coop_update_folds(int64_t count, int H);
@@ -411,9 +418,9 @@ struct PmFusedArgs {
     const double *fx0;          // its state (x0_opt as the previous launch left it)
     uint64_t *stamps;           // diagnostics (MPPI_PM_STAMPS=1): [nblocks][PM_STAMPS] s_memrealtime, or null
 };
-// entry, sampled, rolled out, barrier passed, partials stored, ticket taken, staged, (finisher:)
-// stored, published, ranked, end
-constexpr int PM_STAMPS = 11;
+// entry, sampled, rolled out (costs folded into the statistics), barrier passed, partials stored,
+// ticket taken, staged, (finisher:) stored, published, ranked, end, costs computed
+constexpr int PM_STAMPS = 12;
 bool pm_fused_fits(int64_t R, int H);
 size_t pm_fused_lds_bytes(int64_t R, int H);
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);

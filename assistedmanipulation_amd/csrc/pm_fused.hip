@@ -23,8 +23,9 @@
 //            update's keep-best) and the next update's Philox draws of its rollouts.
 //
 // filter() (mppi.cpp:450-479) of the published U* is left pending, as the cooperative rollout
-// launch leaves it: the next launch runs it on block 0's second wave beside that block's rollouts
-// (free: a SIMD that was idle), or a read of the optimal cost runs it first (wait_optimal).
+// launch leaves it: the next launch runs it at the end of block 0's tail, from the U* and state it
+// copied at entry (behind the publish, off the update's chain), or a read of the optimal cost runs
+// it first (wait_optimal).
 //
 // Cross-block hand-offs follow MI355X_MICROARCH.md's measured forms: payloads stored sc1
 // (write-through) and drained with vmcnt(0) before an agent-scope atomic add; readers poll with
@@ -163,6 +164,8 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     uint64_t *Lkey = reinterpret_cast<uint64_t *>(Le + PR);
     double *Leps = reinterpret_cast<double *>(Lkey + S);
     int *Lcnt = reinterpret_cast<int *>(Leps + pm_region(PR, HC, nb));
+    // the previous update's U* [HC] and state [6] for the folded filter()
+    double *LUf = reinterpret_cast<double *>(Lcnt + (QD - 1) * PR);
     __shared__ int s_last;
     const int64_t r0 = (int64_t)b * PR;
     const SampleParams &P = a.sp;
@@ -254,16 +257,26 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     if (t < H) Lgm[t] = gm_t;
     for (int k = t + PT; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
     if (b == 0 && t < a.X) a.x0_out[t] = a.x0v[t];
+    // the previous update's filter() (mppi.cpp:450-479), which its launch left pending, runs in this
+    // block's tail: its inputs are taken now, before this launch's finisher rewrites them - the U*
+    // it published, its state (x0_opt) and whether it threw (then no filter)
+    const bool fold = b == 0 && a.fold_filter && !a.status->all_nan && !a.status->sg_error;
+    if (fold)
+        for (int i = t; i < HC; i += PT) LUf[i] = a.U[i];
+    const double fx = (fold && t < 6) ? a.fx0[t] : 0.0;
+    if (fold && t < 6) LUf[HC + t] = fx;
     __syncthreads();
     stamp(1);
     const int64_t gr = r0 + l;   // the rollout wave's lane l
-    if (w == 0) {   // rollouts (mppi.cpp:272-342): one lane per rollout
-        const bool mine = l < PR && gr < a.R;
-        double J = NAN;
-        if (mine) {
-            J = pm_rollout(a, a.x0v, Lus, Lgm, Leps + l * ES, false);
-            st_sc1(a.cost + gr, J);   // read by every block's rank (tail)
-        }
+    const bool mine = w == 0 && l < PR && gr < a.R;
+    double J = NAN;
+    // rollouts (mppi.cpp:272-342): one lane per rollout through the horizon.  (Splitting the state
+    // chain from the step costs - the positions through LDS, the costs by all threads - measured
+    // slower: 28.7 against 27.6 us per update, profiles/r04/pm_split_ab/.)
+    if (mine) J = pm_rollout(a, a.x0v, Lus, Lgm, Leps + l * ES, false);
+    stamp(11);
+    if (w == 0) {
+        if (mine) st_sc1(a.cost + gr, J);   // read by every block's rank (tail)
         if (l < PR) Lcost[l] = J;
         // the block's min / max / count, then one exact key atomic each into CostStats slot b % 64
         const bool ok = mine && !isnan(J);
@@ -278,15 +291,6 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             atomicAdd(&a.stats->count[32 * slot], (unsigned)n);
         }
         __builtin_amdgcn_s_waitcnt(0);   // the cost stores and the atomics have left this wave
-    } else if (w == 1 && b == 0 && a.fold_filter && l == 0) {
-        // the previous update's filter() (mppi.cpp:450-479), which its launch left pending: the cost
-        // of the U* it published (not yet rewritten: this launch's finisher writes it after the
-        // barrier, which this block reaches after this) from its state; none when it threw
-        const Status *st = a.status;
-        if (!st->all_nan && !st->sg_error) {
-            st_sc1(a.opt_cost, pm_rollout(a, a.fx0, a.U, Lgm, nullptr, true));
-            __builtin_amdgcn_s_waitcnt(0);   // read by the finisher (its host block's optimal cost)
-        }
     }
     __syncthreads();
     stamp(2);
@@ -352,7 +356,6 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     const int G = nb * HC, np = (s_last && !early) ? G + nb : 0, n = np + S;
     // with the batch, unconditionally (a branch or a loop header here makes their wait a trip)
     const int wt = __hip_atomic_load(&a.status->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double oc = ld_sc1(a.opt_cost);   // the previous update's filter(), when folded here
     // the partials are one array (tpart = gpart + G, launch_pm_update checks), so each load's source
     // is a select of two bases, not a branch around each load
     const double *bp = a.gpart, *bk = a.cost + 2 - np;
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
                 for (int i = 1; i < GRAD_SPLIT; i++) st->tsplit[i] = 0.0;
             }
             st->sg_error = wt != 0;   // "the update threw": no filter() (as the finish kernels)
-            a.out[HC + 0] = oc;
+            a.out[HC + 0] = 0.0;      // (filter()'s cost is read behind the stream: wait_optimal)
             a.out[HC + 1] = (double)all_nan;
             a.out[HC + 2] = (double)early;
             a.out[HC + 3] = 0.0;
@@ -460,6 +463,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             for (int c = 0; c < PC; c++) o[c] = e[c];
         }
     }
+    if (fold && t == 0) *a.opt_cost = pm_rollout(a, LUf + HC, LUf, Lgm, nullptr, true);
     stamp(10);
 }
 
@@ -469,13 +473,16 @@ static size_t lds_bytes(int PR, int64_t R, int H)
 {
     const int HC = H * PC;
     const int64_t nb = (R + PR - 1) / PR;
-    return (size_t)((HC + H + 2 * PR + (R - 2) + pm_region(PR, HC, nb)) * 8 + (PT / PR - 1) * PR * 4);
+    return (size_t)((HC + H + 2 * PR + (R - 2) + pm_region(PR, HC, nb) + HC + 6) * 8 + (PT / PR - 1) * PR * 4);
 }
 
 int pm_fused_rows(int64_t R, int H)
 {
     if (R < 4 || H < 1 || R > PM_FUSED_MAX_R) return 0;
-    for (int PR = 16; PR <= 64; PR *= 2)
+#ifndef PM_MIN_ROWS
+#define PM_MIN_ROWS 16
+#endif
+    for (int PR = PM_MIN_ROWS; PR <= 64; PR *= 2)
         if ((R + PR - 1) / PR <= PM_FUSED_MAX_BLOCKS && lds_bytes(PR, R, H) <= 150 * 1024) return PR;
     return 0;
 }
