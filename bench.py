@@ -57,8 +57,8 @@ BYTES_SURVEY_PM = 2 * 3 * 8.0     # 48 B (point mass, C = 3)
 BYTES_EPS_FR = 96.0
 BYTES_REC = 336.0
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
-PMC_JSON = os.path.join(HERE, "profiles", "r03g_pmc_rollout.json")
-PMC_WG_JSON = os.path.join(HERE, "profiles", "r03g_pmc_weights.json")   # weights_gradient_kernel's traffic
+PMC_JSON = os.path.join(HERE, "profiles", "r04", "pmc_rollout.json")
+PMC_WG_JSON = os.path.join(HERE, "profiles", "r04", "pmc_weights.json")   # weights_gradient_kernel's traffic
 PMC_PM_JSON = os.path.join(HERE, "profiles", "r04", "pmc_pm.json")      # pm_update_kernel's traffic
 
 
