@@ -218,6 +218,7 @@ struct mppi_handle {
     int64_t pm_stamp_n = 0;
     // optimise() and finish() in the rollout launch's epilogue (fr_coop.hip epilogue)
     unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
+    EpArgs *d_ep_args = nullptr, *h_ep_args = nullptr;   // the epilogue's arguments (device, pinned staging)
     unsigned ep_total = 0;           // their value after the last epilogue launch
     bool ep_ran = false;             // this update's rollout launch ran the epilogue
     uint64_t *d_ep_stamps = nullptr; // MPPI_EP_STAMPS=1: the epilogue's phase stamps per workgroup
@@ -1048,6 +1049,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
         CREATE_TRY(dalloc(h, &h->d_ep_sync, 2));
+        CREATE_TRY(dalloc(h, &h->d_ep_args, 1));
+        CREATE_TRY(hipHostMalloc((void **)&h->h_ep_args, sizeof(EpArgs), hipHostMallocDefault));
         const char *es = std::getenv("MPPI_EP_STAMPS");
         if (es && es[0] == '1') {
             h->ep_stamp_groups = (unsigned)std::max<int64_t>(1, (h->R + 15) / 16);
@@ -1139,6 +1142,7 @@ void mppi_destroy(mppi_handle *h)
     if (h->graph) (void)hipGraphDestroy(h->graph);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
+    if (h->h_ep_args) (void)hipHostFree(h->h_ep_args);
     if (h->h_opt) (void)hipHostFree(h->h_opt);
     if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
@@ -1704,9 +1708,12 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.ep_sync = h->d_ep_sync;
             a.ep_target = h->ep_total;
             a.ep_stamps = h->d_ep_stamps;
-            a.wg = wgrad_args(h);
-            a.fin = finish_args(h);   // its sequence: publish_seq + 1, as phase 3 publishes it
-            a.fin.rank_n = h->R;      // draw_ahead_possible: S <= RANK_TILED_MAX, rank_draw_kernel's tiles
+            EpArgs &ea = *h->h_ep_args;   // (the previous update's copy has run: its launch published)
+            ea.wg = wgrad_args(h);
+            ea.fin = finish_args(h);   // its sequence: publish_seq + 1, as phase 3 publishes it
+            ea.fin.rank_n = h->R;      // draw_ahead_possible: S <= RANK_TILED_MAX, rank_draw_kernel's tiles
+            HIP_TRY(hipMemcpyAsync(h->d_ep_args, h->h_ep_args, sizeof(EpArgs), hipMemcpyHostToDevice, h->stream));
+            a.ep = h->d_ep_args;
             // a filter() launched by itself on the side stream reads the d_U / d_x0_opt the epilogue rewrites
             if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
         }

@@ -2476,12 +2476,12 @@ __device__ __forceinline__ void ep_sti(int *p, int v) { __hip_atomic_store(p, v,
 __device__ __forceinline__ bool ep_kept(const FrRolloutArgs &fa, int k, int64_t rr)
 {
     const SampleArgs &sa = fa.samp;
-    const int64_t g = fa.wg.begin + rr;
+    const int64_t g = fa.ep->wg.begin + rr;
     return g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
 }
 __device__ __forceinline__ const double *ep_eps_ptr(const FrRolloutArgs &fa, int k, int64_t rr)
 {
-    return fa.wg.noise + ((int64_t)k * fa.wg.Rpad + rr) * FR_C;
+    return fa.ep->wg.noise + ((int64_t)k * fa.ep->wg.Rpad + rr) * FR_C;
 }
 __device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, int k, int64_t rr, double *e)
 {
@@ -2501,7 +2501,7 @@ struct EpPre {
 };
 __device__ __forceinline__ void ep_unit_range(const FrRolloutArgs &fa, int u, int64_t &r0, int64_t &r1, int &k, int &s)
 {
-    const WGradArgs &a = fa.wg;
+    const WGradArgs &a = fa.ep->wg;
     const bool has = u >= 0;
     k = has ? u % a.H : 0;
     s = has ? u / a.H : 0;
@@ -2530,7 +2530,7 @@ __device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, int u, int t
 // on 256 threads t, unsharded with the objective's statistics; u < 0: no unit (the barrier only)
 __device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, double *red, double *ssum, EpPre &p)
 {
-    const WGradArgs &a = fa.wg;
+    const WGradArgs &a = fa.ep->wg;
     constexpr int CP = FR_C;
     const int rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
@@ -2638,7 +2638,7 @@ __device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, d
 template <int NT>
 __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
 {
-    const FinishArgs &a = fa.fin;
+    const FinishArgs &a = fa.ep->fin;
     const SampleArgs &sa = fa.samp;
     const int HC = a.H * a.C;
     Status *st = const_cast<Status *>(a.status);
@@ -2721,7 +2721,7 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
 {
     const int t = threadIdx.x;
     const int groups = gridDim.x, half = t >> 8, ht = t & 255;
-    const int nunits = a.wg.H * GRAD_SPLIT, per = 2 * groups;
+    const int nunits = a.ep->wg.H * GRAD_SPLIT, per = 2 * groups;
     EpPre pre;   // the first pass's eps, loaded while the barrier waits
     {
         const int u = half * groups + (int)blockIdx.x;

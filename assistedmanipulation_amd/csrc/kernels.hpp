@@ -117,6 +117,10 @@ struct FinishArgs {
     double *wait_local;
 };
 
+struct EpArgs {
+    WGradArgs wg;
+    FinishArgs fin;
+};
 constexpr int EP_STAMPS = 4;   // epilogue stamps: barrier arrival, barrier passed, units stored, published (finisher)
 struct FrRolloutArgs {
     const DevModel *model;
@@ -177,8 +181,10 @@ struct FrRolloutArgs {
     unsigned *ep_sync;            // [2] barrier and ticket counters (monotonic)
     unsigned ep_target;           // their value once every workgroup of this launch has added 1
     uint64_t *ep_stamps;          // diagnostics (MPPI_EP_STAMPS=1): [groups][EP_STAMPS] s_memrealtime, or null
-    WGradArgs wg;
-    FinishArgs fin;
+    // the epilogue's weights_gradient_kernel and finish_flat_kernel arguments, in device memory (the
+    // launch's kernel arguments stay small: the launch call's host cost grows with their size,
+    // ~1.8 us more for 1144 bytes than for 16, tools/probe/launch_cost.hip)
+    const EpArgs *ep;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -387,7 +393,7 @@ struct PmFusedArgs {
     const StepConst *steps;     // [H] gamma_k
     SampleParams sp;
     double tdv[3];              // diagonal noise transform
-    double x0v[MAX_X];          // the update's state by value
+    double x0v[8];              // the update's state by value (X = 6)
     double *x0_out;             // [X] the rollout state (block 0)
     int X;
     int H;

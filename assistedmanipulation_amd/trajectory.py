@@ -288,9 +288,12 @@ class Trajectory:
     def update(self, state, time):
         """Trajectory::update (mppi.cpp:154-187)."""
         buf = self._state_buf   # one contiguous buffer and its pointer, built once: the update
-        if np.size(state) != self.X:   # path is latency-bound (microseconds per call)
-            raise ValueError("state must have %d entries, got %d" % (self.X, np.size(state)))
-        np.copyto(buf, np.reshape(state, -1))
+        if type(state) is np.ndarray and state.shape == buf.shape:   # path is latency-bound: the usual
+            buf[...] = state                                         # case in one copy (~0.7 us, not ~2.6)
+        else:
+            if np.size(state) != self.X:
+                raise ValueError("state must have %d entries, got %d" % (self.X, np.size(state)))
+            np.copyto(buf, np.reshape(state, -1))
         st = self._L.mppi_update(self._h, self._state_ptr, float(time))
         if st != abi.MPPI_OK:
             self._check(st)
