@@ -48,6 +48,7 @@ void env_switches_refresh()
     g_env.costs_in_launch_off = is("MPPI_COSTS_IN_LAUNCH", '0');
     g_env.handover_off = is("MPPI_HANDOVER", '0');
     g_env.split_off = is("MPPI_SPLIT", '0');
+    g_env.relay2_off = is("MPPI_RELAY2", '0');
 }
 }  // namespace mppi_eng
 
@@ -219,6 +220,9 @@ struct mppi_handle {
     // optimise() and finish() in the rollout launch's epilogue (fr_coop.hip epilogue)
     unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
     EpArgs *d_ep_args = nullptr, *h_ep_args = nullptr;   // the epilogue's arguments (device, pinned staging)
+    double *d_relay_buf = nullptr;     // relay2: the relay's hand-over between its two workgroups
+    unsigned *d_relay_flag = nullptr;  // [2] monotonic flags (epochs)
+    unsigned relay_epoch = 0;
     unsigned ep_total = 0;           // their value after the last epilogue launch
     bool ep_ran = false;             // this update's rollout launch ran the epilogue
     uint64_t *d_ep_stamps = nullptr; // MPPI_EP_STAMPS=1: the epilogue's phase stamps per workgroup
@@ -1050,6 +1054,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
         CREATE_TRY(dalloc(h, &h->d_ep_sync, 2));
         CREATE_TRY(dalloc(h, &h->d_ep_args, 1));
+        CREATE_TRY(dalloc(h, &h->d_relay_buf, 64 * 3 + 8));
+        CREATE_TRY(dalloc(h, &h->d_relay_flag, 2));
         CREATE_TRY(hipHostMalloc((void **)&h->h_ep_args, sizeof(EpArgs), hipHostMallocDefault));
         const char *es = std::getenv("MPPI_EP_STAMPS");
         if (es && es[0] == '1') {
@@ -1697,6 +1703,11 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.fsteps = h->opt_steps;
             a.fcost = h->d_opt;
             a.frec = h->d_rec_opt;
+        }
+        if (!h->graph_mode && !h->graph_dry && !env_switches().relay2_off) {   // (launch_fr_coop_update decides)
+            a.relay_buf = h->d_relay_buf;
+            a.relay_flag = h->d_relay_flag;
+            a.relay_epoch = ++h->relay_epoch;
         }
         bool folded = false, costs_done = false, tail = false;
         CoopTail ct;

@@ -2103,10 +2103,32 @@ __device__ __forceinline__ int lds_read(int *w)
 {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4)
+// relay2: the workgroup that carries the relay's second half (block 0 keeps the first); any block
+// would do (only write-through data crosses), this one shares block 0's XCD under round-robin
+// dispatch
+constexpr int RELAY_PARTNER = 8;
+#ifndef RELAY2   // measured slower: compiled in only with -DRELAY2
+__device__ __forceinline__ bool relay_partner(const FrRolloutArgs &) { return false; }
+#define RELAY2_ON(a) false
+#else
+__device__ __forceinline__ bool relay_partner(const FrRolloutArgs &a) { return a.relay2 && blockIdx.x == RELAY_PARTNER; }
+#define RELAY2_ON(a) ((a).relay2 != 0)
+#endif
+// relay2's split: the first chunk boundary at or below half the horizon
+__host__ __device__ inline int relay_split(int H) { return (((H + CH - 1) / CH) / 2) * CH; }
+// the relay group's chunks [c0, c1) in this workgroup (relay2 splits them at the split)
+__device__ __forceinline__ void relay_chunks(const FrRolloutArgs &a, int &c0, int &c1)
+{
+    const int nch = (a.H + CH - 1) / CH;
+    c0 = relay_partner(a) ? relay_split(a.H) / CH : 0;
+    c1 = (RELAY2_ON(a) && !relay_partner(a)) ? relay_split(a.H) / CH : nch;
+}
+// first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4: block
+// 0's in the relay2 partner)
 __device__ __forceinline__ int64_t group_row0(const FrRolloutArgs &a, int g)
 {
-    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
+    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE
+                 : a.xbase + (int64_t)(relay_partner(a) ? 0 : blockIdx.x) * ROWS_PER_WAVE;
 }
 // whether chunk c of group g can be read: its records are complete
 __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
@@ -2122,7 +2144,10 @@ template <int CK, bool EN>
 __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c, int lane, const double *Lmodel, double *Lcs,
                                           int *Lq)
 {
-    const int H = a.H, nch = (H + CH - 1) / CH;
+    const int H = a.H;
+    int rc0 = 0, rc1 = (H + CH - 1) / CH;
+    if (g == 4) relay_chunks(a, rc0, rc1);
+    const int nch = rc1 - rc0;   // the group's chunks in this workgroup
     const int i = lane >> 4, k = c * CH + (lane & 15);
     const int64_t lr0 = group_row0(a, g), lr = lr0 + i;
     const bool rl = row_live(a, lr), live = rl && k < H;
@@ -2137,21 +2162,39 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     const int n = __builtin_amdgcn_readfirstlane(
         __hip_atomic_fetch_add(Lq + Q_DONE + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (n + 1 != nch) return;
+    const bool rfirst = g == 4 && RELAY2_ON(a) && !relay_partner(a), rsecond = g == 4 && relay_partner(a);
+    const int hb = rsecond ? relay_split(H) : 0;
+    if (rsecond) {   // the first half's sums (block 0), in step order: J continues from them
+        int w = 0;
+        while (__hip_atomic_load(a.relay_flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.relay_epoch &&
+               w < WAIT_SPINS) {
+            __builtin_amdgcn_s_sleep(2);
+            w++;
+        }
+        if (w == WAIT_SPINS && lane == 0) note_wait_timeout(a);
+    }
     if (lane < ROWS_PER_WAVE) {
         const int64_t r = lr0 + lane;
         if (row_live(a, r)) {
             const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
-            double J = 0.0;
-            for (int q = 0; q < H; q++) J += cr[q];
-            J = isnan(J) ? (double)NAN : J;
-            if (a.fcost != nullptr && r == a.count) {
+            double J = rsecond ? __hip_atomic_load(a.relay_buf + 64 * 3 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            for (int q = hb; q < (rfirst ? relay_split(H) : H); q++) J += cr[q];
+            if (rfirst) {   // block 0: the sums so far to the partner, which finishes the rows
+                __hip_atomic_store(a.relay_buf + 64 * 3 + lane, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (a.fcost != nullptr && r == a.count) {
+                J = isnan(J) ? (double)NAN : J;
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
             } else {
+                J = isnan(J) ? (double)NAN : J;
                 if (a.epilogue) __hip_atomic_store(a.cost_out + a.begin + r, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 else a.cost_out[a.begin + r] = J;
                 mppi_cost::fold_cost_stats(a.stats, J, r);
             }
         }
+    }
+    if (rfirst) {   // every lane's sum stored (write-through), then the flag
+        __builtin_amdgcn_s_waitcnt(0);
+        if (lane == 0) __hip_atomic_store(a.relay_flag + 1, a.relay_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2163,20 +2206,23 @@ __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int
                                          double *Lcs, int *Lflag, int *Lq)
 {
     const int nch = (a.H + CH - 1) / CH;
+    int rc0, rc1;
+    relay_chunks(a, rc0, rc1);
 #pragma unroll 1
     for (int spin = 0; spin < WAIT_SPINS; spin++) {
         bool left = false, did = false;
 #pragma unroll 1
         for (int d = 0; d < ng && !did; d++) {
             const int g = first + d < ng ? first + d : first + d - ng;
+            const int cend = g == 4 ? rc1 : nch;
             const int c0 = lds_read(Lq + Q_NEXT + g);
-            if (c0 >= nch) continue;
+            if (c0 >= cend) continue;
             left = true;
             if (!chunk_ready(a, g, c0, Lflag, Lq)) continue;
             // every lane executes the add (lane 0 adds 1): no lane-dependent branch around it
             const int c = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_fetch_add(Lq + Q_NEXT + g, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (c >= nch) continue;
+            if (c >= cend) continue;
             int w = 0;
             while (!chunk_ready(a, g, c, Lflag, Lq) && w < WAIT_SPINS) {
                 __builtin_amdgcn_s_sleep(4);
@@ -2212,8 +2258,14 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
-__device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
+// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps, or
+// with relay2 eight stages, four on each side of the split
+__device__ __forceinline__ int relay_step(int r, int H, bool two = false)
+{
+    if (!two) return r >= 4 ? H - 1 : (r * (H - 1)) / 4;
+    const int hb = relay_split(H);
+    return r >= 8 ? H - 1 : r <= 4 ? (r * hb) / 4 : hb + ((r - 4) * (H - 1 - hb)) / 4;
+}
 
 // Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): makes the next
 // update's draws for main wave r's rows (r > 0; wave 0's are left to rank_draw_kernel, as the
@@ -2222,18 +2274,54 @@ __device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 
 // last stage raises the relay's records flag.  Without a.handover wave 4 runs every step itself at
 // the main waves' priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage
 // ran (false: the previous stage never signalled, counted in Status::wait_timeouts).
+// relay2's two crossings, kept out of line so that the relay loop's code is as without them
+__device__ __attribute__((noinline)) bool relay2_receive(const FrRolloutArgs &a, int lane, double *Lst)
+{
+    int i = 0;
+    while (__hip_atomic_load(a.relay_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.relay_epoch && i < (1 << 22)) {
+        __builtin_amdgcn_s_sleep(2);
+        i++;
+    }
+    if (i == (1 << 22)) return false;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+        Lst[3 * lane + c] = __hip_atomic_load(a.relay_buf + 3 * lane + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+__device__ __attribute__((noinline)) void relay2_send(const FrRolloutArgs &a, int lane, const double *Lst)
+{
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+        __hip_atomic_store(a.relay_buf + 3 * lane + c, Lst[3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // (and this stage's records: block 0's half of the chunks)
+    if (lane == 0) __hip_atomic_store(a.relay_flag, a.relay_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// relay2: stages 0..3 run in block 0, 4..7 in RELAY_PARTNER.  Stage 3 writes the lanes' state
+// through to relay_buf and raises relay_flag[0]; stage 4 waits for it (bounded) and resumes from
+// it.  Each side's objective takes its own half of the relay rows' chunks (cost_chunk).
 template <int CK, bool EN>
 __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
                                             const double *Lmodel, const double *Lx0, int *Lflag, int *Lq, double *Lst)
 {
     const int H = a.H;
-    const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
+    const bool two = RELAY2_ON(a), partner = relay_partner(a);
+    const int last = two ? 7 : 3;
+    const int64_t xlr = a.xbase + (int64_t)(partner ? 0 : blockIdx.x) * ROWS_PER_WAVE + (lane >> 4);
     const int wblk = gridDim.x * 4 + blockIdx.x;
     if (!a.handover) {
         coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
     } else {
-        if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
-        if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
+        // the next update's draws for main wave s's rows first (block 0's wave 0 rows are left to
+        // rank_draw_kernel; the partner is an ordinary workgroup for its draws)
+        const int s = partner ? r - 4 : r;
+        if ((partner || r > 0) && a.ahead_noise) group_draws(a, s, lane, Lflag);
+        if (partner && r == 4) {   // the state block 0's stage 3 handed over (bounded)
+            if (!relay2_receive(a, lane, Lst)) {
+                if (lane == 0) note_wait_timeout(a);
+                return false;
+            }
+        } else if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
             int st = 0;
             for (int i = 0; i < (1 << 22) && st < r; i++) {
                 st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -2244,13 +2332,21 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
                 return false;
             }
         }
-        __builtin_amdgcn_s_setprio(3);
-        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H), relay_step(r + 1, H));
+#ifndef RELAY_PRIO
+#define RELAY_PRIO 3   // (A/B builds: 1 = the main waves' own priority)
+#endif
+        __builtin_amdgcn_s_setprio(RELAY_PRIO);
+        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H, two), relay_step(r + 1, H, two));
         __builtin_amdgcn_s_setprio(0);
 #ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
-        if (a.trace && blockIdx.x == 0 && lane == 0) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (a.trace && blockIdx.x == 0 && lane == 0 && r < 4) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
+        if (two && r == 3) {   // across to the partner: the state written through, then the flag
+            relay2_send(a, lane, Lst);
+            if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
+            return true;
+        }
+        if (r < last) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
             // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
             if (!((a.debug & 1) && r == 1))
@@ -2258,8 +2354,8 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
             return true;
         }
     }
-    if (blockIdx.x == 0 && lane == 0)   // write-through: the epilogue's finisher reads this line (sc1)
-        __hip_atomic_store(&const_cast<Status *>(a.status)->handover, a.handover ? relay_step(1, H) : -1, __ATOMIC_RELAXED,
+    if ((partner || blockIdx.x == 0) && lane == 0)   // write-through: the epilogue's finisher reads this line (sc1)
+        __hip_atomic_store(&const_cast<Status *>(a.status)->handover, a.handover ? relay_step(1, H, two) : -1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
     return true;
@@ -2798,8 +2894,10 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (wv < 5) fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
     }
     const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
-    const int ng = xr ? 5 : 4;   // row groups of the objective
-    if (!xr && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
+    const bool xp = relay_partner(a);   // it carries the relay's second half (block 0's rows)
+    const int ng = (xr || xp) ? 5 : 4;   // row groups of the objective
+    if (!(xr || xp) && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
+    if (xp && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = relay_split(a.H) / CH;   // its chunks start at the split
     __syncthreads();
     // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
     const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
@@ -2828,8 +2926,8 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     } else {
         const int s = wv - 4;   // this wave's SIMD
-        const bool relay = xr && (s == 0 || a.handover);
-        if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
+        const bool relay = (xr && (s == 0 || a.handover)) || xp;
+        if (relay) relay_stage<CK, EN>(a, xp ? 4 + s : s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
         if (!cil) return;   // (no epilogue without the objective in the launch)
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
@@ -2986,6 +3084,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
         a.handover = handover_enabled() ? 1 : 0;
         if (!a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
         a.epilogue = 0;   // (two launches: optimise and finish stay separate launches)
+        a.relay2 = 0;
         FrRolloutArgs A = row_slice(a, 0, n0), B = row_slice(a, n0, rest);
         A.fcost = nullptr;   // the previous filter() rides with the rows left over
         A.xbase = n0;
@@ -3018,6 +3117,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
         if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.epilogue = 0;
+        a.relay2 = 0;
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
         a.costs_in_launch = groups > 0 && costs_in_launch_enabled() ? 1 : 0;   // each wave its own rows'
@@ -3043,6 +3143,10 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.epilogue = (a0.epilogue && xrows != 0 && a.costs_in_launch && a.fuse_sample == 2 && a.H * FR_C <= EP_MAXE * 64 * XW &&
                   a.ep_sync != nullptr) ? 1 : 0;
     a.ep_target = a0.ep_target + (a.epilogue ? (unsigned)groups : 0u);
+    // the relay over two workgroups: one relay group (block 0's), a partner past it, the objective
+    // in the launch, at least two chunks (the split is a chunk boundary), no epilogue
+    a.relay2 = (a0.relay_buf != nullptr && a.handover && xrows != 0 && xrows <= ROWS_PER_WAVE && groups > RELAY_PARTNER &&
+                a.costs_in_launch && !a.epilogue && a.H >= 2 * CH && relay_split(a.H) < a.H - 1) ? 1 : 0;
     *tail_drawn = a.ahead_noise != nullptr;
     if (final) *final = a;
     if (x_kernel) *x_kernel = xrows != 0;

@@ -859,7 +859,10 @@ __device__ __forceinline__ double wave_sum(double v) { return mppi_dev::wave_sum
 constexpr int WV = 16;       // waves of the 1024-thread reduction order
 constexpr int WU = 8;        // costs per (virtual) thread and pass
 constexpr int NV = WV / 4;   // virtual waves per real wave
-constexpr int GR = 3;        // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
+#ifndef WG_GR
+#define WG_GR 3
+#endif
+constexpr int GR = WG_GR;     // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
 
 // Large R (R > SM_LARGE_R, configs 4 / 5: every rank weighs all R global costs): recomputing
 // min / max / normaliser over all R in each of the H x GRAD_SPLIT blocks costs O(H R) exps, so

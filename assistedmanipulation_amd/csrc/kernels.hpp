@@ -168,6 +168,13 @@ struct FrRolloutArgs {
     // fr_coop_x_kernel: the fifth wave's rows move to the first of waves 1..3 to end its own rows
     // (fr_coop.hip take_over; MPPI_HANDOVER=0 keeps them on the doubled SIMD)
     int handover;
+    // relay2 (fr_coop_x_kernel): the relay's eight stages over two workgroups, block 0 (stages 0..3,
+    // steps before the split) and block 8 (4..7): the state crosses once, with the first half's
+    // step-cost sums, through relay_buf (write-through) behind relay_flag[0] / [1] == relay_epoch
+    int relay2;
+    unsigned relay_epoch;
+    double *relay_buf;            // [64 * 3] the lanes' (q, qd, E) at the split, then [4] the rows' J so far
+    unsigned *relay_flag;         // [2] monotonic: the state handed over, the first half's sums written
     // sharded over RCCL: the rank's slot R of the cost vector the engine all-reduces, to which every
     // in-launch wait that gives up adds 1 (so every rank's finish kernel sees any rank's), or null
     double *wait_sum;
@@ -339,7 +346,8 @@ bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MP
 // A/B switches from the environment, read once per mppi_create (tests set them before creating a
 // handle) instead of by getenv on every update (~80 ns each on the host's path between updates)
 struct EnvSwitches {
-    bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off;
+    bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off,
+        relay2_off;
 };
 const EnvSwitches &env_switches();
 void env_switches_refresh();
