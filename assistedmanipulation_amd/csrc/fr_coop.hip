@@ -3145,8 +3145,12 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.ep_target = a0.ep_target + (a.epilogue ? (unsigned)groups : 0u);
     // the relay over two workgroups: one relay group (block 0's), a partner past it, the objective
     // in the launch, at least two chunks (the split is a chunk boundary), no epilogue
+#ifdef RELAY2
     a.relay2 = (a0.relay_buf != nullptr && a.handover && xrows != 0 && xrows <= ROWS_PER_WAVE && groups > RELAY_PARTNER &&
                 a.costs_in_launch && !a.epilogue && a.H >= 2 * CH && relay_split(a.H) < a.H - 1) ? 1 : 0;
+#else
+    a.relay2 = 0;
+#endif
     *tail_drawn = a.ahead_noise != nullptr;
     if (final) *final = a;
     if (x_kernel) *x_kernel = xrows != 0;
