@@ -45,6 +45,7 @@ PROTOTYPES = {
     "mppi_update": (C.c_int, [_h, _dp, C.c_double]),
     "mppi_set_graph": (C.c_int, [_h, C.c_int]),
     "mppi_debug_inject": (C.c_int, [_h, C.c_int, C.c_int]),
+    "mppi_debug_folded_cost": (C.c_int, [_h, C.POINTER(C.c_double)]),
     "mppi_graph_updates": (C.c_int, [_h, _i64p]),
     "mppi_update_phase1": (C.c_int, [_h, _dp, C.c_double]),
     "mppi_update_phase2": (C.c_int, [_h]),

@@ -2153,6 +2153,15 @@ mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates)
     return MPPI_OK;
 }
 
+mppi_status mppi_debug_folded_cost(mppi_handle *h, double *cost)
+{
+    if (!h || !cost) return MPPI_ERR_INVALID;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(cost, h->d_opt, sizeof(double), hipMemcpyDeviceToHost));   // no state change
+    return MPPI_OK;
+}
+
 mppi_status mppi_set_graph(mppi_handle *h, int enable)
 {
     if (!h || enable < 0 || enable > 1) return MPPI_ERR_INVALID;

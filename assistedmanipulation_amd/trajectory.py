@@ -435,6 +435,13 @@ class Trajectory:
         rollout launches carry fault bits `fault` (abi.MPPI_DEBUG_*)."""
         self._check(self._L.mppi_debug_inject(self._h, int(fault), int(updates)))
 
+    def debug_folded_cost(self):
+        """The previous update's filter() cost as the last launch folded it (mppi_debug_folded_cost;
+        tests only: no pending filter() is run or waited for)."""
+        v = C.c_double()
+        self._check(self._L.mppi_debug_folded_cost(self._h, C.byref(v)))
+        return v.value
+
     def smoothing_windows(self):
         """(uu, tt, start_idx) of the per-dimension SG windows (SavitzkyGolayFilter::get_windows)."""
         w = self.configuration.smoothing.window

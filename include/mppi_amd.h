@@ -402,6 +402,11 @@ mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
  * stage 2, so the bounded in-launch waits give up and the update must fail (MPPI_ERR_DEVICE). */
 #define MPPI_DEBUG_RELAY_NO_SIGNAL 1
 mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates);
+/* The optimal-rollout cost the device holds now, as the last launch left it, without running or
+ * waiting for a pending filter() (tests only): after an update whose launch folded the previous
+ * update's filter() (MPPI_INFO_FOLDED_FILTER), that filter()'s cost - which mppi_optimal_cost no
+ * longer returns, since it answers for the latest update. */
+mppi_status mppi_debug_folded_cost(mppi_handle *h, double *cost);
 
 /* Savitzky-Golay window state (SavitzkyGolayFilter::get_windows(), filter.hpp): per control
  * dimension the value and time buffers (C x (H + 2w + 1), row per dimension) and start index. */

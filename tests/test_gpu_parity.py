@@ -687,3 +687,22 @@ def test_in_launch_wait_timeout_fails_the_update():
         step_both(dev, orc, x, 0.05 * j, rng, sd)
         assert dev.update_info()["wait_timeouts"] == 0
         assert_update_parity(dev, orc, "after timeout %d" % j)
+
+
+def test_folded_filter_row_against_oracle():
+    """The previous update's filter() as one more row of the rollout launch (fr_coop_x_kernel's
+    folded row, MPPI_INFO_FOLDED_FILTER): read back as the launch left it (mppi_debug_folded_cost,
+    which runs nothing) and checked against the oracle's filter() of the update before, at 1000
+    rollouts (rows left over, so the row rides along).  No optimal-cost read in between."""
+    conf, dev, orc, sd = fr_pair(S=1000, horison=0.64)
+    rng = np.random.default_rng(3)
+    x = am.huddled_state()
+    prev_opt = None
+    for j in range(4):
+        step_both(dev, orc, x, 0.05 * j, rng, sd)
+        info = dev.update_info()
+        assert info["folded_filter"] == (0 if j == 0 else 1), info
+        if prev_opt is not None:
+            folded = dev.debug_folded_cost()
+            assert abs(folded - prev_opt) <= 1e-11 * max(1.0, abs(prev_opt)), (j, folded, prev_opt)
+        prev_opt = orc.optimal_cost()

@@ -95,3 +95,26 @@ def test_fused_update_all_nan_and_recovery():
         info = t.update_info()
         assert info["fused_update"] == 1 and info["wait_timeouts"] == 0, info
         assert np.all(np.isfinite(t.costs()))
+
+
+def test_folded_filter_cost_against_oracle():
+    """filter() (mppi.cpp:450-479) of each update, left pending and folded into the next launch's
+    tail (block 0, from the U* and state it copied at entry): read back as that launch left it
+    (mppi_debug_folded_cost, which runs nothing) and checked against the oracle's filter() of the
+    update before.  No optimal-cost read in between, so every launch folds."""
+    conf, dev = _pm(1024, 0.32)
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, dev.dynamics.descriptor(), dev.cost.descriptor())
+    x = np.zeros(6)
+    prev_costs, prev_noise = np.zeros(dev.R), np.zeros((dev.R, dev.H, dev.C))
+    prev_opt = None
+    for j, tm in enumerate(TIMES):
+        costs, noise = replay_device_draws(dev, orc, x, tm, prev_costs, prev_noise, 20)
+        info = dev.update_info()
+        assert info["fused_update"] == 1 and info["folded_filter"] == (0 if j == 0 else 1), info
+        if prev_opt is not None:
+            folded = dev.debug_folded_cost()
+            assert abs(folded - prev_opt) <= 1e-11 * max(1.0, abs(prev_opt)), (j, folded, prev_opt)
+        prev_opt = orc.optimal_cost()
+        prev_costs, prev_noise = costs, noise
+        x = x + 0.01
