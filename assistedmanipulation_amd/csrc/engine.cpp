@@ -1061,7 +1061,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         if (es && es[0] == '1') {
             h->ep_stamp_groups = (unsigned)std::max<int64_t>(1, (h->R + 15) / 16);
             CREATE_TRY(dalloc(h, &h->d_ep_stamps, (size_t)h->ep_stamp_groups * EP_STAMPS));
-            h->ep_stamp_sum.assign(4, 0.0);
+            h->ep_stamp_sum.assign(9, 0.0);
         }
         CREATE_TRY(launch_fr_body_table(h->d_model, h->d_cost, h->d_table, nullptr));
         CREATE_TRY(hipDeviceSynchronize());
@@ -1128,6 +1128,10 @@ void mppi_destroy(mppi_handle *h)
         std::fprintf(stderr, "epilogue phases (us, mean of %lld): arrivals spread %.2f  barrier release %.2f  units %.2f  "
                              "ticket+finish+publish %.2f\n", (long long)h->ep_stamp_n, h->ep_stamp_sum[0] / h->ep_stamp_n,
                      h->ep_stamp_sum[1] / h->ep_stamp_n, h->ep_stamp_sum[2] / h->ep_stamp_n, h->ep_stamp_sum[3] / h->ep_stamp_n);
+    if (h->ep_stamp_n > 0)
+        std::fprintf(stderr, "epilogue finisher (us): ticket %.2f  loads %.2f  compute+stores %.2f  acknowledged %.2f  flag %.2f\n",
+                     h->ep_stamp_sum[4] / h->ep_stamp_n, h->ep_stamp_sum[5] / h->ep_stamp_n, h->ep_stamp_sum[6] / h->ep_stamp_n,
+                     h->ep_stamp_sum[7] / h->ep_stamp_n, h->ep_stamp_sum[8] / h->ep_stamp_n);
     if (h->pm_stamp_n > 0) {
         std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
                      (long long)h->pm_stamp_n);
@@ -1999,7 +2003,7 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
         std::vector<uint64_t> sv((size_t)h->ep_stamp_groups * EP_STAMPS);
         HIP_TRY(hipStreamSynchronize(h->stream));
         HIP_TRY(hipMemcpy(sv.data(), h->d_ep_stamps, sv.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        uint64_t first = ~0ull, last_arr = 0, pass = 0, stored = 0, pub = 0;
+        uint64_t first = ~0ull, last_arr = 0, pass = 0, stored = 0, pub = 0, fin[4] = {0, 0, 0, 0};
         for (unsigned b = 0; b < h->ep_stamp_groups; b++) {
             const uint64_t *v = &sv[(size_t)b * EP_STAMPS];
             if (!v[0]) continue;
@@ -2008,12 +2012,20 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
             pass = std::max(pass, v[1]);
             stored = std::max(stored, v[2]);
             pub = std::max(pub, v[3]);
+            for (int i = 0; i < 4; i++) fin[i] = std::max(fin[i], v[4 + i]);
         }
         if (last_arr) {
             h->ep_stamp_sum[0] += (double)(last_arr - first) * 0.01;   // spread of the arrivals
             h->ep_stamp_sum[1] += (double)(pass - last_arr) * 0.01;    // barrier release
             h->ep_stamp_sum[2] += (double)(stored - pass) * 0.01;      // units (the weight reduce)
             h->ep_stamp_sum[3] += (double)(pub - stored) * 0.01;       // ticket + finish + publish
+            if (fin[0]) {   // the finisher: ticket, loads, compute + stores issued, stores acknowledged, flag
+                h->ep_stamp_sum[4] += (double)(fin[0] - stored) * 0.01;
+                h->ep_stamp_sum[5] += (double)(fin[1] - fin[0]) * 0.01;
+                h->ep_stamp_sum[6] += (double)(fin[2] - fin[1]) * 0.01;
+                h->ep_stamp_sum[7] += (double)(fin[3] - fin[2]) * 0.01;
+                h->ep_stamp_sum[8] += (double)(pub - fin[3]) * 0.01;
+            }
             h->ep_stamp_n++;
         }
         HIP_TRY(hipMemset(h->d_ep_stamps, 0, sv.size() * sizeof(uint64_t)));

@@ -2565,24 +2565,28 @@ __device__ __forceinline__ double ep_ld(const double *p) { return __hip_atomic_l
 __device__ __forceinline__ void ep_st(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ int ep_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void ep_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// a store to the mapped host block, system scope (write-through to host memory)
+__device__ __forceinline__ void ep_pub(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
 // eps of rollout rr (local) at step k as the rollout launch used it: a kept row's columns were
 // copied in this launch (write-through: loaded sc1, after the barrier), the rest are the draws
 // made ahead by earlier launches (plain loads, issued before the barrier)
-__device__ __forceinline__ bool ep_kept(const FrRolloutArgs &fa, int k, int64_t rr)
+// (the weights and finish arguments live in device memory, EpArgs: each function works on a copy
+// in registers, since a load through fa.ep after any global store would have to be repeated)
+__device__ __forceinline__ bool ep_kept(const FrRolloutArgs &fa, const WGradArgs &a, int k, int64_t rr)
 {
     const SampleArgs &sa = fa.samp;
-    const int64_t g = fa.ep->wg.begin + rr;
+    const int64_t g = a.begin + rr;
     return g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
 }
-__device__ __forceinline__ const double *ep_eps_ptr(const FrRolloutArgs &fa, int k, int64_t rr)
+__device__ __forceinline__ const double *ep_eps_ptr(const WGradArgs &a, int k, int64_t rr)
 {
-    return fa.ep->wg.noise + ((int64_t)k * fa.ep->wg.Rpad + rr) * FR_C;
+    return a.noise + ((int64_t)k * a.Rpad + rr) * FR_C;
 }
-__device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, int k, int64_t rr, double *e)
+__device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, const WGradArgs &a, int k, int64_t rr, double *e)
 {
-    const double *n = ep_eps_ptr(fa, k, rr);
-    if (ep_kept(fa, k, rr)) {
+    const double *n = ep_eps_ptr(a, k, rr);
+    if (ep_kept(fa, a, k, rr)) {
 #pragma unroll
         for (int c = 0; c < FR_C; c++) e[c] = ep_ld(n + c);
     } else {
@@ -2595,9 +2599,8 @@ struct EpPre {
     double ne[EP_GR][FR_C];
     bool kept[EP_GR];
 };
-__device__ __forceinline__ void ep_unit_range(const FrRolloutArgs &fa, int u, int64_t &r0, int64_t &r1, int &k, int &s)
+__device__ __forceinline__ void ep_unit_range(const WGradArgs &a, int u, int64_t &r0, int64_t &r1, int &k, int &s)
 {
-    const WGradArgs &a = fa.ep->wg;
     const bool has = u >= 0;
     k = has ? u % a.H : 0;
     s = has ? u / a.H : 0;
@@ -2605,17 +2608,17 @@ __device__ __forceinline__ void ep_unit_range(const FrRolloutArgs &fa, int u, in
     r0 = (int64_t)s * chunk;
     r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
 }
-__device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, int u, int t, EpPre &p)
+__device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, const WGradArgs &a, int u, int t, EpPre &p)
 {
     int64_t r0, r1;
     int k, s;
-    ep_unit_range(fa, u, r0, r1, k, s);
+    ep_unit_range(a, u, r0, r1, k, s);
 #pragma unroll
     for (int m = 0; m < EP_GR; m++) {
         const int64_t r = r0 + t + 256 * m;
         const int64_t rr = (u >= 0 && r < r1) ? r : 0;
-        p.kept[m] = ep_kept(fa, k, rr);
-        const double *n = ep_eps_ptr(fa, k, rr);
+        p.kept[m] = ep_kept(fa, a, k, rr);
+        const double *n = ep_eps_ptr(a, k, rr);
         if (!p.kept[m])
 #pragma unroll
             for (int c = 0; c < FR_C; c++) p.ne[m][c] = n[c];
@@ -2624,16 +2627,16 @@ __device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, int u, int t
 
 // weights_gradient_kernel<FR_C, false> (kernels.hip) block (k, s) = unit u (k = u mod H, s = u / H)
 // on 256 threads t, unsharded with the objective's statistics; u < 0: no unit (the barrier only)
-__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, double *red, double *ssum, EpPre &p)
+__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, const WGradArgs &a, int u, int t, double *red, double *ssum,
+                                        EpPre &p)
 {
-    const WGradArgs &a = fa.ep->wg;
     constexpr int CP = FR_C;
     const int rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
     const bool has = u >= 0;
     int64_t r0, r1;
     int k, s;
-    ep_unit_range(fa, u, r0, r1, k, s);
+    ep_unit_range(a, u, r0, r1, k, s);
     double (&ne)[EP_GR][CP] = p.ne;
     double cpre[EP_GR];
 #pragma unroll
@@ -2641,7 +2644,7 @@ __device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, d
         const int64_t r = r0 + t + 256 * m;
         const int64_t rr = (has && r < r1) ? r : 0;
         if (p.kept[m]) {
-            const double *n = ep_eps_ptr(fa, k, rr);
+            const double *n = ep_eps_ptr(a, k, rr);
 #pragma unroll
             for (int c = 0; c < CP; c++) ne[m][c] = ep_ld(n + c);
         }
@@ -2710,7 +2713,7 @@ __device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, d
             part += wr;
         }
         double e[CP];
-        ep_eps(fa, k, r, e);
+        ep_eps(fa, a, k, r, e);
 #pragma unroll
         for (int c = 0; c < CP; c++) acc[c] += wr * e[c];
     }
@@ -2734,7 +2737,14 @@ __device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, int u, int t, d
 template <int NT>
 __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
 {
-    const FinishArgs &a = fa.ep->fin;
+    auto stamp = [&](int i) {   // diagnostics (MPPI_EP_STAMPS=1): after this wave's memory operations
+        if (fa.ep_stamps && tid == 0) {
+            __builtin_amdgcn_s_waitcnt(0);
+            fa.ep_stamps[blockIdx.x * EP_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    stamp(4);
+    const FinishArgs a = fa.ep->fin;
     const SampleArgs &sa = fa.samp;
     const int HC = a.H * a.C;
     Status *st = const_cast<Status *>(a.status);
@@ -2764,6 +2774,7 @@ __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
         }
     }
     __syncthreads();
+    stamp(5);
 #pragma unroll
     for (int e = 0; e < EP_MAXE; e++) {
         const int t = tid + e * NT;
@@ -2787,28 +2798,42 @@ __device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
         a.Ushift[t] = u;   // U*_shifted as sample() and the gradient step leave it
         const double v = ok ? u : uo;
         if (ok) U[t] = v;
-        a.out[t] = v;
+        ep_pub(a.out + t, v);
     }
     if (tid < a.X) a.x0_opt[tid] = sa.x0v[tid];
     for (int64_t i = tid; i < a.rank_n; i += NT) a.rank_zero[i] = 0;   // for rank_draw_kernel's tiles
     if (tid == 0) {
         st->sg_error = wt != 0;   // read by the next filter() row as "the update threw"
         if (upd) st->total = total;
-        a.out[HC + 0] = 0.0;      // (the folded filter() cost is read behind the stream)
-        a.out[HC + 1] = (double)all_nan;
-        a.out[HC + 2] = (double)early;
-        a.out[HC + 3] = 0.0;
-        a.out[HC + 4] = mn;
-        a.out[HC + 5] = mx;
-        a.out[HC + 7] = (double)wt;
+        ep_pub(a.out + HC + 0, 0.0);   // (the folded filter() cost is read behind the stream)
+        ep_pub(a.out + HC + 1, (double)all_nan);
+        ep_pub(a.out + HC + 2, (double)early);
+        ep_pub(a.out + HC + 3, 0.0);
+        ep_pub(a.out + HC + 4, mn);
+        ep_pub(a.out + HC + 5, mx);
+        ep_pub(a.out + HC + 7, (double)wt);
     }
     if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, tid);
+    if (fa.ep_stamps && tid == 0) fa.ep_stamps[blockIdx.x * EP_STAMPS + 6] = __builtin_amdgcn_s_memrealtime();
+    stamp(7);
+#ifdef PUB_FENCE
     __syncthreads();
     if (tid == 0) {
         st->wait_timeouts = 0;
         __threadfence_system();
         __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+#else
+    // The host reads only the mapped block (fine-grained host memory, not cached in L2): its stores
+    // went out system-scope, so once every wave has them acknowledged the flag can follow, without
+    // the system-scope release's write-back of this XCD's L2 (the step records it holds)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+        st->wait_timeouts = 0;
+        __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#endif
 }
 
 // the epilogue of fr_coop_x_kernel (NT = 64 XW threads): barrier, units, ticket, finish
@@ -2817,11 +2842,12 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
 {
     const int t = threadIdx.x;
     const int groups = gridDim.x, half = t >> 8, ht = t & 255;
-    const int nunits = a.ep->wg.H * GRAD_SPLIT, per = 2 * groups;
+    const WGradArgs wg = a.ep->wg;
+    const int nunits = wg.H * GRAD_SPLIT, per = 2 * groups;
     EpPre pre;   // the first pass's eps, loaded while the barrier waits
     {
         const int u = half * groups + (int)blockIdx.x;
-        ep_preload(a, u < nunits ? u : -1, ht, pre);
+        ep_preload(a, wg, u < nunits ? u : -1, ht, pre);
     }
     auto stamp = [&](int i) {   // diagnostics: one clock stamp per workgroup and phase
         if (a.ep_stamps && t == 0) a.ep_stamps[blockIdx.x * EP_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
@@ -2842,8 +2868,8 @@ __device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, in
     stamp(1);
     for (int base = 0; base < nunits; base += per) {
         const int u = base + half * groups + (int)blockIdx.x;
-        if (base > 0) ep_preload(a, u < nunits ? u : -1, ht, pre);
-        ep_unit(a, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8, pre);
+        if (base > 0) ep_preload(a, wg, u < nunits ? u : -1, ht, pre);
+        ep_unit(a, wg, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8, pre);
         __syncthreads();   // the halves' LDS is reused by the next pass
     }
     __builtin_amdgcn_s_waitcnt(0);   // every wave's unit stores have left it

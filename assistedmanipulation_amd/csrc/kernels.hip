@@ -1142,19 +1142,32 @@ __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, i
     gpart[t] = s;
 }
 
-// The host block is complete: after every thread's stores, one system-scope release store of the
-// update's sequence number, which the host polls (no event behind the finish kernel: an event
-// record delayed the next kernel on the stream by ~6 us).  Call from every thread of the block.
+// A store into the mapped host block (fine-grained host memory, not cached in L2): system scope,
+// so it leaves the GPU when issued and counts on this wave's vmcnt until host memory has it.
+__device__ __forceinline__ void pub(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+
+// The host block is complete: every thread waits for its own block stores (pub) to be acknowledged,
+// then one store of the update's sequence number, which the host polls (no event behind the finish
+// kernel: an event record delayed the next kernel on the stream by ~6 us).  No system-scope release:
+// its L2 write-back is for the device-memory stores, which only later kernels on the stream read.
+// Call from every thread of the block.
 __device__ __forceinline__ void publish_block(const FinishArgs &a)
 {
+#ifndef PUB_FENCE
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         // every thread has read this update's wait-timeout count (update_wait_timeouts): reset it
         // for the next rollout launch (stream-ordered after this kernel)
         a.status_w->wait_timeouts = 0;
         if (a.wait_local) *a.wait_local = 0.0;
+#ifdef PUB_FENCE   // (A/B builds: the release as before)
         __threadfence_system();
         __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+        __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     }
 }
 
@@ -1276,19 +1289,19 @@ __device__ __forceinline__ void finish_block(const FinishArgs &a, int &sg_err)
     for (int t = threadIdx.x; t < HC; t += blockDim.x) {
         const double v = ok ? a.Ushift[t] : a.U[t];
         if (ok) a.U[t] = v;
-        a.out[t] = v;
+        pub(a.out + t, v);
     }
     if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = a.x0[threadIdx.x];
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
         a.status_w->sg_error = sg_err || wt;   // read by the filter() row as "the update threw"
-        a.out[HC + 0] = *a.opt_cost;
-        a.out[HC + 1] = (double)stt.all_nan;
-        a.out[HC + 2] = (double)stt.early;
-        a.out[HC + 3] = (double)sg_err;
-        a.out[HC + 4] = stt.minimum;
-        a.out[HC + 5] = stt.maximum;
-        a.out[HC + 7] = (double)wt;
+        pub(a.out + HC + 0, *a.opt_cost);
+        pub(a.out + HC + 1, (double)stt.all_nan);
+        pub(a.out + HC + 2, (double)stt.early);
+        pub(a.out + HC + 3, (double)sg_err);
+        pub(a.out + HC + 4, stt.minimum);
+        pub(a.out + HC + 5, stt.maximum);
+        pub(a.out + HC + 7, (double)wt);
     }
 }
 
@@ -1347,20 +1360,20 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         }
         const double v = ok ? u : uo;
         if (ok) U[t] = v;
-        a.out[t] = v;
+        pub(a.out + t, v);
     }
     if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = x0;
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (threadIdx.x == 0) {
         a.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
         if (upd) a.status_w->total = total;
-        a.out[HC + 0] = oc;
-        a.out[HC + 1] = (double)stt.all_nan;
-        a.out[HC + 2] = (double)stt.early;
-        a.out[HC + 3] = 0.0;
-        a.out[HC + 4] = stt.minimum;
-        a.out[HC + 5] = stt.maximum;
-        a.out[HC + 7] = (double)wt;
+        pub(a.out + HC + 0, oc);
+        pub(a.out + HC + 1, (double)stt.all_nan);
+        pub(a.out + HC + 2, (double)stt.early);
+        pub(a.out + HC + 3, 0.0);
+        pub(a.out + HC + 4, stt.minimum);
+        pub(a.out + HC + 5, stt.maximum);
+        pub(a.out + HC + 7, (double)wt);
     }
     if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, threadIdx.x);
     publish_block(a);
@@ -1552,19 +1565,19 @@ __global__ __launch_bounds__(1024) void sg_finish_kernel(FinishArgs a)
     for (int i = t; i < HC; i += blockDim.x) {
         const double v = ok ? a.Ushift[i] : a.U[i];
         if (ok) a.U[i] = v;
-        a.out[i] = v;
+        pub(a.out + i, v);
     }
     if (t < a.X) a.x0_opt[t] = a.x0[t];
     for (int64_t i = t; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
     if (t == 0) {
         a.status_w->sg_error = err || wt;   // read by the filter() row as "the update threw"
-        a.out[HC + 7] = (double)wt;
-        a.out[HC + 0] = *a.opt_cost;
-        a.out[HC + 1] = (double)stt.all_nan;
-        a.out[HC + 2] = (double)stt.early;
-        a.out[HC + 3] = (double)err;
-        a.out[HC + 4] = stt.minimum;
-        a.out[HC + 5] = stt.maximum;
+        pub(a.out + HC + 7, (double)wt);
+        pub(a.out + HC + 0, *a.opt_cost);
+        pub(a.out + HC + 1, (double)stt.all_nan);
+        pub(a.out + HC + 2, (double)stt.early);
+        pub(a.out + HC + 3, (double)err);
+        pub(a.out + HC + 4, stt.minimum);
+        pub(a.out + HC + 5, stt.maximum);
     }
     if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, t);
     publish_block(a);

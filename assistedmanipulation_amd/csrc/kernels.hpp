@@ -121,7 +121,8 @@ struct EpArgs {
     WGradArgs wg;
     FinishArgs fin;
 };
-constexpr int EP_STAMPS = 4;   // epilogue stamps: barrier arrival, barrier passed, units stored, published (finisher)
+constexpr int EP_STAMPS = 8;   // epilogue stamps: barrier arrival, barrier passed, units stored, published (finisher);
+                                // the finisher's ticket, loads done, stores issued, stores acknowledged
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;

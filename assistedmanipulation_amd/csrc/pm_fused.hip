@@ -51,6 +51,8 @@ namespace {
 
 constexpr int PT = PM_FUSED_THREADS;   // threads per block
 constexpr int PC = 3;                  // control dimension of the point mass
+// a store into the mapped host block, system scope (kernels.hip pub)
+__device__ __forceinline__ void pub(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 constexpr int BAR_SPINS = 1 << 22;     // about a second of s_sleep 1
 constexpr int IB = 8;                  // phase A items per thread per batch of loads
 #ifndef PM_SB
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             if (upd || P.shift_by > 0) a.Us[o] = u;   // U*_shifted as sample() and the step leave it
             const double v = ok ? u : a.U[o];
             if (ok) a.U[o] = v;
-            a.out[o] = v;
+            pub(a.out + o, v);
         }
         if (t < a.X) a.x0_opt[t] = a.x0v[t];
         if (t == 0) {
@@ -409,21 +411,28 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
                 for (int i = 1; i < GRAD_SPLIT; i++) st->tsplit[i] = 0.0;
             }
             st->sg_error = wt != 0;   // "the update threw": no filter() (as the finish kernels)
-            a.out[HC + 0] = 0.0;      // (filter()'s cost is read behind the stream: wait_optimal)
-            a.out[HC + 1] = (double)all_nan;
-            a.out[HC + 2] = (double)early;
-            a.out[HC + 3] = 0.0;
-            a.out[HC + 4] = mn;
-            a.out[HC + 5] = mx;
-            a.out[HC + 7] = (double)wt;
+            pub(a.out + HC + 0, 0.0);      // (filter()'s cost is read behind the stream: wait_optimal)
+            pub(a.out + HC + 1, (double)all_nan);
+            pub(a.out + HC + 2, (double)early);
+            pub(a.out + HC + 3, 0.0);
+            pub(a.out + HC + 4, mn);
+            pub(a.out + HC + 5, mx);
+            pub(a.out + HC + 7, (double)wt);
         }
         if (t < CS_SLOTS) mppi_sample::reset_cost_stats(a.stats, t);   // every block has read them (ticket)
+#ifndef PUB_FENCE   // the host block's stores acknowledged, then the flag (kernels.hip publish_block)
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
         __syncthreads();
         stamp(7);
         if (t == 0) {
             st->wait_timeouts = 0;
+#ifdef PUB_FENCE
             __threadfence_system();
             __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+            __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
         }
         stamp(8);
     }

@@ -147,7 +147,7 @@ step_pmstamps() {   # [variant]: the fused point-mass kernel's phase stamps (MPP
 step_epstamps() {   # the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1, printed at destroy)
     MPPI_EPILOGUE=1 MPPI_EP_STAMPS=1 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline $BENCH_ARGS \
         > $O/epstamps.json 2> $O/epstamps.err || { echo "epstamps rc=$?"; tail -20 $O/epstamps.err; return 1; }
-    grep "epilogue phases" $O/epstamps.err
+    grep "epilogue" $O/epstamps.err
     summary $O/epstamps.json epstamps
 }
 
