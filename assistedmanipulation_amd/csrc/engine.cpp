@@ -49,6 +49,7 @@ void env_switches_refresh()
     g_env.handover_off = is("MPPI_HANDOVER", '0');
     g_env.split_off = is("MPPI_SPLIT", '0');
     g_env.relay2_off = is("MPPI_RELAY2", '0');
+    g_env.weights_finish = is("MPPI_WEIGHTS_FINISH", '1');
 }
 }  // namespace mppi_eng
 
@@ -190,6 +191,8 @@ struct mppi_handle {
     // (rollout, weights + gradient, finish, rank + draws ahead) captured once and replayed with each
     // update's arguments written into the executable graph's kernel nodes
     int graph_mode = 0;
+    bool wf_fused = false;            // this update's optimise() + finish() run as one launch (phase 3)
+    unsigned *d_wf_ticket = nullptr;  // weights_finish_kernel's ticket (left at zero by the kernel)
     bool graph_dry = false;             // phases fill `gargs` instead of launching
     struct GraphArgs {
         FrRolloutArgs roll, roll2;   // the rollout launch (the split's two: roll, roll2)
@@ -987,6 +990,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
+    CREATE_TRY(dalloc(h, &h->d_wf_ticket, 1));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_cstats, 1));
     // the first update's statistics start empty (later ones are reset by the finish kernel)
@@ -1859,6 +1863,7 @@ mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
+    h->wf_fused = false;
     if (h->ep_ran) return MPPI_OK;   // optimise() ran in the rollout launch's epilogue
     WGradArgs w{};
     w.cost = h->d_costs;
@@ -1877,8 +1882,12 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     h->gargs.wg = w;
     if (h->graph_dry) return MPPI_OK;
-    // sharded: the partial gradient is summed here and all-reduced before phase 3
-    HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
+    // optimise() and finish() as one launch where it applies: phase 3 launches it (its arguments
+    // include the publish sequence).  Sharded: the partial gradient is summed here and all-reduced
+    // before phase 3.
+    // (opt-in, MPPI_WEIGHTS_FINISH=1: measured slower)
+    h->wf_fused = env_switches().weights_finish && !h->graph_mode && weights_finish_eligible(w, finish_args(h));
+    if (!h->wf_fused) HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_wg, h->stream));
     return MPPI_OK;
 }
@@ -1890,7 +1899,13 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     h->gargs.fin = finish_args(h);
-    if (!h->graph_dry && !h->ep_ran) HIP_TRY(launch_finish(h->gargs.fin, h->stream));   // (or in the epilogue)
+    if (!h->graph_dry && !h->ep_ran) {   // (or in the epilogue)
+        if (h->wf_fused) {
+            HIP_TRY(launch_weights_finish(h->gargs.wg, h->gargs.fin, h->d_wf_ticket, h->stream));
+            h->info[MPPI_INFO_FUSED_UPDATE] = 2;
+        }
+        else HIP_TRY(launch_finish(h->gargs.fin, h->stream));
+    }
     const double seq = (double)(++h->publish_seq);
     *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));

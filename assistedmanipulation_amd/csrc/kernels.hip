@@ -1379,6 +1379,194 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
     publish_block(a);
 }
 
+// optimise() and finish() in one launch (the usual unsharded update: cost statistics from the
+// rollout launch, no Savitzky-Golay, R <= SM_LARGE_R).  Block k is step k of weights_gradient_kernel
+// for all GRAD_SPLIT rollout ranges at once: its 512 threads are splits s, s + 2, s + 4 and s + 6 of
+// thread t at 256 (s mod 2) + t, so each wave holds the same 64 (split, thread) pairs as one of that kernel's
+// waves and every sum - per thread in row order, the wave butterflies, the four wave sums, the
+// eight split partials in order - is formed as the two launches form it: gradient, normaliser,
+// weights and U* are bit-identical to weights_gradient_kernel + finish_flat_kernel.  Every block
+// evaluates all R exponentials for the normaliser (the eight slice blocks did so between them), so
+// block k can step, clamp and publish its step's C elements of U* at once; the last block to take
+// the ticket writes the status words and raises the flag (the partial gradients never leave the
+// block: the finish launch and its memory trip go).
+constexpr int WF_NT = 512, WF_GR = 2, WF_NJ = GRAD_SPLIT * 256 / WF_NT;   // splits per thread
+struct WfFinishIn {   // finish_flat_kernel's inputs for element e (unconditional loads: no branches)
+    double us, uo, hi, lo, oc, x0;
+    __device__ __forceinline__ void load(const FinishArgs &f, int e, int cc, int T)
+    {
+        us = f.Ushift[e];
+        uo = f.U[e];
+        hi = f.cmax[cc];
+        lo = f.cmin[cc];
+        oc = *f.opt_cost;
+        x0 = f.x0[T < f.X ? T : 0];
+    }
+};
+template <int C>
+__global__ __launch_bounds__(WF_NT) void weights_finish_kernel(WGradArgs a, FinishArgs f, unsigned *ticket)
+{
+    static_assert(GRAD_SPLIT * 256 == WF_NJ * WF_NT && WF_NT % 256 == 0, "whole splits per thread");
+    constexpr int SS = WF_NT / 256;   // split stride
+    __shared__ double red[GRAD_SPLIT][4][C];
+    __shared__ double ssum[GRAD_SPLIT][4];
+    __shared__ int last;
+    const int T = threadIdx.x, t = T & 255, sl = T >> 8, rw = t >> 6, l = T & 63;
+    const int k = blockIdx.x, HC = f.H * C;
+    // 32-bit indexing (weights_finish_eligible: R <= SM_LARGE_R, eps under 2 GB): the loads take one
+    // VGPR offset each from the arrays' SGPR bases
+    const int R = (int)a.R, chunk = (R + GRAD_SPLIT - 1) / GRAD_SPLIT;
+    const unsigned kb = (unsigned)k * (unsigned)a.Rpad;
+    int r0[WF_NJ], r1[WF_NJ];
+#pragma unroll
+    for (int j = 0; j < WF_NJ; j++) {
+        r0[j] = (sl + SS * j) * chunk;
+        r1[j] = (r0[j] + chunk < R) ? r0[j] + chunk : R;
+    }
+    // one memory trip: the statistics' slots, the first rows' eps and costs (the finish's inputs
+    // follow the sums)
+    const unsigned long long kmn = a.stats->kmin[16 * l], kmx = a.stats->kmax[16 * l];
+    const unsigned int kct = a.stats->count[32 * l];
+    const int wt = f.status->wait_timeouts;   // unsharded: update_wait_timeouts
+    double ne[WF_NJ][WF_GR][C], cpre[WF_NJ][WF_GR];
+#pragma unroll
+    for (int j = 0; j < WF_NJ; j++)
+#pragma unroll
+        for (int m = 0; m < WF_GR; m++) {
+            const int r = r0[j] + t + 256 * m, rr = r < r1[j] ? r : 0;
+            const double *n = a.noise + (kb + (unsigned)rr) * (unsigned)C;
+#pragma unroll
+            for (int c = 0; c < C; c++) ne[j][m][c] = n[c];
+            cpre[j][m] = a.cost[rr];
+        }
+    __builtin_amdgcn_sched_barrier(0);   // every load above is issued before the reductions wait for any
+    const int cc = T < C ? T : 0, e = k * C + cc;
+    // min / max / count (weights_gradient_kernel's stats path)
+    static_assert(CS_SLOTS == 64, "one slot per lane");
+    const unsigned long long kn = mppi_dev::wave_umin64_dpp(kmn), kx = mppi_dev::wave_umax64_dpp(kmx);
+    const unsigned int nv = (unsigned int)mppi_dev::wave_sum_dpp((double)kct);
+    const double minimum = nv ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
+    const double maximum = nv ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
+    const bool all_nan = (double)nv <= 1.0;   // minmax_element over <= 1 element: it1 == it2 -> throw
+    const double difference = maximum - minimum;
+    const bool early = all_nan || difference < 1e-6;   // early return (mppi.cpp:373-375)
+    WfFinishIn fin;
+    if (early) fin.load(f, e, cc, T);
+    if (!early) {
+        auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
+        double acc[WF_NJ][C], part[WF_NJ];
+#pragma unroll
+        for (int j = 0; j < WF_NJ; j++) {
+            {   // the first row starts the sums (0 + x is x: the same values as from zero), so the
+                // sums take over its eps registers
+                const int r = r0[j] + t;
+                const bool in = r < r1[j];
+                const double wr = expw(cpre[j][0]);
+                if (k == 0 && in) a.wexp[r] = wr;
+                part[j] = in ? wr : 0.0;
+#pragma unroll
+                for (int c = 0; c < C; c++) acc[j][c] = in ? wr * ne[j][0][c] : 0.0;
+            }
+#pragma unroll
+            for (int m = 1; m < WF_GR; m++) {
+                const int r = r0[j] + t + 256 * m;
+                if (r < r1[j]) {
+                    const double wr = expw(cpre[j][m]);
+                    if (k == 0) a.wexp[r] = wr;
+                    part[j] += wr;
+#pragma unroll
+                    for (int c = 0; c < C; c++) acc[j][c] += wr * ne[j][m][c];
+                }
+            }
+            for (int r = r0[j] + t + 256 * WF_GR; r < r1[j]; r += 256) {
+                const double wr = expw(a.cost[r]);
+                if (k == 0) a.wexp[r] = wr;
+                part[j] += wr;
+                const double *n = a.noise + (kb + (unsigned)r) * (unsigned)C;
+#pragma unroll
+                for (int c = 0; c < C; c++) acc[j][c] += wr * n[c];
+            }
+        }
+        fin.load(f, e, cc, T);   // behind the sums (their eps registers are free), ahead of the butterflies
+#pragma unroll
+        for (int j = 0; j < WF_NJ; j++) {
+            part[j] = wave_sum(part[j]);
+#pragma unroll
+            for (int c = 0; c < C; c++) acc[j][c] = wave_sum(acc[j][c]);
+            if (l == 0) {
+                ssum[sl + SS * j][rw] = part[j];
+#pragma unroll
+                for (int c = 0; c < C; c++) red[sl + SS * j][rw][c] = acc[j][c];
+            }
+        }
+    }
+    __syncthreads();
+    const bool upd = !early && !wt, ok = !all_nan && !wt;   // no filter: no SG error
+    double total = 0.0;
+    if (T < C || (k == 0 && T < GRAD_SPLIT)) {
+        // the normaliser: the eight slice sums (four wave sums each) in order (softmin_total)
+#pragma unroll
+        for (int s = 0; s < GRAD_SPLIT; s++) {
+            const double ts = (ssum[s][0] + ssum[s][1]) + (ssum[s][2] + ssum[s][3]);
+            total = s == 0 ? ts : total + ts;
+        }
+    }
+    if (T < C) {   // finish_flat_kernel's element (k, T)
+        double g = 0.0;
+#pragma unroll
+        for (int s = 0; s < GRAD_SPLIT; s++) {
+            const double p = (red[s][0][T] + red[s][1][T]) + (red[s][2][T] + red[s][3][T]);
+            g = s == 0 ? p : g + p;
+        }
+        g /= total;   // sum_r e_r eps_r / sum_r e_r
+        double u = fin.us;
+        if (upd) {
+            f.gradient[e] = g;
+            u += g * f.gradient_step;
+            if (f.control_bound) {
+                u = smin(u, fin.hi);
+                u = smax(u, fin.lo);
+            }
+            f.Ushift[e] = u;
+        }
+        const double v = ok ? u : fin.uo;
+        if (ok) f.U[e] = v;
+        pub(f.out + e, v);
+    }
+    if (k == 0) {   // the weights kernel's lead and slice blocks, finish's x0 copy
+        Status *st = a.status;
+        if (T == 0) {
+            st->all_nan = all_nan;
+            st->early = early;
+            st->minimum = minimum;
+            st->maximum = maximum;
+            if (upd) f.status_w->total = total;
+        }
+        if (!early && T < GRAD_SPLIT) st->tsplit[T] = (ssum[T][0] + ssum[T][1]) + (ssum[T][2] + ssum[T][3]);
+        if (T < f.X) f.x0_opt[T] = fin.x0;
+    }
+    for (int64_t i = (int64_t)k * WF_NT + T; i < f.rank_n; i += (int64_t)gridDim.x * WF_NT) f.rank_zero[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's host-block stores acknowledged, its statistics read
+    __syncthreads();
+    if (T == 0) last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
+    __syncthreads();
+    if (!last) return;
+    // every block has stored its step and read the statistics: the status words, the reset, the flag
+    if (T == 0) {
+        f.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
+        pub(f.out + HC + 0, fin.oc);
+        pub(f.out + HC + 1, (double)all_nan);
+        pub(f.out + HC + 2, (double)early);
+        pub(f.out + HC + 3, 0.0);
+        pub(f.out + HC + 4, minimum);
+        pub(f.out + HC + 5, maximum);
+        pub(f.out + HC + 7, (double)wt);
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next update
+    }
+    if (f.stats_reset) mppi_sample::reset_cost_stats(f.stats_reset, T);
+    publish_block(f);
+}
+
 
 
 // finish() with the Savitzky-Golay filter (configs[4]), one wave per control dimension with its
@@ -1660,6 +1848,20 @@ hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_s
     const int HC = a.H * a.C;
     hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, a.gsplit, GRAD_SPLIT, HC,
                        (const Status *)a.status, gpart);
+    return hipGetLastError();
+}
+
+bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f)
+{
+    return a.C == FR_C && f.C == FR_C && a.stats != nullptr && a.R <= SM_LARGE_R && a.begin == 0 && a.count == a.R &&
+           f.sg_window == 0 && f.wait_all == nullptr && f.ns == GRAD_SPLIT && f.H == a.H && f.X <= WF_NT &&
+           a.Rpad >= a.R && (int64_t)a.H * a.Rpad * a.C * (int64_t)sizeof(double) < ((int64_t)1 << 31);
+}
+
+hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, unsigned *ticket, hipStream_t s)
+{
+    if (!weights_finish_eligible(a, f) || ticket == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(weights_finish_kernel<FR_C>, dim3((unsigned)a.H), dim3(WF_NT), 0, s, a, f, ticket);
     return hipGetLastError();
 }
 

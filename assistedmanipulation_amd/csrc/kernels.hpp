@@ -31,7 +31,8 @@ struct Status {
 // order-preserving keys (exact, so deterministic) by whoever evaluates the objective (the rollout
 // launch or fr_step_cost_kernel), and read by weights_gradient_kernel instead of a pass over all R
 // costs in each of its blocks.  CS_SLOTS slots, one 128-byte line each, spread the atomics: on one
-// address 4099 x 3 of them cost ~40 us.  Reset by the update's sampling launch.
+// address 4099 x 3 of them cost ~40 us.  Reset by the finish kernels (a launch boundary before the
+// next update's folds).
 constexpr int CS_SLOTS = 64;
 struct CostStats {
     unsigned long long kmin[CS_SLOTS * 16];
@@ -348,7 +349,7 @@ bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MP
 // handle) instead of by getenv on every update (~80 ns each on the host's path between updates)
 struct EnvSwitches {
     bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off,
-        relay2_off;
+        relay2_off, weights_finish;
 };
 const EnvSwitches &env_switches();
 void env_switches_refresh();
@@ -358,6 +359,11 @@ bool fr_coop_update_folds(int64_t count, int H);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
+// optimise() + finish() as one launch of H blocks (weights_finish_kernel, bit-identical to the two
+// launches); eligible: unsharded, cost statistics from the rollout launch, no Savitzky-Golay,
+// R <= SM_LARGE_R, FrankaRidgeback's C.  ticket: a device counter at zero (left at zero).
+bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f);
+hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, unsigned *ticket, hipStream_t s);
 
 // FrankaRidgeback::PinocchioDynamics as one device-resident object (fr_object.hip): the members of
 // pinocchio_dynamics.hpp:380-425 the methods read and write.

@@ -401,16 +401,23 @@ def run(args, world, rank, local_rank, dist):
     # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
     # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
     # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
-    if kt[6] > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
+    # (with optimise() and finish() as one launch, weights_finish_kernel, that launch is the
+    # breakdown's reduce phase kt[2]: the weight reduce plus the finish's few hundred bytes)
+    wf = not pm and info.get("fused_update") == 2
+    wg_ms = kt[2] if wf else kt[6]
+    if wg_ms > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
         wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
-        wg = {"kernel": "weights_gradient_kernel", "bound": "hbm", "ms": kt[6], "bytes_per_launch": wg_bytes,
-              "achieved_GBs": wg_bytes / (kt[6] * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
+        wg = {"kernel": "weights_finish_kernel (optimise + finish)" if wf else "weights_gradient_kernel", "bound": "hbm",
+              "ms": wg_ms, "bytes_per_launch": wg_bytes,
+              "achieved_GBs": wg_bytes / (wg_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
         wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS
         wg["traffic"] = None
         if os.path.exists(PMC_WG_JSON) and world == 1 and default_workload and not pm:
             with open(PMC_WG_JSON) as f:
-                wg["traffic"] = json.load(f)["traffic_bytes"]
-            wg["traffic_source"] = recorded_label(PMC_WG_JSON)
+                rec = json.load(f)
+            if wg["kernel"].split()[0] in rec["kernel"]:   # recorded for the kernel this run used
+                wg["traffic"] = rec["traffic_bytes"]
+                wg["traffic_source"] = recorded_label(PMC_WG_JSON)
         hbm["weight_reduce"] = wg
     if rank != 0:
         if dist:

@@ -390,9 +390,11 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
                                              rollout launch (a bug if nonzero: that update then
                                              failed with MPPI_ERR_DEVICE and published nothing) */
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
-#define MPPI_INFO_FUSED_UPDATE 9          /* the whole update ran as one launch (point mass), or
+#define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass), or
                                              optimise() and finish() ran in the rollout launch
-                                             (FrankaRidgeback, opt-in MPPI_EPILOGUE=1) */
+                                             (FrankaRidgeback, opt-in MPPI_EPILOGUE=1); 2: optimise()
+                                             and finish() ran as one launch after it (opt-in
+                                             MPPI_WEIGHTS_FINISH=1, weights_finish_kernel) */
 #define MPPI_UPDATE_INFO_N 10
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
