@@ -50,6 +50,7 @@ void env_switches_refresh()
     g_env.split_off = is("MPPI_SPLIT", '0');
     g_env.relay2_off = is("MPPI_RELAY2", '0');
     g_env.weights_finish = is("MPPI_WEIGHTS_FINISH", '1');
+    g_env.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
 }
 }  // namespace mppi_eng
 
@@ -971,7 +972,15 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         fr_coop_set_cu_count((unsigned)ncu);
     }
-    CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    // the update stream at the greatest priority (its queue's dispatches go first): measured
+    // 0.7-1.4 us per update faster over seven interleaved pairs at 4096x64
+    if (!env_switches().stream_prio_off) {
+        int lo = 0, hi = 0;
+        CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CREATE_TRY(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
+    } else {
+        CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    }
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream_opt, hipStreamNonBlocking));
     // timing-only events without the system-scope fence: with it each record held the next kernel
     // on the stream back by ~6 us (cache write-back and invalidate); the host reads nothing they guard

@@ -349,7 +349,7 @@ bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MP
 // handle) instead of by getenv on every update (~80 ns each on the host's path between updates)
 struct EnvSwitches {
     bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off,
-        relay2_off, weights_finish;
+        relay2_off, weights_finish, stream_prio_off;
 };
 const EnvSwitches &env_switches();
 void env_switches_refresh();
