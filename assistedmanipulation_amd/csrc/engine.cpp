@@ -31,26 +31,19 @@
 
 using namespace mppi_eng;
 
-namespace {
-EnvSwitches g_env;
-}
-
 namespace mppi_eng {
-const EnvSwitches &env_switches() { return g_env; }
-void env_switches_refresh()
+EnvSwitches env_switches_read()
 {
     auto is = [](const char *name, char c) { const char *e = std::getenv(name); return e && e[0] == c; };
-    g_env.draw_ahead_off = is("MPPI_DRAW_AHEAD", '0');
-    g_env.tail_draws_off = is("MPPI_TAIL_DRAWS", '0');
-    g_env.fuse_sample = is("MPPI_FUSE_SAMPLE", '1');
-    g_env.epilogue = is("MPPI_EPILOGUE", '1');
-    g_env.pm_fused_off = is("MPPI_PM_FUSED", '0');
-    g_env.costs_in_launch_off = is("MPPI_COSTS_IN_LAUNCH", '0');
-    g_env.handover_off = is("MPPI_HANDOVER", '0');
-    g_env.split_off = is("MPPI_SPLIT", '0');
-    g_env.relay2_off = is("MPPI_RELAY2", '0');
-    g_env.weights_finish = is("MPPI_WEIGHTS_FINISH", '1');
-    g_env.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
+    EnvSwitches e{};
+    e.draw_ahead_off = is("MPPI_DRAW_AHEAD", '0');
+    e.tail_draws_off = is("MPPI_TAIL_DRAWS", '0');
+    e.pm_fused_off = is("MPPI_PM_FUSED", '0');
+    e.costs_in_launch_off = is("MPPI_COSTS_IN_LAUNCH", '0');
+    e.handover_off = is("MPPI_HANDOVER", '0');
+    e.split_off = is("MPPI_SPLIT", '0');
+    e.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
+    return e;
 }
 }  // namespace mppi_eng
 
@@ -67,6 +60,7 @@ struct DeviceBuf {
 
 struct mppi_handle {
     int device = 0;
+    EnvSwitches env{};   // the A/B switches as the environment held them at create (env_switches_read)
     hipStream_t stream = nullptr;
     hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
 
@@ -174,7 +168,6 @@ struct mppi_handle {
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
-    bool coop = true;   // FrankaRidgeback: cooperative 16-lane kernel (MPPI_FR_KERNEL=lane: one lane per rollout)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
     size_t inj_capacity = 0;   // doubles
@@ -192,8 +185,6 @@ struct mppi_handle {
     // (rollout, weights + gradient, finish, rank + draws ahead) captured once and replayed with each
     // update's arguments written into the executable graph's kernel nodes
     int graph_mode = 0;
-    bool wf_fused = false;            // this update's optimise() + finish() run as one launch (phase 3)
-    unsigned *d_wf_ticket = nullptr;  // weights_finish_kernel's ticket (left at zero by the kernel)
     bool graph_dry = false;             // phases fill `gargs` instead of launching
     struct GraphArgs {
         FrRolloutArgs roll, roll2;   // the rollout launch (the split's two: roll, roll2)
@@ -221,18 +212,6 @@ struct mppi_handle {
     uint64_t *d_pm_stamps = nullptr;   // MPPI_PM_STAMPS=1: the launch's phase stamps per block
     std::vector<double> pm_stamp_sum; // their per-phase sums (us after the block's entry), printed at destroy
     int64_t pm_stamp_n = 0;
-    // optimise() and finish() in the rollout launch's epilogue (fr_coop.hip epilogue)
-    unsigned *d_ep_sync = nullptr;   // [2] grid-barrier and ticket counters (monotonic)
-    EpArgs *d_ep_args = nullptr, *h_ep_args = nullptr;   // the epilogue's arguments (device, pinned staging)
-    double *d_relay_buf = nullptr;     // relay2: the relay's hand-over between its two workgroups
-    unsigned *d_relay_flag = nullptr;  // [2] monotonic flags (epochs)
-    unsigned relay_epoch = 0;
-    unsigned ep_total = 0;           // their value after the last epilogue launch
-    bool ep_ran = false;             // this update's rollout launch ran the epilogue
-    uint64_t *d_ep_stamps = nullptr; // MPPI_EP_STAMPS=1: the epilogue's phase stamps per workgroup
-    unsigned ep_stamp_groups = 0;
-    std::vector<double> ep_stamp_sum;   // us: last arrival -> barrier passed (last), -> units stored (last), -> published
-    int64_t ep_stamp_n = 0;
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -533,38 +512,21 @@ void dfree(mppi_handle *h, T *&p)
     p = nullptr;
 }
 
-// The single-lane kernel (MPPI_FR_KERNEL=lane, A/B runs) implements AssistedManipulation only.
-// the lane kernel implements the default AssistedManipulation only (no TrackPoint, no energy tank)
-bool use_coop(const mppi_handle *h)
-{
-    return h->coop || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || h->am.enable_energy_limit;
-}
-
-// Sampling inside the cooperative update launch (fr_coop.hip fused_sample): FrankaRidgeback rows
-// in one round of four-wave workgroups, opt-in (MPPI_FUSE_SAMPLE=1).  Measured even with the
-// separate sample_kernel (0.3604-0.3622 vs 0.3610-0.3629 ms/update at 4096 x 64): the prologue
-// delays the critical workgroup (the one whose fifth wave doubles a SIMD) by what the launch saves.
 // The next update's draws made behind the publish (phase 3) so that its sampling launch leaves
-// the critical path: device Philox, diagonal transform, an update whose rollout launch runs one
-// round of workgroups (it copies the kept columns in, fused_sample mode 2).  MPPI_DRAW_AHEAD=0
-// turns it off (A/B).
+// the critical path: device Philox, diagonal transform, an update whose rollout launch runs rounds
+// of four-wave workgroups (it copies the kept columns in, FrRolloutArgs::drawn_ahead).
+// MPPI_DRAW_AHEAD=0 turns it off (A/B).
 static bool draw_ahead_possible(const mppi_handle *h)
 {
-    if (env_switches().draw_ahead_off) return false;
-    return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C && h->tdiag &&
-           h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count);
+    if (h->env.draw_ahead_off) return false;
+    return h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && h->C == FR_C && h->tdiag &&
+           h->noise_source == MPPI_NOISE_DEVICE_PHILOX && fr_coop_update_fusable(h->count, h->env);
 }
 
 // MPPI_TAIL_DRAWS=0: the next update's draws all in rank_draw_kernel behind the publish (A/B)
-static bool tail_draws_disabled()
+static bool tail_draws_disabled(const mppi_handle *h)
 {
-    return env_switches().tail_draws_off;
-}
-
-bool fuse_sampling(const mppi_handle *h)
-{
-    return env_switches().fuse_sample && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h) && h->C == FR_C &&
-           fr_coop_update_fusable(h->count);
+    return h->env.tail_draws_off;
 }
 
 mppi_status alloc_shard_buffers(mppi_handle *h)
@@ -883,7 +845,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     mppi_handle *h = nullptr;
     if (!cfg || !dyn || !cost || !out) return fail(nullptr, MPPI_ERR_INVALID, "null argument");
     *out = nullptr;
-    env_switches_refresh();   // the A/B switches, as the environment holds them now
+    const EnvSwitches env = env_switches_read();   // the A/B switches, as the environment holds them now
     const int64_t Cd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 3 : (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK ? FR_C : -1);
     const int64_t Xd = dyn->kind == MPPI_DYNAMICS_POINT_MASS ? 6 : FR_X;
     const bool fr_cost = cost->kind == MPPI_COST_ASSISTED_MANIPULATION || cost->kind == MPPI_COST_TRACK_POINT;
@@ -912,6 +874,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     }
 
     h = new mppi_handle();
+    h->env = env;
     {
         const char *e = getenv("MPPI_HOST_TRACE");
         h->host_trace = e && e[0] == '1';
@@ -948,10 +911,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     h->count = h->R;
     h->U_host.assign((size_t)(h->H * h->C), 0.0);
     if (const char *tp = std::getenv("MPPI_WAVE_TRACE")) h->trace_path = tp;
-    {
-        const char *kv = std::getenv("MPPI_FR_KERNEL");
-        h->coop = !(kv && std::string(kv) == "lane");
-    }
     noise_transform((int)Cd, cfg->covariance, h->T, h->tdiag);
     if (h->H < 1 || h->H > (1 << 20)) { delete h; return fail(nullptr, MPPI_ERR_INVALID, "horizon steps out of range"); }
 
@@ -971,10 +930,11 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         int ncu = 0;
         CREATE_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         fr_coop_set_cu_count((unsigned)ncu);
+        pm_fused_set_device(device);
     }
     // the update stream at the greatest priority (its queue's dispatches go first): measured
     // 0.7-1.4 us per update faster over seven interleaved pairs at 4096x64
-    if (!env_switches().stream_prio_off) {
+    if (!h->env.stream_prio_off) {
         int lo = 0, hi = 0;
         CREATE_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         CREATE_TRY(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
@@ -999,7 +959,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
-    CREATE_TRY(dalloc(h, &h->d_wf_ticket, 1));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_cstats, 1));
     // the first update's statistics start empty (later ones are reset by the finish kernel)
@@ -1065,17 +1024,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(dalloc(h, &h->d_cost, 1));
         CREATE_TRY(hipMemcpy(h->d_cost, &c, sizeof(c), hipMemcpyHostToDevice));
         CREATE_TRY(dalloc(h, &h->d_table, FR_BODY_TABLE));
-        CREATE_TRY(dalloc(h, &h->d_ep_sync, 2));
-        CREATE_TRY(dalloc(h, &h->d_ep_args, 1));
-        CREATE_TRY(dalloc(h, &h->d_relay_buf, 64 * 3 + 8));
-        CREATE_TRY(dalloc(h, &h->d_relay_flag, 2));
-        CREATE_TRY(hipHostMalloc((void **)&h->h_ep_args, sizeof(EpArgs), hipHostMallocDefault));
-        const char *es = std::getenv("MPPI_EP_STAMPS");
-        if (es && es[0] == '1') {
-            h->ep_stamp_groups = (unsigned)std::max<int64_t>(1, (h->R + 15) / 16);
-            CREATE_TRY(dalloc(h, &h->d_ep_stamps, (size_t)h->ep_stamp_groups * EP_STAMPS));
-            h->ep_stamp_sum.assign(9, 0.0);
-        }
         CREATE_TRY(launch_fr_body_table(h->d_model, h->d_cost, h->d_table, nullptr));
         CREATE_TRY(hipDeviceSynchronize());
     } else {
@@ -1137,14 +1085,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 void mppi_destroy(mppi_handle *h)
 {
     if (!h) return;
-    if (h->ep_stamp_n > 0)
-        std::fprintf(stderr, "epilogue phases (us, mean of %lld): arrivals spread %.2f  barrier release %.2f  units %.2f  "
-                             "ticket+finish+publish %.2f\n", (long long)h->ep_stamp_n, h->ep_stamp_sum[0] / h->ep_stamp_n,
-                     h->ep_stamp_sum[1] / h->ep_stamp_n, h->ep_stamp_sum[2] / h->ep_stamp_n, h->ep_stamp_sum[3] / h->ep_stamp_n);
-    if (h->ep_stamp_n > 0)
-        std::fprintf(stderr, "epilogue finisher (us): ticket %.2f  loads %.2f  compute+stores %.2f  acknowledged %.2f  flag %.2f\n",
-                     h->ep_stamp_sum[4] / h->ep_stamp_n, h->ep_stamp_sum[5] / h->ep_stamp_n, h->ep_stamp_sum[6] / h->ep_stamp_n,
-                     h->ep_stamp_sum[7] / h->ep_stamp_n, h->ep_stamp_sum[8] / h->ep_stamp_n);
     if (h->pm_stamp_n > 0) {
         std::fprintf(stderr, "pm_update_kernel phases (us after the first block's entry, last block, mean of %lld):",
                      (long long)h->pm_stamp_n);
@@ -1165,7 +1105,6 @@ void mppi_destroy(mppi_handle *h)
     if (h->graph) (void)hipGraphDestroy(h->graph);
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
-    if (h->h_ep_args) (void)hipHostFree(h->h_ep_args);
     if (h->h_opt) (void)hipHostFree(h->h_opt);
     if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
@@ -1485,7 +1424,7 @@ void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 // kernel (CostStats); sharded ones see only their own costs there and reduce after the all-reduce.
 static bool cost_stats_used(const mppi_handle *h)
 {
-    return !sharded(h) && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
+    return !sharded(h) && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK;
 }
 
 // Where an update's rollout costs go: d_costs, or the rank's zero-padded local vector that the
@@ -1545,13 +1484,10 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         a.cost_kind = h->cost_kind;
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.rec = h->d_rec_opt;
-        if (use_coop(h)) {   // the row's objective after its loop (fr_coop_kernel's one-wave path)
-            a.costs_in_launch = fr_coop_costs_in_launch() ? 1 : 0;
-            HIP_TRY(launch_fr_coop(a, h->stream_opt));
-            if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
-        } else {
-            HIP_TRY(launch_fr_rollout(a, h->stream_opt));
-        }
+        // the row's objective after its loop (fr_coop_kernel's one-wave path)
+        a.costs_in_launch = fr_coop_costs_in_launch(h->env) ? 1 : 0;
+        HIP_TRY(launch_fr_coop(a, h->stream_opt));
+        if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -1574,18 +1510,6 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
     return MPPI_OK;
 }
 
-// optimise() and finish() in the rollout launch's epilogue: unsharded, no smoothing, the eager path
-// (the hipGraph path keeps its captured four-kernel chain), timing below level 2 (whose events
-// separate the kernels).  Opt-in (MPPI_EPILOGUE=1): on MI355X the in-launch weight reduce and
-// finish cost the launch ~15.6 us against ~14.6 us for the two launches they replace (r04 A/B,
-// DESIGN.md §5), so the default keeps the three launches
-static bool epilogue_wanted(const mppi_handle *h)
-{
-    if (!env_switches().epilogue) return false;
-    return h->d_ep_sync && !sharded(h) && h->sg_window == 0 && h->timing < 2 && !h->graph_mode && !h->graph_dry &&
-           draw_ahead_possible(h) && !h->d_trace;
-}
-
 static WGradArgs wgrad_args(const mppi_handle *h);
 static FinishArgs finish_args(mppi_handle *h);
 
@@ -1595,7 +1519,6 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
     h->tail_drawn = false;
-    h->ep_ran = false;
     if (h->host_trace && h->ht_n[0] > h->ht_n[1]) {
         h->ht_sum[1] += std::chrono::duration<double, std::micro>(h->t_start - h->ht_ret).count();
         h->ht_n[1]++;
@@ -1636,14 +1559,14 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
     }
     // the stable order of the previous costs was ranked behind the previous publish (phase 3)
     // phase-split callers all-reduce d_costs in place: clear the other ranks' slots first
-    if (h->world > 1 && !h->comm) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)h->R * sizeof(double), h->stream));
+    // (R + 1: slot R carries the ranks' in-launch wait timeouts, which the caller all-reduces too)
+    if (h->world > 1 && !h->comm) HIP_TRY(hipMemsetAsync(h->d_costs, 0, (size_t)(h->R + 1) * sizeof(double), h->stream));
     // this update's draws were made ahead (behind the previous publish) when nothing they depend
     // on changed since; else the cooperative update launch may sample its own rows (opt-in)
     const bool ahead = h->ahead_valid && draw_ahead_possible(h) && h->ahead.update_index == h->update_count &&
                        h->ahead.seed == h->seed && h->ahead.begin == h->begin && h->ahead.count == h->count &&
                        h->ahead.H == h->H && h->ahead.C == h->C;
     h->ahead_valid = false;
-    const bool fuse = ahead || fuse_sampling(h);
     SampleArgs sa{};
     {   // eps of this update into the other buffer; the kept rollouts read the previous one
         std::swap(h->d_noise, h->d_noise_prev);
@@ -1665,10 +1588,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         sa.X = (int)h->X;
         if (h->tdiag)
             for (int64_t c = 0; c < h->C && c < FR_C; c++) sa.tdv[c] = h->T[(size_t)(c * h->C + c)];
-        if (!fuse) HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
+        if (!ahead) HIP_TRY(launch_sample(sa, h->tdiag, h->stream));
     }
     // timing level 1 with the cooperative kernel: the rollout launch records its own events
-    const bool ev_in_launch = h->timing == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h);
+    const bool ev_in_launch = h->timing == 1 && h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK;
     // the rollout launch's event pair: the ring's next pair at level 1, ev[1] / ev_dyn at level 2
     hipEvent_t ev_r0 = h->ev[1], ev_r1 = h->ev_dyn;
     if (h->timing == 1) {
@@ -1700,20 +1623,21 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
         a.rec = h->d_rec;
-        a.wait_sum = h->comm ? h->d_costs_local + h->R : nullptr;
+        // sharded: this rank's wait timeouts into cost slot R, which the all-reduce carries to every rank
+        a.wait_sum = h->comm ? h->d_costs_local + h->R : (sharded(h) ? h->d_costs + h->R : nullptr);
         if (h->debug_updates > 0) {   // mppi_debug_inject: this update's launch carries the fault
             a.debug = h->debug_flags;
             h->debug_updates--;
         }
-        if (fuse) {   // U*_shifted read from U* with the shift; the state from the launch
-            a.fuse_sample = ahead ? 2 : 1;
+        if (ahead) {   // U*_shifted read from U* with the shift; the state from the launch
+            a.drawn_ahead = 1;
             a.samp = sa;
             a.Ushift = sp.shift_by > 0 ? h->d_U : h->d_Us;
             a.ush = sp.shift_by > 0 ? (int)std::min<int64_t>(sp.shift_by, h->H) : 0;
         }
         // a pending filter() not folded here stays pending: this update's phase 3 supersedes it,
         // and only the latest one is observable (mppi_optimal_cost / logger)
-        const bool fold = use_coop(h) && h->opt_state == mppi_handle::OPT_PENDING;
+        const bool fold = h->opt_state == mppi_handle::OPT_PENDING;
         if (fold) {   // the previous update's filter() as one more row of the remainder launch
             a.fx0 = h->d_x0_opt;
             a.fU = h->d_U;
@@ -1721,57 +1645,28 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             a.fcost = h->d_opt;
             a.frec = h->d_rec_opt;
         }
-        if (!h->graph_mode && !h->graph_dry && !env_switches().relay2_off) {   // (launch_fr_coop_update decides)
-            a.relay_buf = h->d_relay_buf;
-            a.relay_flag = h->d_relay_flag;
-            a.relay_epoch = ++h->relay_epoch;
-        }
         bool folded = false, costs_done = false, tail = false;
         CoopTail ct;
         a.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
-        // optimise() and finish() in the launch's epilogue (launch_fr_coop_update takes it where the
-        // launch shape allows: one round of fr_coop_x_kernel with the draws made ahead)
-        a.epilogue = epilogue_wanted(h) ? 1 : 0;
-        if (a.epilogue) {
-            a.ep_sync = h->d_ep_sync;
-            a.ep_target = h->ep_total;
-            a.ep_stamps = h->d_ep_stamps;
-            EpArgs &ea = *h->h_ep_args;   // (the previous update's copy has run: its launch published)
-            ea.wg = wgrad_args(h);
-            ea.fin = finish_args(h);   // its sequence: publish_seq + 1, as phase 3 publishes it
-            ea.fin.rank_n = h->R;      // draw_ahead_possible: S <= RANK_TILED_MAX, rank_draw_kernel's tiles
-            HIP_TRY(hipMemcpyAsync(h->d_ep_args, h->h_ep_args, sizeof(EpArgs), hipMemcpyHostToDevice, h->stream));
-            a.ep = h->d_ep_args;
-            // a filter() launched by itself on the side stream reads the d_U / d_x0_opt the epilogue rewrites
-            if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
-        }
         // the next update's draws in the launch's tail, into the buffer it will write (phase 3 makes
-        // the rest with the rank); needs the sampling arguments (fused launch) and no tail switch-off
-        a.ahead_noise = (fuse && draw_ahead_possible(h) && !tail_draws_disabled()) ? h->d_noise_prev : nullptr;
-        if (use_coop(h)) {
-            HIP_TRY(launch_fr_coop_update(a, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
-                                          &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry, &ct,
-                                          &h->gargs.roll2));
-            h->gargs.folded = folded;
-            h->gargs.nroll = ct.launches;
-            h->ep_ran = !h->graph_dry && h->gargs.roll.epilogue != 0;
-            if (h->ep_ran) h->ep_total = h->gargs.roll.ep_target;
-            if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
-            if (!folded) a.fcost = nullptr;
-            if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
-        } else {
-            HIP_TRY(launch_fr_rollout(a, h->stream));
-            if (h->timing >= 1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
-        }
+        // the rest with the rank); needs the draws made ahead and no tail switch-off
+        a.ahead_noise = (ahead && !tail_draws_disabled(h)) ? h->d_noise_prev : nullptr;
+        HIP_TRY(launch_fr_coop_update(a, h->env, h->stream, ev_in_launch ? ev_r0 : nullptr, ev_in_launch ? ev_r1 : nullptr,
+                                      &folded, &costs_done, &tail, &h->gargs.roll, &h->gargs.x_kernel, h->graph_dry, &ct,
+                                      &h->gargs.roll2));
+        h->gargs.folded = folded;
+        h->gargs.nroll = ct.launches;
+        if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
+        if (!folded) a.fcost = nullptr;
+        if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
         h->tail_drawn = tail;
-        h->info[MPPI_INFO_COOPERATIVE] = use_coop(h) ? 1 : 0;
+        h->info[MPPI_INFO_COOPERATIVE] = 1;
         h->info[MPPI_INFO_FOLDED_FILTER] = folded ? 1 : 0;
         h->info[MPPI_INFO_OBJECTIVE_IN_LAUNCH] = costs_done ? 1 : 0;
         h->info[MPPI_INFO_TAIL_DRAWS] = tail ? 1 : 0;
-        h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : (fuse ? 1 : 0);
+        h->info[MPPI_INFO_SAMPLING] = ahead ? 2 : 0;
         h->info[MPPI_INFO_ROWS] = h->count + (folded ? 1 : 0);
         h->info[MPPI_INFO_HANDOVER] = h->gargs.x_kernel ? -2 : -1;   // -2: read from the device on request
-        h->info[MPPI_INFO_FUSED_UPDATE] = h->ep_ran ? 1 : 0;
         if (tail) {   // the rows the launch left to rank_draw_kernel (fr_coop.hip relay_stage, group_draws)
             h->tail_row0 = ct.row0;
             h->tail_xbase = ct.xbase;
@@ -1843,7 +1738,7 @@ static FinishArgs finish_args(mppi_handle *h)
     f.rank_zero = h->d_rank;
     f.rank_n = h->S <= RANK_TILED_MAX ? h->R : 0;
     f.stats_reset = h->d_cstats;
-    f.wait_all = h->comm ? h->d_costs + h->R : nullptr;
+    f.wait_all = sharded(h) ? h->d_costs + h->R : nullptr;   // (phase-split callers: cleared by phase 1)
     f.wait_local = h->comm ? h->d_costs_local + h->R : nullptr;
     return f;
 }
@@ -1872,8 +1767,6 @@ mppi_status mppi_update_phase2(mppi_handle *h)
 {
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
-    h->wf_fused = false;
-    if (h->ep_ran) return MPPI_OK;   // optimise() ran in the rollout launch's epilogue
     WGradArgs w{};
     w.cost = h->d_costs;
     w.R = h->R;
@@ -1891,12 +1784,8 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     h->gargs.wg = w;
     if (h->graph_dry) return MPPI_OK;
-    // optimise() and finish() as one launch where it applies: phase 3 launches it (its arguments
-    // include the publish sequence).  Sharded: the partial gradient is summed here and all-reduced
-    // before phase 3.
-    // (opt-in, MPPI_WEIGHTS_FINISH=1: measured slower)
-    h->wf_fused = env_switches().weights_finish && !h->graph_mode && weights_finish_eligible(w, finish_args(h));
-    if (!h->wf_fused) HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
+    // sharded: the partial gradient is summed here and all-reduced before phase 3
+    HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_wg, h->stream));
     return MPPI_OK;
 }
@@ -1908,17 +1797,11 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     h->gargs.fin = finish_args(h);
-    if (!h->graph_dry && !h->ep_ran) {   // (or in the epilogue)
-        if (h->wf_fused) {
-            HIP_TRY(launch_weights_finish(h->gargs.wg, h->gargs.fin, h->d_wf_ticket, h->stream));
-            h->info[MPPI_INFO_FUSED_UPDATE] = 2;
-        }
-        else HIP_TRY(launch_finish(h->gargs.fin, h->stream));
-    }
+    if (!h->graph_dry) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
     const double seq = (double)(++h->publish_seq);
     *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
-    const bool standalone_filter = !(h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK && use_coop(h));
+    const bool standalone_filter = h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK;
     if (standalone_filter) HIP_TRY(hipEventRecord(h->ev_pub, h->stream));   // the side stream waits on it
     // filter(): cost of the published U* (mppi.cpp:450-479).  With the cooperative kernel it rides
     // in the next update's remainder launch (it then shares a SIMD with rollouts 0 and 1 instead of
@@ -2023,37 +1906,6 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
     h->update_last = h->rollout_time;
     ++h->update_count;
     h->published_once = true;   // a filter() row exists from here on (mppi_optimal_terms)
-    if (h->d_ep_stamps && h->ep_ran) {   // diagnostics: the epilogue's phases (s_memrealtime, 100 MHz)
-        std::vector<uint64_t> sv((size_t)h->ep_stamp_groups * EP_STAMPS);
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipMemcpy(sv.data(), h->d_ep_stamps, sv.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        uint64_t first = ~0ull, last_arr = 0, pass = 0, stored = 0, pub = 0, fin[4] = {0, 0, 0, 0};
-        for (unsigned b = 0; b < h->ep_stamp_groups; b++) {
-            const uint64_t *v = &sv[(size_t)b * EP_STAMPS];
-            if (!v[0]) continue;
-            first = std::min(first, v[0]);
-            last_arr = std::max(last_arr, v[0]);
-            pass = std::max(pass, v[1]);
-            stored = std::max(stored, v[2]);
-            pub = std::max(pub, v[3]);
-            for (int i = 0; i < 4; i++) fin[i] = std::max(fin[i], v[4 + i]);
-        }
-        if (last_arr) {
-            h->ep_stamp_sum[0] += (double)(last_arr - first) * 0.01;   // spread of the arrivals
-            h->ep_stamp_sum[1] += (double)(pass - last_arr) * 0.01;    // barrier release
-            h->ep_stamp_sum[2] += (double)(stored - pass) * 0.01;      // units (the weight reduce)
-            h->ep_stamp_sum[3] += (double)(pub - stored) * 0.01;       // ticket + finish + publish
-            if (fin[0]) {   // the finisher: ticket, loads, compute + stores issued, stores acknowledged, flag
-                h->ep_stamp_sum[4] += (double)(fin[0] - stored) * 0.01;
-                h->ep_stamp_sum[5] += (double)(fin[1] - fin[0]) * 0.01;
-                h->ep_stamp_sum[6] += (double)(fin[2] - fin[1]) * 0.01;
-                h->ep_stamp_sum[7] += (double)(fin[3] - fin[2]) * 0.01;
-                h->ep_stamp_sum[8] += (double)(pub - fin[3]) * 0.01;
-            }
-            h->ep_stamp_n++;
-        }
-        HIP_TRY(hipMemset(h->d_ep_stamps, 0, sv.size() * sizeof(uint64_t)));
-    }
     if (h->host_trace) {
         h->ht_ret = std::chrono::steady_clock::now();
         h->ht_sum[0] += std::chrono::duration<double, std::micro>(h->ht_ret - h->ht_flag).count();
@@ -2083,13 +1935,13 @@ mppi_status mppi_update_phase3(mppi_handle *h)
 static bool graph_eligible(const mppi_handle *h)
 {
     if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
-    if (!draw_ahead_possible(h) || tail_draws_disabled() || !fr_coop_costs_in_launch()) return false;
+    if (!draw_ahead_possible(h) || tail_draws_disabled(h) || !fr_coop_costs_in_launch(h->env)) return false;
     if (h->fc.type != FC_NONE || h->S > RANK_TILED_MAX) return false;   // SG: sg_finish_kernel is the finish node
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
     // the launch path the replayed nodes assume: fr_coop_x_kernel with the filter() row folded and
     // the objective in the launch (a rollout count that is a multiple of 16 takes fr_coop_kernel<4>
     // with filter() left pending, a horizon past 128 steps adds the cost kernel)
-    if (!fr_coop_update_folds(h->count, (int)h->H) || h->debug_updates > 0) return false;
+    if (!fr_coop_update_folds(h->count, (int)h->H, h->env) || h->debug_updates > 0) return false;
     return h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
            h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
 }
@@ -2216,7 +2068,7 @@ mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count)
 // transform, unsharded, no smoothing, timing off or level 1 (MPPI_PM_FUSED=0: the five launches)
 static bool pm_fused_eligible(const mppi_handle *h)
 {
-    if (env_switches().pm_fused_off) return false;
+    if (h->env.pm_fused_off) return false;
     return h->dyn_kind == MPPI_DYNAMICS_POINT_MASS && h->d_pm_sync && h->noise_source == MPPI_NOISE_DEVICE_PHILOX &&
            h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->host_trace && !h->d_trace;
 }
@@ -2265,7 +2117,7 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     a.tpart = h->d_pm_part + (size_t)h->pm_nblocks * (size_t)(h->H * h->C);
     a.bar = h->d_pm_sync;
     a.ticket = h->d_pm_sync + 1;
-    a.epoch = ++h->pm_epoch;
+    a.epoch = h->pm_epoch + 1;   // committed once the launch is queued (the counters then reach it)
     a.nblocks = h->pm_nblocks;
     a.cost_scale = h->cost_scale;
     a.gradient_step = h->gradient_step;
@@ -2296,6 +2148,7 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
         HIP_TRY(hipEventRecord(ev_r0, h->stream));
     }
     HIP_TRY(launch_pm_update(a, h->stream));
+    h->pm_epoch = a.epoch;
     if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
     // filter() of this update is left pending (as phase 3 leaves the cooperative launch's); the next
     // update's draws are in d_noise_prev
@@ -2450,7 +2303,7 @@ mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
 mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
 {
     if (!h || !terms7) return MPPI_ERR_INVALID;
-    if (h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION || !use_coop(h))
+    if (h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION)
         return fail(h, MPPI_ERR_UNSUPPORTED, "per-term totals: AssistedManipulation on the cooperative kernel only");
     HIP_TRY(hipSetDevice(h->device));
     if (!h->published_once) {   // before the first update that published: reset(0), no filter() row yet

@@ -66,17 +66,6 @@ constexpr int NSLOT = FR_NB + 1;   // + a dummy body slot that lanes 12..15 stor
 // slots) are 144 B and 80 B: their 16-byte stores then start at 36 j and 20 j (mod 64) dwords,
 // sixteen disjoint four-bank groups per row.  With 128 B / 64 B strides the lanes of a row fell
 // on two / four bank groups (8- / 4-way conflicts on the solve's transpose and the S stores).
-#ifdef LDS_NOPAD
-constexpr int CSTR = ROW;
-constexpr int L_I = 0;
-constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x CSTR) over L_I
-constexpr int L_TP = L_COL + 16 * CSTR;     // no tank: the solved right-hand side (12)
-constexpr int L_S = 274;                    // 16-byte aligned; per slot S (6), qd, pad
-constexpr int S_STR = 8;
-constexpr int LDS_KIN = 400;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
-constexpr int L_F = 378;                    // energy tank: spatial force f of each body slot
-constexpr int LDS_KIN_EN = 464;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
-#else
 constexpr int CSTR = 18;
 constexpr int L_I = 0;
 constexpr int L_COL = 0;                    // no tank: the mass-matrix block (16 x CSTR) over L_I
@@ -86,7 +75,6 @@ constexpr int S_STR = 10;
 constexpr int LDS_KIN = 432;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
 constexpr int L_F = 430;                    // energy tank: spatial force f of each body slot
 constexpr int LDS_KIN_EN = 528;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
-#endif
 constexpr int L_U = 0;
 constexpr int L_DU = L_U + FR_NB * ROW;
 constexpr int L_QDD = L_DU + FR_NB * 2;
@@ -123,8 +111,6 @@ template <int N>
 __device__ __forceinline__ double bcast(double x) { return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + N, 0xF, 0xF, true); }
 template <int S>
 __device__ __forceinline__ double shr(double x) { return dmov<0x110 + S>(x); }     // row_shr:S
-template <int S>
-__device__ __forceinline__ double shl(double x) { return dmov<0x100 + S>(x); }     // row_shl:S
 
 // acc + sum_{r<6} x[lane r] * y[r]: six v_fmac_f64_dpp row_newbcast:r (broadcast and multiply-add
 // in one instruction; the compiler does not form 64-bit DPP FMAs).  The leading s_nop covers the
@@ -144,17 +130,6 @@ __device__ __forceinline__ double bfma6(double x, const double *y, double acc)
         : "v"(x), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]));
     return acc;
 }
-#if defined(PHASE_TRACE) || defined(PHASE_FK)
-// diagnostics: shader-clock stamp once `dep` has been computed and the wave's LDS ops are done
-__device__ __forceinline__ uint64_t stamp(double dep)
-{
-    uint64_t t;
-    uint32_t tmp;
-    asm volatile("v_readfirstlane_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(t), "=s"(tmp) : "v"(__double2loint(dep)) : "memory");
-    return t;
-}
-#endif
 // c[k] += x[lane k] * y for k < 6 (the rank-1 update of the articulated inertia rows)
 __device__ __forceinline__ void bfma6_rank1(double x, double y, double *c)
 {
@@ -177,41 +152,6 @@ __device__ __forceinline__ double bsum<0, 6>(double x, double one)
 {
     const double ones[6] = {one, one, one, one, one, one};
     return bfma6(x, ones, 0.0);
-}
-template <>
-__device__ __forceinline__ double bsum<0, 10>(double x, double one)
-{
-    double acc = 0.0;
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf"
-        : "+&v"(acc)
-        : "v"(x), "v"(one));
-    return acc;
-}
-template <>
-__device__ __forceinline__ double bsum<3, 10>(double x, double one)
-{
-    double acc = 0.0;
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf"
-        : "+&v"(acc)
-        : "v"(x), "v"(one));
-    return acc;
 }
 template <>
 __device__ __forceinline__ double bsum<0, 12>(double x, double one)
@@ -254,19 +194,6 @@ __device__ __forceinline__ void bfma6_pair(double U, double P, const double *S, 
     D = d0;
     sp = p0;
 }
-// bfma6_pair as four chains of three (D and sp each split at row 3)
-__device__ __forceinline__ void bfma6_quad(double U, double P, const double *S, double &D, double &sp)
-{
-    double d0 = 0.0, p0 = 0.0, d1 = 0.0, p1 = 0.0;
-    asm("s_nop 1\n\t"
-        DPPF("%0", "%4", "%6", 0) DPPF("%1", "%5", "%6", 0) DPPF("%2", "%4", "%9", 3) DPPF("%3", "%5", "%9", 3)
-        DPPF("%0", "%4", "%7", 1) DPPF("%1", "%5", "%7", 1) DPPF("%2", "%4", "%10", 4) DPPF("%3", "%5", "%10", 4)
-        DPPF("%0", "%4", "%8", 2) DPPF("%1", "%5", "%8", 2) DPPF("%2", "%4", "%11", 5) DPPF("%3", "%5", "%11", 5)
-        : "+&v"(d0), "+&v"(p0), "+&v"(d1), "+&v"(p1)
-        : "v"(U), "v"(P), "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]));
-    D = d0 + d1;
-    sp = p0 + p1;
-}
 // sum over lanes 0..5 of x: two chains (lanes 0..2, 3..5)
 __device__ __forceinline__ double bsum6_split(double x, double one)
 {
@@ -278,22 +205,6 @@ __device__ __forceinline__ double bsum6_split(double x, double one)
         : "+&v"(a0), "+&v"(a1)
         : "v"(x), "v"(one));
     return a0 + a1;
-}
-// two sums over lanes 0..11, each split in two chains (lanes 0..5, 6..11): four chains
-__device__ __forceinline__ void bsum12_pair(double x, double y, double one, double &sx, double &sy)
-{
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    asm("s_nop 1\n\t"
-        DPPF("%0", "%4", "%6", 0) DPPF("%2", "%5", "%6", 0) DPPF("%1", "%4", "%6", 6) DPPF("%3", "%5", "%6", 6)
-        DPPF("%0", "%4", "%6", 1) DPPF("%2", "%5", "%6", 1) DPPF("%1", "%4", "%6", 7) DPPF("%3", "%5", "%6", 7)
-        DPPF("%0", "%4", "%6", 2) DPPF("%2", "%5", "%6", 2) DPPF("%1", "%4", "%6", 8) DPPF("%3", "%5", "%6", 8)
-        DPPF("%0", "%4", "%6", 3) DPPF("%2", "%5", "%6", 3) DPPF("%1", "%4", "%6", 9) DPPF("%3", "%5", "%6", 9)
-        DPPF("%0", "%4", "%6", 4) DPPF("%2", "%5", "%6", 4) DPPF("%1", "%4", "%6", 10) DPPF("%3", "%5", "%6", 10)
-        DPPF("%0", "%4", "%6", 5) DPPF("%2", "%5", "%6", 5) DPPF("%1", "%4", "%6", 11) DPPF("%3", "%5", "%6", 11)
-        : "+&v"(a0), "+&v"(a1), "+&v"(b0), "+&v"(b1)
-        : "v"(x), "v"(y), "v"(one));
-    sx = a0 + a1;
-    sy = b0 + b1;
 }
 static_assert(FR_EE_PARENT == 9 && FR_ARM0 == 3 && FR_ARM1 == 10, "kinematic sum ranges");
 
@@ -693,255 +604,6 @@ __device__ __forceinline__ void gj_pivot_11(double *Mc, double nt)
         : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10])
         : "v"(nt));
 }
-// the same pivots without the pipelining (GJ_SERIAL builds, A/B)
-// pivot 0 (d = the composite mass of body 0; inv = 1 / d)
-__device__ __forceinline__ void gj_serial_pivot_0(double *Mc, double inv)
-{
-    const double nt = -Mc[0] * inv;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 1 (d = the composite mass of body 1; inv = 1 / d)
-__device__ __forceinline__ void gj_serial_pivot_1(double *Mc, double inv)
-{
-    const double nt = -Mc[1] * inv;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[2]), "+v"(Mc[0]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 2
-__device__ __forceinline__ void gj_serial_pivot_2(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[2]));
-    const double nt = neg_quot(Mc[2], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[3]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 3
-__device__ __forceinline__ void gj_serial_pivot_3(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[3]));
-    const double nt = neg_quot(Mc[3], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[4]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 4
-__device__ __forceinline__ void gj_serial_pivot_4(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[4]));
-    const double nt = neg_quot(Mc[4], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[5]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 5
-__device__ __forceinline__ void gj_serial_pivot_5(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[5]));
-    const double nt = neg_quot(Mc[5], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[6]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 6
-__device__ __forceinline__ void gj_serial_pivot_6(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[6]));
-    const double nt = neg_quot(Mc[6], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[7]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 7
-__device__ __forceinline__ void gj_serial_pivot_7(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[7]));
-    const double nt = neg_quot(Mc[7], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[8]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 8
-__device__ __forceinline__ void gj_serial_pivot_8(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[8]));
-    const double nt = neg_quot(Mc[8], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[9]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[10]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 9
-__device__ __forceinline__ void gj_serial_pivot_9(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[9]));
-    const double nt = neg_quot(Mc[9], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[10]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[11])
-        : "v"(nt));
-}
-// pivot 10
-__device__ __forceinline__ void gj_serial_pivot_10(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[10]));
-    const double nt = neg_quot(Mc[10], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9])
-        : "v"(nt));
-}
-// pivot 11
-__device__ __forceinline__ void gj_serial_pivot_11(double *Mc)
-{
-    double d;
-    asm("v_mov_b64_dpp %0, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(d) : "v"(Mc[11]));
-    const double nt = neg_quot(Mc[11], d);
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10])
-        : "v"(nt));
-}
 // ---- END generated by tools/gen_gj.py ----
 
 // The third column of a rotation in delta form (D = R - I, row-major) from its first two, r2 = r0 x r1:
@@ -1112,15 +774,12 @@ struct LaneConst {
     bool vsum;      // the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
     // opaque lane masks (0 / -1) for msel, built once before the horizon loop
     int m_vsum;     // vsum
-    int m_j0, m_j1, m_j2, m_j10, m_j12, m_j13, m_j14, m_j15;   // j == n
+    int m_j0, m_j1, m_j2, m_j12, m_j13, m_j14, m_j15;   // j == n
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
-    int anc;        // bit i: body i is an ancestor of body j (i < j, finger 11 not under finger 10)
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
-#ifndef CI_SCAN
     double desc[10];   // composite_dpp: 1.0 when body i + 2 is in the subtree of body j (lanes 0, 1: all)
-#endif
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
 };
@@ -1128,14 +787,8 @@ struct LaneConst {
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
 template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
-                                        double *Lk, CoopKin &kin, CoopBody &bd, const double *grav, uint64_t *phf = nullptr)
+                                        double *Lk, CoopKin &kin, CoopBody &bd, const double *grav)
 {
-#ifdef PHASE_FK
-#define FKSTAMP(i, dep) if (phf) { const uint64_t t_ = stamp(dep); phf[i] += t_ - phf[4]; phf[4] = t_; }
-    FKSTAMP(0, q)
-#else
-#define FKSTAMP(i, dep)
-#endif
     const double cz = __builtin_fma(L.rz, cq, L.nrz);   // cq on revolute lanes, 1 elsewhere
     const double sz = L.rz * sq;                         // sq on revolute lanes, 0 elsewhere
     const double qprev = shr<1>(q);
@@ -1151,19 +804,11 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     D[0] -= 1.0;
     D[4] -= 1.0;
     D[8] -= 1.0;
-    FKSTAMP(0, D[8])
-#ifndef ABL_NOSCAN   // instruction-count ablations (compile-only probes, tools/isa_regions.sh)
     scan_level2<1>(D, p);
     scan_level2<2>(D, p);
     scan_level2<4>(D, p);
-#ifdef FK_SCAN8
-    scan_level2<8>(D, p);
-#else
     scan_level_planar8(D, p);
-#endif
-#endif
     delta_col2(D);
-    FKSTAMP(1, p[2])
     double R[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) R[k] = D[k];
@@ -1182,30 +827,8 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     S[4] = w[1] * rotf;
     S[5] = w[2] * rotf;
     double com[3], Iw[6], Ib[6];
-#ifdef ABL_NOWI
-    for (int k = 0; k < 3; k++) com[k] = p[k];
-    for (int k = 0; k < 6; k++) Iw[k] = Ib[k] = R[k];
-#else
     world_inertia(M, R, p, com, Iw, Ib);
-#endif
-#ifdef OLD_ABA
-    inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);
-#else
     if constexpr (EN) inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);   // coop_aba's input
-#endif
-#ifdef DUMMY_BODY0
-    {
-        const double live = M[T_NROT] + M[T_ROT];   // 1 for a real body, 0 on lanes 12..15
-        bd.m = M[T_M] * live;
-#pragma unroll
-        for (int k = 0; k < 3; k++) bd.h[k] = (M[T_M] * com[k]) * live;
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            bd.Ib[k] = Ib[k] * live;
-            bd.S[k] = S[k];
-        }
-    }
-#else
     {   // lanes 12..15: the table's dummy body has zero mass and inertia, so h = Ib = 0 there
         bd.m = M[T_M];
 #pragma unroll
@@ -1216,7 +839,6 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
             bd.S[k] = S[k];
         }
     }
-#endif
 #pragma unroll
     for (int k = 0; k < 6; k++) Lk[L_S + L.slot * S_STR + k] = S[k];
     Lk[L_S + L.slot * S_STR + 6] = qd;
@@ -1264,7 +886,6 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         for (int k = 0; k < 6; k++) Lk[L_F + L.slot * 6 + k] = f[k];
         kin.pw = ((f[0] * V[0] + f[1] * V[1]) + f[2] * V[2]) + ((f[3] * V[3] + f[4] * V[4]) + f[5] * V[5]);
     }
-    FKSTAMP(2, bd.S[5])
     double fpos[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) fpos[r] = p[r] + ((R[3 * r] * M[T_F] + R[3 * r + 1] * M[T_F + 1]) + R[3 * r + 2] * M[T_F + 2]);
@@ -1278,9 +899,6 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     // The frame velocity J v over the EE chain (bodies 0..9) and J_a J_a^T over the arm (bodies
     // 3..9): nine sums, lane m computes sum m from the S / qd slots the row just wrote to LDS
     // (ten LDS-read FMAs per lane instead of 72 DPP-broadcast FMAs that every lane repeats).
-#ifdef ABL_NOKIN
-    return;
-#endif
     const double *xs = Lk + L_S + L.ka, *ys = Lk + L_S + L.kb;
     double acc = 0.0;
 #pragma unroll
@@ -1290,8 +908,6 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         acc = __builtin_fma(xs[i * S_STR], y, acc);
     }
     kin.ks = acc;
-    FKSTAMP(3, acc)
-#undef FKSTAMP
 }
 
 // Articulated-body passes over the world inertias / S staged in LDS (energy-tank rollouts, whose
@@ -1302,7 +918,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
 // parent's own inertia added before the update.  Forward pass per level: qdd_i = (u_i - U_i . a_p)
 // / D_i, a_i = a_p + S_i qdd_i.
 template <bool EN>
-__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, double &pe, uint64_t &t_bwd)
+__device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, double &pe)
 {
     const int r = j < 6 ? j : 5;   // lanes 0..5 hold rows 0..5; the others mirror row 5, unused
     int off[6];
@@ -1337,11 +953,7 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         // D = S.U and S.pA: rows 0..5 broadcast from lanes 0..5, every lane holds S
         double D, sp;
         bfma6_pair(U, pAr, S, D, sp);
-#ifdef ABL_RCP1
-        const double Dinv = __builtin_amdgcn_rcp(D);
-#else
         const double Dinv = frcp(D);
-#endif
         const double u = tau - sp;
         Lw[L_U + i * ROW + j] = U;
         Lw[L_DU + 2 * i] = Dinv;
@@ -1369,9 +981,6 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
         }
     }
     pe = 0.0;
-#ifdef PHASE_TRACE
-    t_bwd = stamp(pA);
-#endif
     {
         double acc = 0.0, a9 = 0.0;
         double Srf = Lk[L_S + r], Uf = Lw[L_U + j], Dvf = Lw[L_DU], uf = Lw[L_DU + 1];
@@ -1407,6 +1016,11 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 // constant composite mass on the diagonal (S_0, S_1 unit translations), whatever h and Ib hold.
 // Ninety v_fmac_f64_dpp in nine interleaved chains replace the four-level suffix scan (72 DPP
 // moves, 36 adds) and finger 10's select (18).  (r04)
+// The second asm block has no leading s_nop: the scheduler may place it right behind the first, and
+// a VALU write the compiler puts between them to one of its sources would be a VALU-write ->
+// DPP-read hazard the compiler does not see.  tools/dpp_hazard_check.py scans every build's
+// assembly for exactly that (fewer than two wait states between a VALU write and a DPP read of the
+// same VGPR) and fails the build, so the nop is only spent where a build would need it.
 __device__ __forceinline__ void composite_dpp(const double *x, const double *desc, double *v)
 {
 #pragma unroll
@@ -1521,33 +1135,14 @@ __device__ __forceinline__ void composite_dpp(const double *x, const double *des
 //                       LDS.  Lane 12 holds the right-hand side tau.
 //   Gauss-Jordan        twelve pivots, each one broadcast of the pivot, a reciprocal and eleven
 //                       broadcast FMAs per lane; then qdd_j = tau'_j / M'_jj.
-__device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const CoopBody &bd, double tau_l, double *Lk,
-                                             uint64_t &t_mid)
+__device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const CoopBody &bd, double tau_l, double *Lk)
 {
     // (h, Ib) summed over the subtree; the subtree's mass is a per-lane constant of the body table (T_MC)
     double v[9] = {bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
-#ifndef CI_SCAN
     {
         const double x[9] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
         composite_dpp(x, L.desc, v);
     }
-#else   // round 3: suffix scan over the lanes (row_shl 1, 2, 4, 8), finger 10 its own subtree
-    double own[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) own[k] = v[k];
-#ifndef ABL_NOISCAN
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] += shl<1>(v[k]);
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] += shl<2>(v[k]);
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] += shl<4>(v[k]);
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] += shl<8>(v[k]);
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] = msel(L.m_j10, v[k], own[k]);
-#endif
-#endif
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
     const double m = L.mc, h0 = v[0], h1 = v[1], h2 = v[2];
@@ -1560,20 +1155,12 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     F[4] = (h2 * S[0] - h0 * S[2]) + ((I01 * S[3] + I11 * S[4]) + I12 * S[5]);
     F[5] = (h0 * S[1] - h1 * S[0]) + ((I02 * S[3] + I12 * S[4]) + I22 * S[5]);
     double Mc[12];
-#ifdef ABL_NOCD
-    for (int i = 0; i < 11; i++) Mc[i] = F[i % 6];
-#else
     column_dots(S, F, Mc);
-#endif
     const double diag = ((S[0] * F[0] + S[1] * F[1]) + (S[2] * F[2] + S[3] * F[3])) + (S[4] * F[4] + S[5] * F[5]);
     // strictly-upper part of column j: M_ij for the ancestors i of j (finger 11 hangs off body 9,
     // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column
 #pragma unroll
-#ifdef ANC_BFI
-    for (int i = 0; i < 11; i++) Mc[i] = msel(__builtin_amdgcn_sbfe(L.anc, i, 1), 0.0, Mc[i]);
-#else
     for (int i = 0; i < 11; i++) Mc[i] *= L.ancd[i];
-#endif
     Mc[11] = 0.0;
     // row j of the block: that column, then tau_j and zeros in slots 12..15, then the diagonal over
     // slot j (LDS stores of a wave land in order).  Entry (i, j) of the block is then column i's
@@ -1588,21 +1175,11 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     Row[j] = diag;
 #pragma unroll
     for (int i = 0; i < 12; i++) Mc[i] += Lk[L_COL + i * CSTR + j];
-#ifdef PHASE_TRACE
-    t_mid = stamp(Mc[0]);   // mass matrix formed: "backward" = CRBA, "forward" = Gauss-Jordan
-#endif
-#ifdef ABL_NOGJ
-#elif defined(GJ_SERIAL)
-    gj_serial_pivot_0(Mc, L.inv_m0); gj_serial_pivot_1(Mc, L.inv_m1); gj_serial_pivot_2(Mc); gj_serial_pivot_3(Mc);
-    gj_serial_pivot_4(Mc); gj_serial_pivot_5(Mc); gj_serial_pivot_6(Mc); gj_serial_pivot_7(Mc); gj_serial_pivot_8(Mc);
-    gj_serial_pivot_9(Mc); gj_serial_pivot_10(Mc); gj_serial_pivot_11(Mc);
-#else
     double nt = -Mc[0] * L.inv_m0;   // each pivot's block returns the next pivot's quotient
     nt = gj_pivot_0(Mc, nt, L.inv_m1);
     nt = gj_pivot_1(Mc, nt); nt = gj_pivot_2(Mc, nt); nt = gj_pivot_3(Mc, nt); nt = gj_pivot_4(Mc, nt);
     nt = gj_pivot_5(Mc, nt); nt = gj_pivot_6(Mc, nt); nt = gj_pivot_7(Mc, nt); nt = gj_pivot_8(Mc, nt);
     nt = gj_pivot_9(Mc, nt); nt = gj_pivot_10(Mc, nt); gj_pivot_11(Mc, nt);
-#endif
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
     // tau' at L_TP and every other lane its column in its own block row (read above, dead now), so
     // lane j reads M'_jj back at slot j of that row: no per-lane register select, no branch.
@@ -1641,15 +1218,9 @@ __global__ void fr_body_table_kernel(const DevModel *model, const DevCost *cost,
         double v;
         if (f < T_P) v = Rs[f];
         else if (f < T_M) v = ps[f - T_P];
-#ifdef DUMMY_BODY0
-        else if (f == T_M) v = db.mass;
-        else if (f < T_I) v = db.c[f - T_C];
-        else if (f < T_F) v = db.Ic[f - T_I];
-#else
         else if (f == T_M) v = live * db.mass;   // the dummy body (lanes 12..15) is massless:
         else if (f < T_I) v = live * db.c[f - T_C];   // its world inertia, F and M column vanish
         else if (f < T_F) v = live * db.Ic[f - T_I];
-#endif
         else if (f < T_MA) v = (b == FR_EE_PARENT) ? dm.ee_p[f - T_F] : ((b == FR_AM_PARENT) ? dm.am_p[f - T_F] : 0.0);
         else if (f < T_AX) {
             const int r = f - T_MA;
@@ -1684,21 +1255,10 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
 // step's basic block): lanes 0..11 write (q_j, qd_j) and lanes 12..15 the EE / arm-mount
 // positions and the tank energy (one 16-byte store), then lane j writes kinematic sum min(j, 8)
 // (lanes 9..15 repeat lane 8: same address, same value).
-// vreg: a register value the optimiser cannot trace back to a memory location (keeps the record
-// selects as v_cndmask instead of a dynamically indexed private copy of CoopKin)
-__device__ __forceinline__ double vreg(double x)
-{
-    asm("" : "+v"(x));   // not volatile: a volatile asm would end the scheduling region here
-    return x;
-}
 template <bool EN>
 __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst &L, double q, double qd, const CoopKin &kin,
                                              double E)
 {
-#ifdef ABL_NOREC
-    return;
-#endif
-#ifndef REC_SELECT
     if constexpr (!EN) {
         // Without the tank E = 0, and the dummy lanes 12..15 hold q = qd = 0: they store their pair
         // over slots 30..31 (E, pad), which hold zeros either way, so no select builds their part of
@@ -1714,7 +1274,6 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
         rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
         return;
     }
-#endif
     double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
     a0 = msel(L.m_j13, a0, kin.ee[2]);
     a1 = msel(L.m_j13, a1, kin.am[0]);
@@ -1758,9 +1317,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         a.trace[4 * wblk + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         a.trace[4 * wblk + 2] = hw;
-#ifndef PRO_TRACE
         a.trace[4 * wblk + 3] = xcc;
-#endif
     }
 #endif
     // FROW: the row after the last rollout is the previous update's filter() (optimal rollout)
@@ -1769,7 +1326,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     if (!live) return -1;   // row-uniform: the row's lanes leave together (no DPP partner is lost)
     const int H = a.H;
     const bool opt_row = a.optimal || frow;   // no noise (mppi.cpp:450-479)
-    // U*_shifted row k is Up row min(k + ush, H - 1): with fused sampling (a.fuse_sample) the
+    // U*_shifted row k is Up row min(k + ush, H - 1): with the draws made ahead (a.drawn_ahead) the
     // shift reads U* itself (mppi.cpp:197-207); the state staged in LDS (stage_x0)
     const double *x0p = FROW && frow ? a.fx0 : Lx0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
@@ -1798,7 +1355,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     L.m_j0 = opaque_mask(j == 0);
     L.m_j1 = opaque_mask(j == 1);
     L.m_j2 = opaque_mask(j == 2);
-    L.m_j10 = opaque_mask(j == 10);
     L.m_j12 = opaque_mask(j == 12);
     L.m_j13 = opaque_mask(j == 13);
     L.m_j14 = opaque_mask(j == 14);
@@ -1809,7 +1365,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         int anc = (1 << (j < 11 ? j : 11)) - 1;   // bodies i < j
         if (j == FR_NB - 1) anc &= ~(1 << (FR_NB - 2));   // finger 11 is not under finger 10
         asm volatile("" : "+v"(anc));
-        L.anc = anc;
         int ro = j < FR_NB ? 2 * j : REC_E;
         asm volatile("" : "+v"(ro));
         L.rec_off = ro;
@@ -1819,7 +1374,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
             L.ancd[i] = d;
         }
-#ifndef CI_SCAN
 #pragma unroll
         for (int i = 2; i < FR_NB; i++) {
             const bool in = j < 2 || (j < FR_NB - 2 && i >= j) || i == j;   // fingers: themselves
@@ -1827,7 +1381,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             asm volatile("" : "+v"(d));
             L.desc[i - 2] = d;
         }
-#endif
     }
     L.mc = M[T_MC];
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
@@ -1861,31 +1414,17 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     int64_t nstride = sampled ? a.Rpad * FR_C : 0;   // unsampled rows re-read their first element
     asm volatile("" : "+v"(nstride));
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
-#ifdef NO_EPS_PREFETCH
-    store_record<EN>(recp(0), j, L, q, qd, kin, E);
-    for (int k = 0; k < H - 1; k++) {
-        const double eps_l = np[(int64_t)k * nstride];
-        const double ub_l = Up[min(k + ush, H - 1) * FR_C + jb];
-#else
     // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
     // whose latency a single wave per SIMD cannot hide within one step
     // (issued before the first record store: the loop header then waits for the loads alone,
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
     if (kb == 0) store_record<EN>(recp(0), j, L, q, qd, kin, E);
-#ifdef PHASE_FK
-    uint64_t phf[5] = {0, 0, 0, 0, 0};   // cycles: FK pre-scan, scan, inertia + S + LDS, EE + kinematic sums
-#endif
-#ifdef PHASE_TRACE
-    uint64_t ph[4] = {0, 0, 0, 0};   // cycles: FK + record, ABA backward, ABA forward, integrate + sincos
-    uint64_t t_top = stamp(sq);
-#endif
     for (int k = kb; k < kend; k++) {
         if constexpr (PROG) __hip_atomic_store(Lprog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
-#endif
         // bit masks, not selects: a select here became a branch around the eps use, and the
         // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
         const double eps = __hiloint2double(__double2hiint(eps_l) & smask, __double2loint(eps_l) & smask);
@@ -1899,40 +1438,13 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             const double vy = s * u0 + c * u1;
             qd = msel(L.m_j0, msel(L.m_j1, msel(L.m_j2, qd, u), vy), vx);
         }
-#ifndef OLD_ABA
         if constexpr (EN)
-#endif
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
-#ifndef ABL_NOFK
-#ifdef PHASE_FK
-        phf[4] = stamp(q);
-        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav, phf);
-#else
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
-#endif
-#endif
         double pe = 0.0;
-        uint64_t t_bwd = 0;
-#ifdef PHASE_TRACE
-        const uint64_t t_fk = stamp(kin.ee[0]);
-        ph[0] += t_fk - t_top;
-#endif
-#ifdef ABL_NOABA
-        const double qdd = u * 1e-3;
-#else
-#ifdef OLD_ABA
-        const double qdd = coop_aba<EN>(j, Lk, Lw, pe, t_bwd);
-#else
         double qdd;
-        if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe, t_bwd);
-        else qdd = coop_solve(j, L, bd, msel(L.m_tau, 0.0, u), Lk, t_bwd);
-#endif
-#endif
-#ifdef PHASE_TRACE
-        const uint64_t t_fwd = stamp(qdd);
-        ph[1] += t_bwd - t_fk;
-        ph[2] += t_fwd - t_bwd;
-#endif
+        if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe);
+        else qdd = coop_solve(j, L, bd, msel(L.m_tau, 0.0, u), Lk);
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
         if constexpr (EN) {   // power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
@@ -1941,17 +1453,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             E = smax(0.0, E + power * a.dt);
         }
         store_record<EN>(recp(k + 1), j, L, q, qd, kin, E);
-#ifdef ABL_SINCOS
-        sq = q - q * q * q * (1.0 / 6.0);
-        cq = 1.0 - q * q * 0.5;
-#else
         fsincos(q, &sq, &cq, scK);
-#endif
-#ifdef PHASE_TRACE
-        const uint64_t t_end = stamp(sq);
-        ph[3] += t_end - t_fwd;
-        t_top = t_end;
-#endif
     }
     if (HO == 3 && kend < H - 1) {   // the next relay stage resumes at step kend
         Lst[3 * lane] = q;
@@ -1959,14 +1461,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         Lst[3 * lane + 2] = E;
     }
     // the final step's dynamics are never observed (deviation 5)
-#ifdef PHASE_TRACE
-    if (a.trace && lane == 0 && !FROW)
-        for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)ph[i];
-#endif
-#ifdef PHASE_FK
-    if (a.trace && lane == 0 && !FROW)
-        for (int i = 0; i < 4; i++) a.trace[4 * wblk + i] = (uint32_t)phf[i];
-#endif
 #ifdef COOP_TRACE
     if (a.trace && lane == 0) a.trace[4 * wblk + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -2103,32 +1597,10 @@ __device__ __forceinline__ int lds_read(int *w)
 {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// relay2: the workgroup that carries the relay's second half (block 0 keeps the first); any block
-// would do (only write-through data crosses), this one shares block 0's XCD under round-robin
-// dispatch
-constexpr int RELAY_PARTNER = 8;
-#ifndef RELAY2   // measured slower: compiled in only with -DRELAY2
-__device__ __forceinline__ bool relay_partner(const FrRolloutArgs &) { return false; }
-#define RELAY2_ON(a) false
-#else
-__device__ __forceinline__ bool relay_partner(const FrRolloutArgs &a) { return a.relay2 && blockIdx.x == RELAY_PARTNER; }
-#define RELAY2_ON(a) ((a).relay2 != 0)
-#endif
-// relay2's split: the first chunk boundary at or below half the horizon
-__host__ __device__ inline int relay_split(int H) { return (((H + CH - 1) / CH) / 2) * CH; }
-// the relay group's chunks [c0, c1) in this workgroup (relay2 splits them at the split)
-__device__ __forceinline__ void relay_chunks(const FrRolloutArgs &a, int &c0, int &c1)
-{
-    const int nch = (a.H + CH - 1) / CH;
-    c0 = relay_partner(a) ? relay_split(a.H) / CH : 0;
-    c1 = (RELAY2_ON(a) && !relay_partner(a)) ? relay_split(a.H) / CH : nch;
-}
-// first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4: block
-// 0's in the relay2 partner)
+// first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4)
 __device__ __forceinline__ int64_t group_row0(const FrRolloutArgs &a, int g)
 {
-    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE
-                 : a.xbase + (int64_t)(relay_partner(a) ? 0 : blockIdx.x) * ROWS_PER_WAVE;
+    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
 }
 // whether chunk c of group g can be read: its records are complete
 __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
@@ -2145,9 +1617,7 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
                                           int *Lq)
 {
     const int H = a.H;
-    int rc0 = 0, rc1 = (H + CH - 1) / CH;
-    if (g == 4) relay_chunks(a, rc0, rc1);
-    const int nch = rc1 - rc0;   // the group's chunks in this workgroup
+    const int nch = (H + CH - 1) / CH;   // the group's chunks
     const int i = lane >> 4, k = c * CH + (lane & 15);
     const int64_t lr0 = group_row0(a, g), lr = lr0 + i;
     const bool rl = row_live(a, lr), live = rl && k < H;
@@ -2162,39 +1632,20 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     const int n = __builtin_amdgcn_readfirstlane(
         __hip_atomic_fetch_add(Lq + Q_DONE + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (n + 1 != nch) return;
-    const bool rfirst = g == 4 && RELAY2_ON(a) && !relay_partner(a), rsecond = g == 4 && relay_partner(a);
-    const int hb = rsecond ? relay_split(H) : 0;
-    if (rsecond) {   // the first half's sums (block 0), in step order: J continues from them
-        int w = 0;
-        while (__hip_atomic_load(a.relay_flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.relay_epoch &&
-               w < WAIT_SPINS) {
-            __builtin_amdgcn_s_sleep(2);
-            w++;
-        }
-        if (w == WAIT_SPINS && lane == 0) note_wait_timeout(a);
-    }
     if (lane < ROWS_PER_WAVE) {
         const int64_t r = lr0 + lane;
         if (row_live(a, r)) {
             const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
-            double J = rsecond ? __hip_atomic_load(a.relay_buf + 64 * 3 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-            for (int q = hb; q < (rfirst ? relay_split(H) : H); q++) J += cr[q];
-            if (rfirst) {   // block 0: the sums so far to the partner, which finishes the rows
-                __hip_atomic_store(a.relay_buf + 64 * 3 + lane, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (a.fcost != nullptr && r == a.count) {
-                J = isnan(J) ? (double)NAN : J;
+            double J = 0.0;
+            for (int q = 0; q < H; q++) J += cr[q];
+            J = isnan(J) ? (double)NAN : J;
+            if (a.fcost != nullptr && r == a.count) {
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
             } else {
-                J = isnan(J) ? (double)NAN : J;
-                if (a.epilogue) __hip_atomic_store(a.cost_out + a.begin + r, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else a.cost_out[a.begin + r] = J;
+                a.cost_out[a.begin + r] = J;
                 mppi_cost::fold_cost_stats(a.stats, J, r);
             }
         }
-    }
-    if (rfirst) {   // every lane's sum stored (write-through), then the flag
-        __builtin_amdgcn_s_waitcnt(0);
-        if (lane == 0) __hip_atomic_store(a.relay_flag + 1, a.relay_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2206,23 +1657,20 @@ __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int
                                          double *Lcs, int *Lflag, int *Lq)
 {
     const int nch = (a.H + CH - 1) / CH;
-    int rc0, rc1;
-    relay_chunks(a, rc0, rc1);
 #pragma unroll 1
     for (int spin = 0; spin < WAIT_SPINS; spin++) {
         bool left = false, did = false;
 #pragma unroll 1
         for (int d = 0; d < ng && !did; d++) {
             const int g = first + d < ng ? first + d : first + d - ng;
-            const int cend = g == 4 ? rc1 : nch;
             const int c0 = lds_read(Lq + Q_NEXT + g);
-            if (c0 >= cend) continue;
+            if (c0 >= nch) continue;
             left = true;
             if (!chunk_ready(a, g, c0, Lflag, Lq)) continue;
             // every lane executes the add (lane 0 adds 1): no lane-dependent branch around it
             const int c = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_fetch_add(Lq + Q_NEXT + g, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (c >= cend) continue;
+            if (c >= nch) continue;
             int w = 0;
             while (!chunk_ready(a, g, c, Lflag, Lq) && w < WAIT_SPINS) {
                 __builtin_amdgcn_s_sleep(4);
@@ -2258,70 +1706,30 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps, or
-// with relay2 eight stages, four on each side of the split
-__device__ __forceinline__ int relay_step(int r, int H, bool two = false)
-{
-    if (!two) return r >= 4 ? H - 1 : (r * (H - 1)) / 4;
-    const int hb = relay_split(H);
-    return r >= 8 ? H - 1 : r <= 4 ? (r * hb) / 4 : hb + ((r - 4) * (H - 1 - hb)) / 4;
-}
+// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
+__device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
 
 // Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): makes the next
 // update's draws for main wave r's rows (r > 0; wave 0's are left to rank_draw_kernel, as the
 // engine expects of the first wave of these workgroups), waits for stage r - 1 (Lq[Q_STAGE] == r),
-// runs its quarter of the horizon at priority 3 and passes the state on; the
-// last stage raises the relay's records flag.  Without a.handover wave 4 runs every step itself at
-// the main waves' priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage
-// ran (false: the previous stage never signalled, counted in Status::wait_timeouts).
-// relay2's two crossings, kept out of line so that the relay loop's code is as without them
-__device__ __attribute__((noinline)) bool relay2_receive(const FrRolloutArgs &a, int lane, double *Lst)
-{
-    int i = 0;
-    while (__hip_atomic_load(a.relay_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.relay_epoch && i < (1 << 22)) {
-        __builtin_amdgcn_s_sleep(2);
-        i++;
-    }
-    if (i == (1 << 22)) return false;
-#pragma unroll
-    for (int c = 0; c < 3; c++)
-        Lst[3 * lane + c] = __hip_atomic_load(a.relay_buf + 3 * lane + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-}
-__device__ __attribute__((noinline)) void relay2_send(const FrRolloutArgs &a, int lane, const double *Lst)
-{
-#pragma unroll
-    for (int c = 0; c < 3; c++)
-        __hip_atomic_store(a.relay_buf + 3 * lane + c, Lst[3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);   // (and this stage's records: block 0's half of the chunks)
-    if (lane == 0) __hip_atomic_store(a.relay_flag, a.relay_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// relay2: stages 0..3 run in block 0, 4..7 in RELAY_PARTNER.  Stage 3 writes the lanes' state
-// through to relay_buf and raises relay_flag[0]; stage 4 waits for it (bounded) and resumes from
-// it.  Each side's objective takes its own half of the relay rows' chunks (cost_chunk).
+// runs its quarter of the horizon at priority 3 and passes the state on; the last stage raises the
+// relay's records flag.  Without a.handover wave 4 runs every step itself at the main waves'
+// priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage ran (false: the
+// previous stage never signalled, counted in Status::wait_timeouts).
 template <int CK, bool EN>
 __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
                                             const double *Lmodel, const double *Lx0, int *Lflag, int *Lq, double *Lst)
 {
     const int H = a.H;
-    const bool two = RELAY2_ON(a), partner = relay_partner(a);
-    const int last = two ? 7 : 3;
-    const int64_t xlr = a.xbase + (int64_t)(partner ? 0 : blockIdx.x) * ROWS_PER_WAVE + (lane >> 4);
+    const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
     const int wblk = gridDim.x * 4 + blockIdx.x;
-    if (!a.handover) {
-        coop_rows<CK, EN, true>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0);
+    if (!a.handover) {   // every step on this wave (the stages' code with one stage)
+        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, 0, 0x7FFFFFFF);
     } else {
-        // the next update's draws for main wave s's rows first (block 0's wave 0 rows are left to
-        // rank_draw_kernel; the partner is an ordinary workgroup for its draws)
-        const int s = partner ? r - 4 : r;
-        if ((partner || r > 0) && a.ahead_noise) group_draws(a, s, lane, Lflag);
-        if (partner && r == 4) {   // the state block 0's stage 3 handed over (bounded)
-            if (!relay2_receive(a, lane, Lst)) {
-                if (lane == 0) note_wait_timeout(a);
-                return false;
-            }
-        } else if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
+        // the next update's draws for main wave r's rows first (block 0's wave 0 rows are left to
+        // rank_draw_kernel)
+        if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
+        if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
             int st = 0;
             for (int i = 0; i < (1 << 22) && st < r; i++) {
                 st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -2332,21 +1740,13 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
                 return false;
             }
         }
-#ifndef RELAY_PRIO
-#define RELAY_PRIO 3   // (A/B builds: 1 = the main waves' own priority)
-#endif
-        __builtin_amdgcn_s_setprio(RELAY_PRIO);
-        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H, two), relay_step(r + 1, H, two));
+        __builtin_amdgcn_s_setprio(3);   // above the main waves (1) and the objective's (0)
+        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H), relay_step(r + 1, H));
         __builtin_amdgcn_s_setprio(0);
 #ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
         if (a.trace && blockIdx.x == 0 && lane == 0 && r < 4) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (two && r == 3) {   // across to the partner: the state written through, then the flag
-            relay2_send(a, lane, Lst);
-            if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
-            return true;
-        }
-        if (r < last) {   // the state in Lst (and this stage's records) before the next stage starts
+        if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
             // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
             if (!((a.debug & 1) && r == 1))
@@ -2354,71 +1754,18 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
             return true;
         }
     }
-    if ((partner || blockIdx.x == 0) && lane == 0)   // write-through: the epilogue's finisher reads this line (sc1)
-        __hip_atomic_store(&const_cast<Status *>(a.status)->handover, a.handover ? relay_step(1, H, two) : -1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(1, H) : -1;
     if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
     return true;
 }
 
-// The update's state into LDS: from the launch's arguments with fused sampling, else from x0
+// The update's state into LDS: from the launch's arguments with the draws made ahead, else from x0
 __device__ __forceinline__ void stage_x0(const FrRolloutArgs &a, double *Lx0)
 {
-    if ((int)threadIdx.x < MAX_X) Lx0[threadIdx.x] = a.fuse_sample ? a.samp.x0v[threadIdx.x] : a.x0[threadIdx.x < FR_X ? threadIdx.x : 0];
+    if ((int)threadIdx.x < MAX_X) Lx0[threadIdx.x] = a.drawn_ahead ? a.samp.x0v[threadIdx.x] : a.x0[threadIdx.x < FR_X ? threadIdx.x : 0];
 }
 
-// Trajectory::sample for the workgroup's own rows, ahead of its horizon loop (a.fuse_sample): the
-// eps pieces of rows [r0, r0 + n1) and [x0r, x0r + n2) for every step (sample_device.hpp).  A
-// thread keeps one (row, piece) and walks the steps k0, k0 + kstep, ... four at a time, computing
-// the four pieces (their loads issued together) before storing them: with five waves on the CU
-// the prologue is latency-bound, not issue-bound.  The rows read U*_shifted from U*
-// (FrRolloutArgs::ush); block 0 writes U*_shifted and x0 back for the kernels that follow (finish,
-// filter()).  This replaces the sample_kernel launch ahead of the rollouts.  The caller's
-// __syncthreads makes the eps stores visible to the workgroup's rows.
-template <int NT, bool DIAG>
-__device__ __forceinline__ void fused_sample_rows(const SampleArgs &sa, int64_t r0, int n1, int64_t x0r, int n2)
-{
-    constexpr int NB = DIAG ? (FR_C + 3) / 4 : 1;
-    constexpr int CW = DIAG ? 4 : FR_C;
-    constexpr int UN = 4;
-    const int per = (n1 + n2) * NB;   // (row, piece) pairs: <= 20 * 3 <= NT
-    const int kstep = NT / per;
-    const int t = (int)threadIdx.x;
-#ifdef FUSE_NOSAMPLE
-    return;   // timing diagnostics only: the eps tensor is left as it was
-#endif
-    if (per == 0 || t >= per * kstep) return;
-    const int rp = t % per, r = rp / NB, blk = rp - r * NB, k0 = t / per;
-    const int64_t lr = r < n1 ? r0 + r : x0r + (r - n1);
-    const int64_t g = sa.begin + lr;
-    const int rank = g >= 2 ? sa.rank[g] : 0;
-    const int H = sa.H;
-    for (int k = k0; k < H; k += UN * kstep) {
-        double e[UN][CW];
-        if constexpr (DIAG) {   // plans, then every piece's loads, then the draws: one wait per pass
-            mppi_sample::EpsPlan pl[UN];
-            double v[UN][4];
-#pragma unroll
-            for (int u = 0; u < UN; u++) {
-                pl[u] = mppi_sample::eps_plan<FR_C>(sa, k + u * kstep < H ? k + u * kstep : k, lr, g, rank, blk);
-                const double2 *p2 = reinterpret_cast<const double2 *>(pl[u].p);
-                const double2 lo = p2[0], hi = p2[1];
-                v[u][0] = lo.x; v[u][1] = lo.y; v[u][2] = hi.x; v[u][3] = hi.y;
-            }
-#pragma unroll
-            for (int u = 0; u < UN; u++) mppi_sample::eps_finish(sa, pl[u], blk, v[u], e[u]);
-        } else {
-#pragma unroll
-            for (int u = 0; u < UN; u++)
-                if (k + u * kstep < H) mppi_sample::sample_eps<FR_C, false>(sa, k + u * kstep, lr, g, rank, blk, e[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < UN; u++)
-            if (k + u * kstep < H) mppi_sample::store_eps<FR_C, DIAG>(sa, k + u * kstep, lr, blk, e[u]);
-    }
-}
-
-// Draws ahead (a.fuse_sample == 2): the eps tensor already holds this update's draws, made by
+// Draws ahead (a.drawn_ahead): the eps tensor already holds this update's draws, made by
 // draw_ahead_kernel behind the previous update; only the kept rollouts' columns from the previous
 // eps remain (rank < keep: steps k < shifted, or every step when nothing shifted).  A wave copies
 // its own kept rows before its horizon loop (rk: the row's rank, loaded at kernel entry so the load
@@ -2427,7 +1774,7 @@ __device__ __forceinline__ void fused_sample_rows(const SampleArgs &sa, int64_t 
 __device__ __forceinline__ int kept_rank(const FrRolloutArgs &a, int64_t lr)
 {
     const int64_t g = a.samp.begin + lr;
-    return (a.fuse_sample == 2 && lr < a.count && g >= 2) ? a.samp.rank[g] : 0x7FFFFFFF;
+    return (a.drawn_ahead && lr < a.count && g >= 2) ? a.samp.rank[g] : 0x7FFFFFFF;
 }
 __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t lr, int lane, int rk)
 {
@@ -2453,15 +1800,8 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
             for (int u = 0; u < UN; u++) {
                 if (k0 + 4 * u >= kend) break;
                 double *dst = sa.noise + ((int64_t)(k0 + 4 * u) * sa.Rpad + lr) * FR_C + 4 * blk;
-                if (a.epilogue) {   // write-through (sc1): the epilogue reads them from other XCDs in this launch
-                    __hip_atomic_store(dst + 0, v[u][0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(dst + 1, v[u][0].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(dst + 2, v[u][1].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(dst + 3, v[u][1].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    reinterpret_cast<double2 *>(dst)[0] = v[u][0];
-                    reinterpret_cast<double2 *>(dst)[1] = v[u][1];
-                }
+                reinterpret_cast<double2 *>(dst)[0] = v[u][0];
+                reinterpret_cast<double2 *>(dst)[1] = v[u][1];
             }
         }
     }
@@ -2469,25 +1809,16 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
 
-// Block 0's share of sampling in fused / draws-ahead launches: U*_shifted and x0 written back for
+// Block 0's share of sampling in draws-ahead launches: U*_shifted and x0 written back for
 // the kernels after the launch.  (The cost statistics the rows fold into were reset by the previous
 // update's finish kernel, a launch ahead: no reset races the folds inside this launch.)
 template <int NT>
 __device__ __forceinline__ void block0_sample_writes(const FrRolloutArgs &a, int t)
 {
     const SampleArgs &sa = a.samp;
-    if (sa.sp.shift_by > 0 && !a.epilogue)   // (the epilogue's finisher writes U*_shifted itself)
+    if (sa.sp.shift_by > 0)
         for (int i = t; i < sa.H * FR_C; i += NT) sa.Us[i] = mppi_sample::shifted_u(sa, i / FR_C, i % FR_C);
     if (t < sa.X) sa.x0_out[t] = sa.x0v[t];
-}
-
-template <int NT>
-__device__ __forceinline__ void fused_sample(const FrRolloutArgs &a, int64_t r0, int n1, int64_t x0r, int n2)
-{
-    const SampleArgs &sa = a.samp;
-    if (blockIdx.x == 0) block0_sample_writes<NT>(a, threadIdx.x);
-    if (sa.sp.tdiag) fused_sample_rows<NT, true>(sa, r0, n1, x0r, n2);
-    else fused_sample_rows<NT, false>(sa, r0, n1, x0r, n2);
 }
 
 // WPB waves per workgroup.  The update's launch uses WPB = 5 with > 80 KB of LDS per workgroup, so a
@@ -2515,15 +1846,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     if constexpr (WPB == 4) rk = kept_rank(a, (int64_t)wblk * ROWS_PER_WAVE + rowi);
     stage_body_table(a, Lmodel, 64 * WPB);
     stage_x0(a, Lx0);
-    if constexpr (WPB == 4) {
-        if (a.fuse_sample == 1) {
-            const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE;
-            fused_sample<64 * WPB>(a, r0, (int)(r0 + 4 * ROWS_PER_WAVE < a.count ? 4 * ROWS_PER_WAVE : a.count - r0), 0, 0);
-        }
-    }
     __syncthreads();
     if constexpr (WPB == 4) {
-        if (a.fuse_sample == 2) {
+        if (a.drawn_ahead) {
             if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);
             kept_rows_wave(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, rk);
         }
@@ -2544,344 +1869,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
-
-// ---- epilogue: optimise() and finish() inside the update launch (a.epilogue) -------------------
-// After the rows and their objective, every workgroup of the one-round launch meets at a grid
-// barrier (all 256 workgroups are resident: one per CU) and then runs weights_gradient_kernel's
-// (step, split) units, two per workgroup (waves 0..3 and 4..7, each the weights kernel's 256-thread
-// block), and the last workgroup to take the ticket runs finish_flat_kernel's publish.  The unit and
-// the finish are those kernels' arithmetic in the same order (kernels.hip), so every output is
-// bit-identical to the three-launch path; what goes is two launches and their boundaries.
-// Hand-offs inside the launch (MI355X_MICROARCH.md, Workgroup dispatch and visibility): bytes another
-// workgroup reads in this launch are stored write-through (sc1) and loaded sc1 - the costs, the
-// kept rows' eps copies, the units' partials and status words; everything else they read was
-// written by an earlier launch.  The barrier and the ticket are agent-scope adds by one lane per
-// workgroup after every wave drained its stores, polled with sc1 loads, bounded.
-constexpr int EP_GR = 3;   // weights_gradient_kernel's GR: rollouts per thread loaded up front
-constexpr int EP_BAR_SPINS = 1 << 23;
-constexpr int EP_MAXE = 4;   // U* elements per finisher thread: H C <= 4 x 512 (launch_fr_coop_update checks)
-
-__device__ __forceinline__ double ep_ld(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void ep_st(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ int ep_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void ep_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// a store to the mapped host block, system scope (write-through to host memory)
-__device__ __forceinline__ void ep_pub(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
-
-// eps of rollout rr (local) at step k as the rollout launch used it: a kept row's columns were
-// copied in this launch (write-through: loaded sc1, after the barrier), the rest are the draws
-// made ahead by earlier launches (plain loads, issued before the barrier)
-// (the weights and finish arguments live in device memory, EpArgs: each function works on a copy
-// in registers, since a load through fa.ep after any global store would have to be repeated)
-__device__ __forceinline__ bool ep_kept(const FrRolloutArgs &fa, const WGradArgs &a, int k, int64_t rr)
-{
-    const SampleArgs &sa = fa.samp;
-    const int64_t g = a.begin + rr;
-    return g >= 2 && sa.rank[g] < sa.sp.keep && (sa.sp.shift_by <= 0 || k < sa.sp.shifted);
-}
-__device__ __forceinline__ const double *ep_eps_ptr(const WGradArgs &a, int k, int64_t rr)
-{
-    return a.noise + ((int64_t)k * a.Rpad + rr) * FR_C;
-}
-__device__ __forceinline__ void ep_eps(const FrRolloutArgs &fa, const WGradArgs &a, int k, int64_t rr, double *e)
-{
-    const double *n = ep_eps_ptr(a, k, rr);
-    if (ep_kept(fa, a, k, rr)) {
-#pragma unroll
-        for (int c = 0; c < FR_C; c++) e[c] = ep_ld(n + c);
-    } else {
-#pragma unroll
-        for (int c = 0; c < FR_C; c++) e[c] = n[c];
-    }
-}
-// A unit's eps, loaded ahead of the barrier where it can be (rows not kept)
-struct EpPre {
-    double ne[EP_GR][FR_C];
-    bool kept[EP_GR];
-};
-__device__ __forceinline__ void ep_unit_range(const WGradArgs &a, int u, int64_t &r0, int64_t &r1, int &k, int &s)
-{
-    const bool has = u >= 0;
-    k = has ? u % a.H : 0;
-    s = has ? u / a.H : 0;
-    const int64_t chunk = (a.count + GRAD_SPLIT - 1) / GRAD_SPLIT;
-    r0 = (int64_t)s * chunk;
-    r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
-}
-__device__ __forceinline__ void ep_preload(const FrRolloutArgs &fa, const WGradArgs &a, int u, int t, EpPre &p)
-{
-    int64_t r0, r1;
-    int k, s;
-    ep_unit_range(a, u, r0, r1, k, s);
-#pragma unroll
-    for (int m = 0; m < EP_GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        const int64_t rr = (u >= 0 && r < r1) ? r : 0;
-        p.kept[m] = ep_kept(fa, a, k, rr);
-        const double *n = ep_eps_ptr(a, k, rr);
-        if (!p.kept[m])
-#pragma unroll
-            for (int c = 0; c < FR_C; c++) p.ne[m][c] = n[c];
-    }
-}
-
-// weights_gradient_kernel<FR_C, false> (kernels.hip) block (k, s) = unit u (k = u mod H, s = u / H)
-// on 256 threads t, unsharded with the objective's statistics; u < 0: no unit (the barrier only)
-__device__ __forceinline__ void ep_unit(const FrRolloutArgs &fa, const WGradArgs &a, int u, int t, double *red, double *ssum,
-                                        EpPre &p)
-{
-    constexpr int CP = FR_C;
-    const int rw = t >> 6, l = t & 63;
-    const int64_t R = a.R;
-    const bool has = u >= 0;
-    int64_t r0, r1;
-    int k, s;
-    ep_unit_range(a, u, r0, r1, k, s);
-    double (&ne)[EP_GR][CP] = p.ne;
-    double cpre[EP_GR];
-#pragma unroll
-    for (int m = 0; m < EP_GR; m++) {   // the kept rows' eps (sc1) and the costs, after the barrier
-        const int64_t r = r0 + t + 256 * m;
-        const int64_t rr = (has && r < r1) ? r : 0;
-        if (p.kept[m]) {
-            const double *n = ep_eps_ptr(a, k, rr);
-#pragma unroll
-            for (int c = 0; c < CP; c++) ne[m][c] = ep_ld(n + c);
-        }
-        cpre[m] = ep_ld(a.cost + a.begin + rr);
-    }
-    const bool own_slice = has && k == 0 && a.begin == 0 && a.count == R;
-    static_assert(CS_SLOTS == 64, "one slot per lane");
-    const unsigned long long kn = mppi_dev::wave_umin64_dpp(
-        __hip_atomic_load(&a.stats->kmin[16 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned long long kx = mppi_dev::wave_umax64_dpp(
-        __hip_atomic_load(&a.stats->kmax[16 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const unsigned int n = (unsigned int)mppi_dev::wave_sum_dpp(
-        (double)__hip_atomic_load(&a.stats->count[32 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const double minimum = n ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
-    const double maximum = n ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
-    const double valid = (double)n;
-    const bool lead = has && k == 0 && s == 0 && t == 0;
-    Status *st = a.status;
-    if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
-        if (lead) {
-            ep_sti(&st->all_nan, 1);
-            ep_sti(&st->early, 1);
-            ep_st(&st->minimum, minimum);
-            ep_st(&st->maximum, maximum);
-        }
-        return;
-    }
-    const double difference = maximum - minimum;
-    if (difference < 1e-6) {   // early return, weights/gradient stale (mppi.cpp:373-375)
-        if (lead) {
-            ep_sti(&st->all_nan, 0);
-            ep_sti(&st->early, 1);
-            ep_st(&st->minimum, minimum);
-            ep_st(&st->maximum, maximum);
-        }
-        return;
-    }
-    auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
-    if (lead) {
-        ep_sti(&st->all_nan, 0);
-        ep_sti(&st->early, 0);
-        ep_st(&st->minimum, minimum);
-        ep_st(&st->maximum, maximum);
-    }
-    double acc[CP];
-#pragma unroll
-    for (int c = 0; c < CP; c++) acc[c] = 0.0;
-    double part = 0.0;
-#pragma unroll
-    for (int m = 0; m < EP_GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        if (has && r < r1) {
-            const double wr = expw(cpre[m]);
-            if (own_slice) {
-                a.wexp[r] = wr;
-                part += wr;
-            }
-#pragma unroll
-            for (int c = 0; c < CP; c++) acc[c] += wr * ne[m][c];
-        }
-    }
-    for (int64_t r = r0 + t + 256 * EP_GR; has && r < r1; r += 256) {
-        const double wr = expw(ep_ld(a.cost + a.begin + r));
-        if (own_slice) {
-            a.wexp[r] = wr;
-            part += wr;
-        }
-        double e[CP];
-        ep_eps(fa, a, k, r, e);
-#pragma unroll
-        for (int c = 0; c < CP; c++) acc[c] += wr * e[c];
-    }
-    if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
-        part = mppi_dev::wave_sum_dpp(part);
-        if (l == 0) ssum[rw] = part;
-    }
-#pragma unroll
-    for (int c = 0; c < CP; c++) acc[c] = mppi_dev::wave_sum_dpp(acc[c]);
-    if (l == 0)
-#pragma unroll
-        for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
-    __syncthreads();   // both halves of the workgroup reach it (the early returns above are uniform)
-    if (has && t < CP)
-        ep_st(a.gsplit + ((int64_t)s * a.H + k) * FR_C + t, (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]));
-    if (own_slice && t == 0) ep_st(&st->tsplit[s], (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]));
-}
-
-// finish_flat_kernel (kernels.hip) by the last workgroup, NT threads: the units' partials and status
-// words loaded sc1; U*_shifted from U* (block 0 did not write it in this launch) and the state by value
-template <int NT>
-__device__ __forceinline__ void ep_finish(const FrRolloutArgs &fa, int tid)
-{
-    auto stamp = [&](int i) {   // diagnostics (MPPI_EP_STAMPS=1): after this wave's memory operations
-        if (fa.ep_stamps && tid == 0) {
-            __builtin_amdgcn_s_waitcnt(0);
-            fa.ep_stamps[blockIdx.x * EP_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
-        }
-    };
-    stamp(4);
-    const FinishArgs a = fa.ep->fin;
-    const SampleArgs &sa = fa.samp;
-    const int HC = a.H * a.C;
-    Status *st = const_cast<Status *>(a.status);
-    const int wt = __hip_atomic_load(&st->wait_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int early = ep_ldi(&st->early), all_nan = ep_ldi(&st->all_nan);
-    const bool upd = !early && !wt, ok = !all_nan && !wt;
-    double tsp[GRAD_SPLIT];
-#pragma unroll
-    for (int i = 0; i < GRAD_SPLIT; i++) tsp[i] = ep_ld(&st->tsplit[i]);
-    double total = tsp[0];
-#pragma unroll
-    for (int i = 1; i < GRAD_SPLIT; i++) total += tsp[i];
-    const double *__restrict__ gs = a.gsplit;
-    double *__restrict__ U = a.U;
-    const double mn = ep_ld(&st->minimum), mx = ep_ld(&st->maximum);
-    // U*_shifted reads U* at shifted positions: every element's inputs are read before any U* store;
-    // the gradient partials with them (one memory trip for the whole finish)
-    double us[EP_MAXE], uos[EP_MAXE], gp[EP_MAXE][GRAD_SPLIT];
-#pragma unroll
-    for (int e = 0; e < EP_MAXE; e++) {
-        const int t = tid + e * NT;
-        if (t < HC) {
-            us[e] = sa.sp.shift_by > 0 ? mppi_sample::shifted_u(sa, t / a.C, t % a.C) : a.Ushift[t];
-            uos[e] = U[t];
-#pragma unroll
-            for (int i = 0; i < GRAD_SPLIT; i++) gp[e][i] = ep_ld(gs + (int64_t)i * HC + t);
-        }
-    }
-    __syncthreads();
-    stamp(5);
-#pragma unroll
-    for (int e = 0; e < EP_MAXE; e++) {
-        const int t = tid + e * NT;
-        if (t >= HC) break;
-        const int c = t % a.C;
-        double g = gp[e][0];
-#pragma unroll
-        for (int i = 1; i < GRAD_SPLIT; i++) g += gp[e][i];
-        g /= total;   // sum_r e_r eps_r / sum_r e_r
-        double u = us[e];
-        const double uo = uos[e];
-        const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
-        if (upd) {
-            a.gradient[t] = g;
-            u += g * a.gradient_step;
-            if (a.control_bound) {
-                u = smin(u, hi);
-                u = smax(u, lo);
-            }
-        }
-        a.Ushift[t] = u;   // U*_shifted as sample() and the gradient step leave it
-        const double v = ok ? u : uo;
-        if (ok) U[t] = v;
-        ep_pub(a.out + t, v);
-    }
-    if (tid < a.X) a.x0_opt[tid] = sa.x0v[tid];
-    for (int64_t i = tid; i < a.rank_n; i += NT) a.rank_zero[i] = 0;   // for rank_draw_kernel's tiles
-    if (tid == 0) {
-        st->sg_error = wt != 0;   // read by the next filter() row as "the update threw"
-        if (upd) st->total = total;
-        ep_pub(a.out + HC + 0, 0.0);   // (the folded filter() cost is read behind the stream)
-        ep_pub(a.out + HC + 1, (double)all_nan);
-        ep_pub(a.out + HC + 2, (double)early);
-        ep_pub(a.out + HC + 3, 0.0);
-        ep_pub(a.out + HC + 4, mn);
-        ep_pub(a.out + HC + 5, mx);
-        ep_pub(a.out + HC + 7, (double)wt);
-    }
-    if (a.stats_reset) mppi_sample::reset_cost_stats(a.stats_reset, tid);
-    if (fa.ep_stamps && tid == 0) fa.ep_stamps[blockIdx.x * EP_STAMPS + 6] = __builtin_amdgcn_s_memrealtime();
-    stamp(7);
-#ifdef PUB_FENCE
-    __syncthreads();
-    if (tid == 0) {
-        st->wait_timeouts = 0;
-        __threadfence_system();
-        __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-#else
-    // The host reads only the mapped block (fine-grained host memory, not cached in L2): its stores
-    // went out system-scope, so once every wave has them acknowledged the flag can follow, without
-    // the system-scope release's write-back of this XCD's L2 (the step records it holds)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) {
-        st->wait_timeouts = 0;
-        __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-#endif
-}
-
-// the epilogue of fr_coop_x_kernel (NT = 64 XW threads): barrier, units, ticket, finish
-template <int NT>
-__device__ __forceinline__ void epilogue(const FrRolloutArgs &a, double *Lsc, int *Lint)
-{
-    const int t = threadIdx.x;
-    const int groups = gridDim.x, half = t >> 8, ht = t & 255;
-    const WGradArgs wg = a.ep->wg;
-    const int nunits = wg.H * GRAD_SPLIT, per = 2 * groups;
-    EpPre pre;   // the first pass's eps, loaded while the barrier waits
-    {
-        const int u = half * groups + (int)blockIdx.x;
-        ep_preload(a, wg, u < nunits ? u : -1, ht, pre);
-    }
-    auto stamp = [&](int i) {   // diagnostics: one clock stamp per workgroup and phase
-        if (a.ep_stamps && t == 0) a.ep_stamps[blockIdx.x * EP_STAMPS + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    __builtin_amdgcn_s_waitcnt(0);   // this wave's cost stores, atomics and eps copies have left it
-    __syncthreads();
-    stamp(0);
-    if (t == 0) {   // every workgroup's costs and statistics are final
-        __hip_atomic_fetch_add(a.ep_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int i = 0;
-        while (__hip_atomic_load(a.ep_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.ep_target && i < EP_BAR_SPINS) {
-            __builtin_amdgcn_s_sleep(2);
-            i++;
-        }
-        if (i == EP_BAR_SPINS) note_wait_timeout(a);   // the update then fails
-    }
-    __syncthreads();
-    stamp(1);
-    for (int base = 0; base < nunits; base += per) {
-        const int u = base + half * groups + (int)blockIdx.x;
-        if (base > 0) ep_preload(a, wg, u < nunits ? u : -1, ht, pre);
-        ep_unit(a, wg, u < nunits ? u : -1, ht, Lsc + half * 64, Lsc + 128 + half * 8, pre);
-        __syncthreads();   // the halves' LDS is reused by the next pass
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // every wave's unit stores have left it
-    __syncthreads();
-    stamp(2);
-    if (t == 0) Lint[0] = __hip_atomic_fetch_add(a.ep_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == a.ep_target;
-    __syncthreads();
-    if (Lint[0]) {
-        ep_finish<NT>(a, t);
-        stamp(3);
-    }
-}
 
 // The update's launch: four waves of main rows per workgroup (rollouts [0, xbase)) and four more
 // waves, one per SIMD beside each main wave, that evaluate the objective in chunks while the rows
@@ -2904,9 +1891,6 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
-#ifdef PRO_TRACE   // kernel entry per main wave (slot 3; coop_rows records the loop's start and end)
-    if (a.trace && lane == 0 && wv < 4) a.trace[4 * (blockIdx.x * 4 + wv) + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#endif
     const int64_t lr = wv < 4 ? (int64_t)(blockIdx.x * 4 + wv) * ROWS_PER_WAVE + rowi
                               : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row (waves < 5)
     const int rk = wv < 5 ? kept_rank(a, lr) : 0x7FFFFFFF;
@@ -2914,21 +1898,14 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     stage_x0(a, Lx0);
     if (threadIdx.x < LF_N) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < Q_N) Lq[threadIdx.x] = threadIdx.x < Q_NEXT ? -1 : 0;
-    if (a.fuse_sample == 1) {   // main rows [16 b, 16 b + 16) and, in the first blocks, the relay's rows
-        const int64_t r0 = (int64_t)blockIdx.x * 4 * ROWS_PER_WAVE, x0r = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
-        const int64_t x1r = x0r < a.count ? (x0r + ROWS_PER_WAVE < a.count ? x0r + ROWS_PER_WAVE : a.count) : x0r;
-        if (wv < 5) fused_sample<320>(a, r0, 4 * ROWS_PER_WAVE, x0r, (int)(x1r - x0r));
-    }
     const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
-    const bool xp = relay_partner(a);   // it carries the relay's second half (block 0's rows)
-    const int ng = (xr || xp) ? 5 : 4;   // row groups of the objective
-    if (!(xr || xp) && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
-    if (xp && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = relay_split(a.H) / CH;   // its chunks start at the split
+    const int ng = xr ? 5 : 4;   // row groups of the objective
+    if (!xr && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
     __syncthreads();
     // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
     const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
     double *Lk = lds_kin + slot * KS, *Lw = lds_scr + slot * LDS_SCR;
-    if (a.fuse_sample == 2) {
+    if (a.drawn_ahead) {
         if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the SIMD of the relay's first stage
         if (wv < 4 || (wv == 4 && xr)) kept_rows_wave(a, lr, lane, rk);
     }
@@ -2952,17 +1929,14 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     } else {
         const int s = wv - 4;   // this wave's SIMD
-        const bool relay = (xr && (s == 0 || a.handover)) || xp;
-        if (relay) relay_stage<CK, EN>(a, xp ? 4 + s : s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
-        if (!cil) return;   // (no epilogue without the objective in the launch)
+        const bool relay = xr && (s == 0 || a.handover);
+        if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
+        if (!cil) return;
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
         if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
         cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
-#ifndef NO_EPILOGUE
-    if (a.epilogue) epilogue<64 * XW>(a, Lcs, Lflag);   // every wave; Lcs and Lflag are free now
-#endif
 }
 
 namespace mppi_eng {
@@ -3020,18 +1994,11 @@ hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, doub
     return hipGetLastError();
 }
 
-// The objective inside the update launch (launch_costs); MPPI_COSTS_IN_LAUNCH=0 keeps the
-// separate fr_step_cost_kernel (A/B)
-static bool costs_in_launch_enabled() { return !env_switches().costs_in_launch_off; }
-
-bool fr_coop_costs_in_launch() { return costs_in_launch_enabled(); }
-
-// The relay in fr_coop_x_kernel (relay_stage, the default); MPPI_HANDOVER=0 leaves the rows left
-// over on wave 4 for the whole horizon, beside main wave 0 (A/B)
-static bool handover_enabled() { return !env_switches().handover_off; }
-
-// MPPI_SPLIT=0: rows just past two waves per SIMD run as one-wave workgroups (A/B)
-static bool split_disabled() { return env_switches().split_off; }
+// The A/B switches (EnvSwitches, the handle's copy): MPPI_COSTS_IN_LAUNCH=0 keeps the separate
+// fr_step_cost_kernel; MPPI_HANDOVER=0 leaves the rows left over on wave 4 for the whole horizon,
+// beside main wave 0, instead of the relay; MPPI_SPLIT=0 runs rows just past two waves per SIMD as
+// one-wave workgroups.
+bool fr_coop_costs_in_launch(const EnvSwitches &env) { return !env.costs_in_launch_off; }
 
 // Whether `count` rows run as two fr_coop_x_kernel launches (launch_fr_coop_update): one-wave
 // workgroups hold two waves per SIMD, 32 rows per CU and round (8192 on 256 CUs), and a count just
@@ -3040,28 +2007,28 @@ static bool split_disabled() { return env_switches().split_off; }
 // kernel).  Two launches of one wave per SIMD (each 1.06-1.1 lone-wave horizons with the objective
 // beside the loops) take less: the first over one round of full four-wave groups, the second over
 // the rest, whose rows left over and the folded filter() row travel through its relay.
-bool fr_coop_update_split(int64_t count)
+bool fr_coop_update_split(int64_t count, const EnvSwitches &env)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t round = (int64_t)g_cu_count * WG_ROWS;
-    if (count <= 2 * round || split_disabled()) return false;
+    if (count <= 2 * round || env.split_off) return false;
     const int64_t rest = count - round, gb = rest / WG_ROWS, xb = rest - gb * WG_ROWS + 1;   // + a folded filter() row
     return gb > 0 && gb <= (int64_t)g_cu_count && xb <= gb * ROWS_PER_WAVE;
 }
 
 // Whether launch_fr_coop_update runs rounds of four-wave groups (the launches that can sample
-// their own rows, a.fuse_sample) for `count` rows: one round, or the two launches of the split.
-bool fr_coop_update_fusable(int64_t count)
+// their kept rows, a.drawn_ahead) for `count` rows: one round, or the two launches of the split.
+bool fr_coop_update_fusable(int64_t count, const EnvSwitches &env)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, xrows = count - groups * WG_ROWS + 1;   // + a folded filter() row
-    return (groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count);
+    return (groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count, env);
 }
 
-bool fr_coop_update_folds(int64_t count, int H)
+bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env)
 {
-    if (!costs_in_launch_enabled() || H > HC_MAX) return false;
-    if (fr_coop_update_split(count)) return true;
+    if (env.costs_in_launch_off || H > HC_MAX) return false;
+    if (fr_coop_update_split(count, env)) return true;
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, extra = count - groups * WG_ROWS;
     return extra > 0 && groups > 0 && groups <= (int64_t)g_cu_count && extra + 1 <= groups * ROWS_PER_WAVE;
@@ -3093,7 +2060,7 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
 }
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry,
                                  CoopTail *tail, FrRolloutArgs *final2)
 {
@@ -3103,14 +2070,12 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     if (tail) *tail = CoopTail{};
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     *folded = false;
-    if (fr_coop_update_split(a0.count)) {   // two launches: one round of full groups, then the rest
+    if (fr_coop_update_split(a0.count, env)) {   // two launches: one round of full groups, then the rest
         const int64_t n0 = (int64_t)g_cu_count * WG_ROWS, rest = a0.count - n0;
         FrRolloutArgs a = a0;
-        a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;
-        a.handover = handover_enabled() ? 1 : 0;
-        if (!a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
-        a.epilogue = 0;   // (two launches: optimise and finish stay separate launches)
-        a.relay2 = 0;
+        a.costs_in_launch = !env.costs_in_launch_off && a.H <= HC_MAX ? 1 : 0;
+        a.handover = env.handover_off ? 0 : 1;
+        if (!a.costs_in_launch || !a.drawn_ahead) a.ahead_noise = nullptr;
         FrRolloutArgs A = row_slice(a, 0, n0), B = row_slice(a, n0, rest);
         A.fcost = nullptr;   // the previous filter() rides with the rows left over
         A.xbase = n0;
@@ -3141,12 +2106,10 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     const int64_t xrows = extra + (frow ? 1 : 0);
     FrRolloutArgs a = a0;
     if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
-        if (a.fuse_sample) return hipErrorInvalidValue;   // the one-wave launch samples nothing
-        a.epilogue = 0;
-        a.relay2 = 0;
+        if (a.drawn_ahead) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
-        a.costs_in_launch = groups > 0 && costs_in_launch_enabled() ? 1 : 0;   // each wave its own rows'
+        a.costs_in_launch = groups > 0 && !env.costs_in_launch_off ? 1 : 0;   // each wave its own rows'
         *costs_done = a.costs_in_launch != 0;
         if (final) *final = a;
         if (dry) return hipSuccess;
@@ -3159,35 +2122,18 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, hipStream_t s, hipEven
     a.xbase = groups * WG_ROWS;
     a.xrows = xrows;
     *folded = frow;
-    a.costs_in_launch = costs_in_launch_enabled() && a.H <= HC_MAX ? 1 : 0;   // Lcs holds HC_MAX steps
-    a.handover = handover_enabled() ? 1 : 0;
+    a.costs_in_launch = !env.costs_in_launch_off && a.H <= HC_MAX ? 1 : 0;   // Lcs holds HC_MAX steps
+    a.handover = env.handover_off ? 0 : 1;
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
-    if (xrows == 0 || !a.costs_in_launch || !a.fuse_sample) a.ahead_noise = nullptr;
-    // the epilogue: fr_coop_x_kernel with the objective in the launch and the draws made ahead (the
-    // finisher reads the state and U* by value / from U*), at most EP_MAXE U* elements per thread
-    a.epilogue = (a0.epilogue && xrows != 0 && a.costs_in_launch && a.fuse_sample == 2 && a.H * FR_C <= EP_MAXE * 64 * XW &&
-                  a.ep_sync != nullptr) ? 1 : 0;
-    a.ep_target = a0.ep_target + (a.epilogue ? (unsigned)groups : 0u);
-    // the relay over two workgroups: one relay group (block 0's), a partner past it, the objective
-    // in the launch, at least two chunks (the split is a chunk boundary), no epilogue
-#ifdef RELAY2
-    a.relay2 = (a0.relay_buf != nullptr && a.handover && xrows != 0 && xrows <= ROWS_PER_WAVE && groups > RELAY_PARTNER &&
-                a.costs_in_launch && !a.epilogue && a.H >= 2 * CH && relay_split(a.H) < a.H - 1) ? 1 : 0;
-#else
-    a.relay2 = 0;
-#endif
+    if (xrows == 0 || !a.costs_in_launch || !a.drawn_ahead) a.ahead_noise = nullptr;
     *tail_drawn = a.ahead_noise != nullptr;
     if (final) *final = a;
     if (x_kernel) *x_kernel = xrows != 0;
     if (tail) *tail = CoopTail{0, a.xbase, (int)((xrows + 3) / 4), 1};
     if (dry) return hipSuccess;
     if (e0) (void)hipEventRecord(e0, s);
-#ifdef FORCE_X
-    if (false) {}
-#else
     if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
-#endif
     else launch_x_any(a, (unsigned)groups, s);
     if (e1) (void)hipEventRecord(e1, s);
     return hipGetLastError();

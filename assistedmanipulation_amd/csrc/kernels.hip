@@ -5,16 +5,16 @@
 //
 //   rank_kernel      stable order of the previous costs            (sample(), mppi.cpp:222-231)
 //   sample_kernel    eps of every (step, rollout); U*_shifted <- shift(U*) (sample(), mppi.cpp:189-270)
-//   fr_rollout_kernel / pm_rollout_kernel
+//   fr_coop_x_kernel (fr_coop.hip) / pm_rollout_kernel
 //                    per rollout: eps columns (kept-shift / fresh draw / -U*), fp64 horizon
-//                    rollout of the dynamics with the per-step cost fused, cost[r]
+//                    rollout of the dynamics and the per-step cost, cost[r]
 //                                                                  (mppi.cpp:242-342)
 //   [RCCL all-reduce of cost[R] when sharded]
 //   weights_gradient_kernel  softmin weights and the partial gradient sum_r w_r eps_r over the
 //                    local shard, one launch (optimise(), mppi.cpp:344-418)
 //   [RCCL all-reduce of the partial gradient when sharded]
 //   finish_kernel    U* += step * g, Savitzky-Golay, clamp          (mppi.cpp:421-447)
-//   fr_rollout_kernel(optimal) / pm_rollout_kernel(optimal)
+//   the optimal rollout (folded into the next rollout launch) / pm_rollout_kernel(optimal)
 //                    cost of the new U* (filter(), mppi.cpp:450-479)
 //   publish_kernel   U* <- U*_shifted, pack the host-visible block   (mppi.cpp:178-182)
 //
@@ -38,408 +38,6 @@ using mppi_dev::smin;
 
 namespace {
 
-// ---------------------------------------------------------------------------------------------
-// Cost primitives (controller/cost.hpp).
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ double right_barrier(const DevBarrier &b, double v)
-{
-    if (v >= b.bound) {
-        double d = v - b.bound;
-        return b.max + b.scale * (d * d);
-    }
-    return smin(b.scale / (b.bound - v), b.max);
-}
-__device__ __forceinline__ double left_barrier(const DevBarrier &b, double v)
-{
-    if (v <= b.bound) {
-        double d = b.bound - v;
-        return b.max + b.scale * (d * d);
-    }
-    return smin(b.scale / (v - b.bound), b.max);
-}
-
-// ---------------------------------------------------------------------------------------------
-// FrankaRidgeback dynamics (PinocchioDynamics::calculate/step, pinocchio_dynamics.cpp:153-260)
-// in world coordinates: a = M(q)^-1 tau_u by a zero-bias articulated-body pass (equal to the
-// reference's aba(q, v, tau_u + nle(q, v)) in exact arithmetic).  Per-body data the backward
-// and forward passes need (world pose, U, 1/D, u) lives in an LDS stack, lane-strided.
-// ---------------------------------------------------------------------------------------------
-// Uniform, read-only model/cost tables.  hipcc hoists them out of the horizon loop into
-// (A)GPRs; forcing per-use reloads through an opaque pointer measured 5% slower at one wave
-// per SIMD (exposed load latency), so the pointer is passed through unchanged.
-template <class T>
-__device__ __forceinline__ const T *opaque(const T *p)
-{
-    return p;
-}
-
-constexpr int STK = 20;   // doubles per body: R[9] p[3] U[6] Dinv u
-
-template <int NT>
-struct Stack {
-    double *base;
-    int lane;
-    __device__ __forceinline__ double &at(int body, int e) const { return base[(body * STK + e) * NT + lane]; }
-};
-
-// Kinematics cached by calculate() for the *next* cost evaluation (the one-step lag).
-struct Kin {
-    double ee[3];   // panda_grasp_joint position
-    double am[3];   // arm_mount_joint position
-    double vl[3];   // EE spatial velocity, linear part, WORLD (at the world origin)
-    double jj[6];   // J_a J_a^T packed (00, 01, 02, 11, 12, 22), J_a = WORLD linear rows, arm cols
-};
-
-// World pose of body i from its parent's world pose and q_i; writes it to the stack.
-template <int NT>
-__device__ __forceinline__ void body_pose(const DevModel &M, int i, double qi, const double *Rpar,
-                                          const double *ppar, double *Rw, double *pw, const Stack<NT> &st)
-{
-    const DevBody &B = *opaque(&M.b[i]);
-    double Rl[9], pl[3];
-    const int kind = FR_KIND[i];
-    if (kind == KIND_RZ) {
-        double s, c;
-        sincos(qi, &s, &c);
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            Rl[3 * r + 0] = B.R[3 * r + 0] * c + B.R[3 * r + 1] * s;
-            Rl[3 * r + 1] = B.R[3 * r + 0] * (-s) + B.R[3 * r + 1] * c;
-            Rl[3 * r + 2] = B.R[3 * r + 2];
-            pl[r] = B.p[r];
-        }
-    } else {
-        const int col = (kind == KIND_PX) ? 0 : 1;
-        const double qq = (kind == KIND_PNY) ? -qi : qi;
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) Rl[3 * r + k] = B.R[3 * r + k];
-            pl[r] = B.p[r] + B.R[3 * r + col] * qq;
-        }
-    }
-    if (FR_PARENT[i] < 0) {
-#pragma unroll
-        for (int k = 0; k < 9; k++) Rw[k] = Rl[k];
-#pragma unroll
-        for (int k = 0; k < 3; k++) pw[k] = pl[k];
-    } else {
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                Rw[3 * r + c] = (Rpar[3 * r + 0] * Rl[c] + Rpar[3 * r + 1] * Rl[3 + c]) + Rpar[3 * r + 2] * Rl[6 + c];
-            pw[r] = ppar[r] + ((Rpar[3 * r + 0] * pl[0] + Rpar[3 * r + 1] * pl[1]) + Rpar[3 * r + 2] * pl[2]);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 9; k++) st.at(i, k) = Rw[k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) st.at(i, 9 + k) = pw[k];
-}
-
-// World motion subspace S_i = (linear, angular) from the body's world pose.
-__device__ __forceinline__ void body_S(int i, const double *Rw, const double *pw, double *S)
-{
-    const int kind = FR_KIND[i];
-    if (kind == KIND_RZ) {
-        double w0 = Rw[2], w1 = Rw[5], w2 = Rw[8];
-        S[0] = pw[1] * w2 - pw[2] * w1;
-        S[1] = pw[2] * w0 - pw[0] * w2;
-        S[2] = pw[0] * w1 - pw[1] * w0;
-        S[3] = w0;
-        S[4] = w1;
-        S[5] = w2;
-    } else {
-        const int col = (kind == KIND_PX) ? 0 : 1;
-        const double sg = (kind == KIND_PNY) ? -1.0 : 1.0;
-        S[0] = sg * Rw[col];
-        S[1] = sg * Rw[3 + col];
-        S[2] = sg * Rw[6 + col];
-        S[3] = 0.0;
-        S[4] = 0.0;
-        S[5] = 0.0;
-    }
-}
-
-template <int NT>
-__device__ __forceinline__ void load_pose(const Stack<NT> &st, int i, double *Rw, double *pw)
-{
-#pragma unroll
-    for (int k = 0; k < 9; k++) Rw[k] = st.at(i, k);
-#pragma unroll
-    for (int k = 0; k < 3; k++) pw[k] = st.at(i, 9 + k);
-}
-
-// Spatial inertia of body i at the world origin, packed upper triangle of the 6x6
-// [[m E, -m[c]x], [m[c]x, I_w + m(|c|^2 E - c c^T)]].
-__device__ __forceinline__ void world_inertia(const DevBody &Bref, const double *R, const double *p, double *P)
-{
-    const DevBody &B = *opaque(&Bref);
-    double c[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) c[r] = ((R[3 * r] * B.c[0] + R[3 * r + 1] * B.c[1]) + R[3 * r + 2] * B.c[2]) + p[r];
-    // Ic full from xx, xy, yy, xz, yz, zz
-    const double I00 = B.Ic[0], I01 = B.Ic[1], I11 = B.Ic[2], I02 = B.Ic[3], I12 = B.Ic[4], I22 = B.Ic[5];
-    double RI[9];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        RI[3 * r + 0] = (R[3 * r] * I00 + R[3 * r + 1] * I01) + R[3 * r + 2] * I02;
-        RI[3 * r + 1] = (R[3 * r] * I01 + R[3 * r + 1] * I11) + R[3 * r + 2] * I12;
-        RI[3 * r + 2] = (R[3 * r] * I02 + R[3 * r + 1] * I12) + R[3 * r + 2] * I22;
-    }
-    double Iw[6];   // 00 01 02 11 12 22
-    int k = 0;
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int s = r; s < 3; s++, k++)
-            Iw[k] = (RI[3 * r] * R[3 * s] + RI[3 * r + 1] * R[3 * s + 1]) + RI[3 * r + 2] * R[3 * s + 2];
-    const double m = B.mass;
-    const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
-    const double cc2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
-    // row 0
-    P[0] = m; P[1] = 0.0; P[2] = 0.0; P[3] = 0.0; P[4] = mc2; P[5] = -mc1;
-    // row 1
-    P[6] = m; P[7] = 0.0; P[8] = -mc2; P[9] = 0.0; P[10] = mc0;
-    // row 2
-    P[11] = m; P[12] = mc1; P[13] = -mc0; P[14] = 0.0;
-    // rows 3..5 (angular block)
-    P[15] = Iw[0] + (m * cc2 - mc0 * c[0]);
-    P[16] = Iw[1] - mc0 * c[1];
-    P[17] = Iw[2] - mc0 * c[2];
-    P[18] = Iw[3] + (m * cc2 - mc1 * c[1]);
-    P[19] = Iw[4] - mc1 * c[2];
-    P[20] = Iw[5] + (m * cc2 - mc2 * c[2]);
-}
-
-__device__ __forceinline__ constexpr int pidx(int r, int c)
-{
-    return (r <= c) ? (r * 6 - r * (r - 1) / 2 + (c - r)) : (c * 6 - c * (c - 1) / 2 + (r - c));
-}
-
-// Forward kinematics at (q, qd): world poses (to the stack), the cost's kinematic cache.
-template <int NT>
-__device__ __forceinline__ void fk_pass(const DevModel &M, const double *q, const double *qd, const Stack<NT> &st, Kin &kin)
-{
-    double Rw[9], pw[3], R9[9], p9[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) kin.vl[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) kin.jj[k] = 0.0;
-    double Rprev[9], pprev[3];
-#pragma unroll
-    for (int i = 0; i < FR_NB; i++) {
-        const double *Rpar = (FR_PARENT[i] == 9 && i != 10) ? R9 : Rprev;
-        const double *ppar = (FR_PARENT[i] == 9 && i != 10) ? p9 : pprev;
-        body_pose<NT>(M, i, q[i], Rpar, ppar, Rw, pw, st);
-        double S[6];
-        body_S(i, Rw, pw, S);
-        if (i <= FR_EE_PARENT) {
-            if (i == 0) {
-#pragma unroll
-                for (int k = 0; k < 3; k++) kin.vl[k] = qd[i] * S[k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; k++) kin.vl[k] = kin.vl[k] + qd[i] * S[k];
-            }
-        }
-        if (i >= FR_ARM0 && i < FR_ARM1) {
-            kin.jj[0] += S[0] * S[0]; kin.jj[1] += S[0] * S[1]; kin.jj[2] += S[0] * S[2];
-            kin.jj[3] += S[1] * S[1]; kin.jj[4] += S[1] * S[2]; kin.jj[5] += S[2] * S[2];
-        }
-        if (i == FR_AM_PARENT) {
-            const double *am = opaque(M.am_p);
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-                kin.am[r] = pw[r] + ((Rw[3 * r] * am[0] + Rw[3 * r + 1] * am[1]) + Rw[3 * r + 2] * am[2]);
-        }
-        if (i == FR_EE_PARENT) {
-            const double *ee = opaque(M.ee_p);
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-                kin.ee[r] = pw[r] + ((Rw[3 * r] * ee[0] + Rw[3 * r + 1] * ee[1]) + Rw[3 * r + 2] * ee[2]);
-#pragma unroll
-            for (int k = 0; k < 9; k++) R9[k] = Rw[k];
-#pragma unroll
-            for (int k = 0; k < 3; k++) p9[k] = pw[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 9; k++) Rprev[k] = Rw[k];
-#pragma unroll
-        for (int k = 0; k < 3; k++) pprev[k] = pw[k];
-    }
-}
-
-// Articulated-body passes over the poses on the stack: qdd = M(q)^-1 tau.
-template <int NT>
-__device__ __forceinline__ void aba_pass(const DevModel &M, const double *tau, const Stack<NT> &st, double *qdd)
-{
-    double acc[21], accp[6];
-    {
-        double R[9], p[3];
-        load_pose<NT>(st, 9, R, p);
-        world_inertia(M.b[9], R, p, acc);   // Ia_9 starts as body 9's own inertia
-#pragma unroll
-        for (int k = 0; k < 6; k++) accp[k] = 0.0;
-    }
-#pragma unroll
-    for (int i = FR_NB - 1; i >= 0; i--) {
-        double Ia[21], pA[6], R[9], p[3], S[6];
-        load_pose<NT>(st, i, R, p);
-        body_S(i, R, p, S);
-        if (i >= 10) {
-            world_inertia(M.b[i], R, p, Ia);
-#pragma unroll
-            for (int k = 0; k < 6; k++) pA[k] = 0.0;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 21; k++) Ia[k] = acc[k];
-#pragma unroll
-            for (int k = 0; k < 6; k++) pA[k] = accp[k];
-        }
-        double U[6];
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-            double a = Ia[pidx(r, 0)] * S[0];
-#pragma unroll
-            for (int c = 1; c < 6; c++) a += Ia[pidx(r, c)] * S[c];
-            U[r] = a;
-        }
-        double Dd = S[0] * U[0];
-#pragma unroll
-        for (int r = 1; r < 6; r++) Dd += S[r] * U[r];
-        const double Dinv = 1.0 / Dd;
-        double sp = S[0] * pA[0];
-#pragma unroll
-        for (int r = 1; r < 6; r++) sp += S[r] * pA[r];
-        const double u = tau[i] - sp;
-#pragma unroll
-        for (int r = 0; r < 6; r++) st.at(i, 12 + r) = U[r];
-        st.at(i, 18) = Dinv;
-        st.at(i, 19) = u;
-        if (i > 0) {
-            if (i <= 9) {   // the parent's accumulator starts from the parent's own inertia
-                double Rq[9], pq[3];
-                load_pose<NT>(st, i - 1, Rq, pq);
-                world_inertia(M.b[i - 1], Rq, pq, acc);
-#pragma unroll
-                for (int k = 0; k < 6; k++) accp[k] = 0.0;
-            }
-            const double ud = u * Dinv;
-            int k = 0;
-#pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double Ud = U[r] * Dinv;
-#pragma unroll
-                for (int c = r; c < 6; c++, k++) acc[k] += Ia[k] - Ud * U[c];
-            }
-#pragma unroll
-            for (int r = 0; r < 6; r++) accp[r] += pA[r] + U[r] * ud;
-        }
-    }
-    double a9[6], a[6];
-#pragma unroll
-    for (int r = 0; r < 6; r++) a[r] = 0.0;
-#pragma unroll
-    for (int i = 0; i < FR_NB; i++) {
-        double ap[6];
-#pragma unroll
-        for (int r = 0; r < 6; r++) ap[r] = (i == 11) ? a9[r] : a[r];
-        double R[9], p[3], S[6];
-        load_pose<NT>(st, i, R, p);
-        body_S(i, R, p, S);
-        double ua = st.at(i, 12) * ap[0];
-#pragma unroll
-        for (int r = 1; r < 6; r++) ua += st.at(i, 12 + r) * ap[r];
-        const double dd = st.at(i, 18) * (st.at(i, 19) - ua);
-        qdd[i] = dd;
-#pragma unroll
-        for (int r = 0; r < 6; r++) a[r] = ap[r] + S[r] * dd;
-        if (i == 9) {
-#pragma unroll
-            for (int r = 0; r < 6; r++) a9[r] = a[r];
-        }
-    }
-}
-
-// AssistedManipulation::get_cost (assisted_manipulation.cpp:37-72) at state x = (q, qd) with
-// the lagged kinematic cache.
-__device__ __forceinline__ double fr_cost(const DevCost &Csref, const StepConst &sc, const double *q, const double *qd, const Kin &kin)
-{
-    const DevCost &Cs = *opaque(&Csref);
-    double cost = 0.0;
-    if (Cs.en_joint) {   // joint_limit_cost (:74-88)
-        double jc = 0.0;
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) {
-            double c = left_barrier(Cs.lower[i], q[i]) + right_barrier(Cs.upper[i], q[i]);
-            jc += c;
-        }
-        cost += jc;
-    }
-    if (Cs.en_self) cost += Cs.self_collision;   // self_collision_cost (:90-158), link positions = 0
-    if (Cs.en_work) {   // workspace_cost (:160-209)
-        double wc = 0.0;
-        double s, c;
-        sincos(q[2], &s, &c);
-        const double r22 = (1.0 - c) + c;
-        const double fw0 = c, fw1 = s, fw2 = 0.0;
-        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
-        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
-        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
-        const double rb0 = kin.am[0] + off0, rb1 = kin.am[1] + off1, rb2 = kin.am[2] + off2;
-        const double t0 = kin.ee[0] - rb0, t1 = kin.ee[1] - rb1, t2 = kin.ee[2] - rb2;
-        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
-        wc += left_barrier(Cs.ws_infront, proj);
-        const double reach = sqrt((t0 * t0 + t1 * t1) + t2 * t2);
-        wc += right_barrier(Cs.ws_reach, reach);
-        const double n1 = sqrt(t0 * t0 + t1 * t1);
-        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
-        const double yaw = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
-        if (!isnan(yaw)) {
-            const double ay = fabs(yaw);
-            wc += (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
-        }
-        wc += left_barrier(Cs.ws_above, kin.ee[2] - rb2);
-        cost += wc;
-    }
-    if (Cs.en_vel) {   // velocity_cost (:224-235)
-        double vc = 0.0;
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) {
-            const double v = fabs(qd[i]);
-            vc += Cs.vel_q[i] * (v * v);
-        }
-        cost += vc;
-    }
-    if (Cs.en_traj) {   // trajectory_cost (:237-290)
-        double tc = 0.0;
-        if (sc.active) {
-            tc += sc.pos_cost;
-            double proj = ((kin.vl[0] * sc.target[0] + kin.vl[1] * sc.target[1]) + kin.vl[2] * sc.target[2]) / sc.tt;
-            const double p0 = proj * sc.target[0], p1 = proj * sc.target[1], p2 = proj * sc.target[2];
-            proj = copysign(1.0, proj) * sqrt((p0 * p0 + p1 * p1) + p2 * p2);
-            const double err = fabs(sc.vtarget - proj);
-            tc += (Cs.traj_vel_c + Cs.traj_vel_l * fabs(err)) + Cs.traj_vel_q * err * err;
-        }
-        cost += tc;
-    }
-    if (Cs.en_manip) {   // manipulability_cost (:292-319)
-        const double m00 = kin.jj[0], m01 = kin.jj[1], m02 = kin.jj[2], m11 = kin.jj[3], m12 = kin.jj[4], m22 = kin.jj[5];
-        const double h0 = m00 * (m11 * m22 - m12 * m12);
-        const double h1 = m01 * (m01 * m22 - m12 * m02);
-        const double h2 = m02 * (m01 * m12 - m11 * m02);
-        const double det = (h0 - h1) + h2;
-        double vol = sqrt(det);
-        if (isnan(vol)) vol = 1e-5;
-        else vol = (vol < 1e-5) ? 1e-5 : ((1e5 < vol) ? 1e5 : vol);
-        const double iv = 1.0 / vol;
-        cost += (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
-    }
-    return cost;
-}
-
 // t0 + k dt exactly as the reference's double expression (mppi.cpp:430, 437): window times are
 // compared with ==/< (filter.cpp:94-106), so no FMA contraction here.
 __device__ __forceinline__ double step_time(double t0, int k, double dt)
@@ -447,8 +45,6 @@ __device__ __forceinline__ double step_time(double t0, int k, double dt)
 #pragma clang fp contract(off)
     return t0 + (double)k * dt;
 }
-
-constexpr int FR_NT = 64;   // one wave per workgroup; the LDS stack takes 120 KiB of the CU's 160
 
 }  // namespace
 
@@ -647,9 +243,7 @@ __device__ __forceinline__ void draw_ahead_block(const SampleArgs &a, unsigned b
     mppi_sample::store_eps<C, true>(a, k, lr, blk, eps);
 }
 
-#ifndef RANK_JS
-#define RANK_JS 4
-#endif
+constexpr unsigned RANK_JS = 4;   // blocks per rank tile: its 256 columns split four ways (r02i)
 // The draws ahead and the stable rank of this update's costs in one launch (neither reads the
 // other's output): blocks [0, nr^2) rank tiles, the rest draw (grid nx x H flattened)
 template <int C>
@@ -692,71 +286,6 @@ hipError_t mppi_eng::launch_draw_ahead(const SampleArgs &a, const double *cost, 
     hipLaunchKernelGGL((rank_draw_kernel<FR_C>), dim3(grid), dim3(256), 0, s, cost, S, rank, nr, a, nx, sub_nxb, sub_xbase,
                        sub_row0);
     return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// FrankaRidgeback rollouts: one lane per rollout (first version).
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(FR_NT) void fr_rollout_kernel(FrRolloutArgs a)
-{
-    __shared__ double stack_mem[FR_NB * STK * FR_NT];
-    if (a.optimal && (a.status->all_nan || a.status->sg_error)) return;   // update threw: no filter()
-    const int lane = threadIdx.x;
-    const int64_t lr = (int64_t)blockIdx.x * FR_NT + lane;   // local rollout
-    const bool live = lr < a.count;
-    const int64_t g = a.optimal ? -1 : a.begin + lr;            // global rollout index
-    Stack<FR_NT> st{stack_mem, lane};
-    const DevModel &M = *a.model;
-    const DevCost &Cs = *a.cost;
-    const int H = a.H;
-
-    double q[FR_NB], qd[FR_NB];
-#pragma unroll
-    for (int i = 0; i < FR_NB; i++) {
-        q[i] = a.x0[i];
-        qd[i] = a.x0[FR_NB + i];
-    }
-    Kin kin;
-    fk_pass<FR_NT>(M, q, qd, st, kin);   // set_state -> calculate() at (q0, v0) (:142-151)
-    double J = 0.0;
-    bool alive = live;
-    for (int k = 0; k < H; k++) {
-        double eps[FR_C];
-#pragma unroll
-        for (int c = 0; c < FR_C; c++) eps[c] = (a.optimal || !live) ? 0.0 : a.noise[((int64_t)k * a.Rpad + lr) * FR_C + c];
-        if (!alive) continue;
-        const StepConst &sc = *opaque(&a.steps[k]);
-        const double step_cost = sc.gamma_k * fr_cost(Cs, sc, q, qd, kin);
-        if (!a.optimal && isnan(step_cost)) {   // rollout cost NaN, stop (mppi.cpp:331-334)
-            J = NAN;
-            alive = false;
-            continue;
-        }
-        J += step_cost;
-        if (k == H - 1) break;   // the final step's dynamics are never observed
-        double u[FR_C];
-#pragma unroll
-        for (int c = 0; c < FR_C; c++) u[c] = a.Ushift[k * FR_C + c] + eps[c];
-        // PinocchioDynamics::step (:226-260)
-        double s, c;
-        sincos(q[2], &s, &c);
-        qd[0] = c * u[0] + (-s) * u[1];
-        qd[1] = s * u[0] + c * u[1];
-        qd[2] = u[2];
-        double tau[FR_NB];
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) tau[i] = (i >= 3 && i < 10) ? u[i] : 0.0;
-        fk_pass<FR_NT>(M, q, qd, st, kin);
-        double qdd[FR_NB];
-        aba_pass<FR_NT>(M, tau, st, qdd);
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) qd[i] = qd[i] + qdd[i] * a.dt;
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) q[i] = q[i] + qd[i] * a.dt;
-    }
-    if (!live) return;
-    if (a.optimal) *a.cost_out = J;
-    else a.cost_out[g] = J;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -859,10 +388,7 @@ __device__ __forceinline__ double wave_sum(double v) { return mppi_dev::wave_sum
 constexpr int WV = 16;       // waves of the 1024-thread reduction order
 constexpr int WU = 8;        // costs per (virtual) thread and pass
 constexpr int NV = WV / 4;   // virtual waves per real wave
-#ifndef WG_GR
-#define WG_GR 3
-#endif
-constexpr int GR = WG_GR;     // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
+constexpr int GR = 3;     // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
 
 // Large R (R > SM_LARGE_R, configs 4 / 5: every rank weighs all R global costs): recomputing
 // min / max / normaliser over all R in each of the H x GRAD_SPLIT blocks costs O(H R) exps, so
@@ -874,10 +400,7 @@ constexpr int GR = WG_GR;     // rollouts per thread whose eps is loaded up fron
 // and weights_gradient_kernel<C, true> folds the NB sums the same way for the normaliser and
 // reads e_r instead of recomputing it.
 constexpr int SM_NB = 64;
-#ifndef SM_LARGE_R_DEF
-#define SM_LARGE_R_DEF 16384
-#endif
-constexpr int64_t SM_LARGE_R = SM_LARGE_R_DEF;
+constexpr int64_t SM_LARGE_R = 16384;
 
 __device__ __forceinline__ void sm_chunk(int64_t R, int b, int64_t &r0, int64_t &r1)
 {
@@ -951,15 +474,10 @@ __global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
     if (t == 0) a.wpart[3 * SM_NB + blockIdx.x] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
-#ifndef GRAD_CSPLIT
-#define GRAD_CSPLIT 1   // control components split over blockIdx.z (A/B builds: 2)
-#endif
 template <int C, bool LARGE>
 __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
-    constexpr int CSP = (C > 3 && C % GRAD_CSPLIT == 0) ? GRAD_CSPLIT : 1;
-    constexpr int CP = C / CSP;   // this block's components [c0, c0 + CP)
-    const int zc = CSP > 1 ? (int)blockIdx.z : 0, c0 = zc * CP;
+    constexpr int CP = C;
     __shared__ double red[4 * CP];
     __shared__ double smn[WV], smx[WV], ssum[WV];
     const int t = threadIdx.x, rw = t >> 6, l = t & 63;
@@ -972,7 +490,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 #pragma unroll
     for (int m = 0; m < GR; m++) {
         const int64_t r = r0 + t + 256 * m;
-        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C + c0;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C;
 #pragma unroll
         for (int c = 0; c < CP; c++) ne[m][c] = n[c];
         const int64_t gi = a.begin + (r < r1 ? r : 0);
@@ -981,7 +499,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     }
     // unsharded, the normaliser slice of block (0, s) is its own rollout range [r0, r1): its e_r come
     // from the gradient loop below, in the same per-thread order as the separate slice pass
-    const bool own_slice = !LARGE && k == 0 && zc == 0 && a.begin == 0 && a.count == R;
+    const bool own_slice = !LARGE && k == 0 && a.begin == 0 && a.count == R;
     double minimum, maximum, valid, total;
     if constexpr (LARGE) {
         if (rw == 0) {
@@ -1055,7 +573,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     __syncthreads();
     total = 0.0;
     }
-    const bool lead = k == 0 && s == 0 && zc == 0 && t == 0;
+    const bool lead = k == 0 && s == 0 && t == 0;
     Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
         if (lead) { st->all_nan = 1; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
@@ -1070,8 +588,8 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     // e_r of global rollout i: recomputed, or (LARGE) written by softmin_exp_kernel
     auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
     if constexpr (LARGE) {   // the normaliser is known: one partial carries it
-        if (k == 0 && zc == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
-    } else if (k == 0 && zc == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
+        if (k == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
+    } else if (k == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
         const int64_t wc = (R + ns - 1) / ns, w0 = (int64_t)s * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
         double part = 0.0;
         for (int64_t i = w0 + t; i < w1; i += 256) {
@@ -1111,7 +629,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
             a.wexp[r] = wr;
             part += wr;
         }
-        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C + c0;
+        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < CP; c++) acc[c] += wr * n[c];
     }
@@ -1127,7 +645,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
     __syncthreads();
     if (t < CP)
-        a.gsplit[((int64_t)s * a.H + k) * C + c0 + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
+        a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
     if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
@@ -1153,21 +671,14 @@ __device__ __forceinline__ void pub(double *p, double v) { __hip_atomic_store(p,
 // Call from every thread of the block.
 __device__ __forceinline__ void publish_block(const FinishArgs &a)
 {
-#ifndef PUB_FENCE
     __builtin_amdgcn_s_waitcnt(0);
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         // every thread has read this update's wait-timeout count (update_wait_timeouts): reset it
         // for the next rollout launch (stream-ordered after this kernel)
         a.status_w->wait_timeouts = 0;
         if (a.wait_local) *a.wait_local = 0.0;
-#ifdef PUB_FENCE   // (A/B builds: the release as before)
-        __threadfence_system();
-        __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
         __hip_atomic_store(a.out + a.H * a.C + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
     }
 }
 
@@ -1379,193 +890,6 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
     publish_block(a);
 }
 
-// optimise() and finish() in one launch (the usual unsharded update: cost statistics from the
-// rollout launch, no Savitzky-Golay, R <= SM_LARGE_R).  Block k is step k of weights_gradient_kernel
-// for all GRAD_SPLIT rollout ranges at once: its 512 threads are splits s, s + 2, s + 4 and s + 6 of
-// thread t at 256 (s mod 2) + t, so each wave holds the same 64 (split, thread) pairs as one of that kernel's
-// waves and every sum - per thread in row order, the wave butterflies, the four wave sums, the
-// eight split partials in order - is formed as the two launches form it: gradient, normaliser,
-// weights and U* are bit-identical to weights_gradient_kernel + finish_flat_kernel.  Every block
-// evaluates all R exponentials for the normaliser (the eight slice blocks did so between them), so
-// block k can step, clamp and publish its step's C elements of U* at once; the last block to take
-// the ticket writes the status words and raises the flag (the partial gradients never leave the
-// block: the finish launch and its memory trip go).
-constexpr int WF_NT = 512, WF_GR = 2, WF_NJ = GRAD_SPLIT * 256 / WF_NT;   // splits per thread
-struct WfFinishIn {   // finish_flat_kernel's inputs for element e (unconditional loads: no branches)
-    double us, uo, hi, lo, oc, x0;
-    __device__ __forceinline__ void load(const FinishArgs &f, int e, int cc, int T)
-    {
-        us = f.Ushift[e];
-        uo = f.U[e];
-        hi = f.cmax[cc];
-        lo = f.cmin[cc];
-        oc = *f.opt_cost;
-        x0 = f.x0[T < f.X ? T : 0];
-    }
-};
-template <int C>
-__global__ __launch_bounds__(WF_NT) void weights_finish_kernel(WGradArgs a, FinishArgs f, unsigned *ticket)
-{
-    static_assert(GRAD_SPLIT * 256 == WF_NJ * WF_NT && WF_NT % 256 == 0, "whole splits per thread");
-    constexpr int SS = WF_NT / 256;   // split stride
-    __shared__ double red[GRAD_SPLIT][4][C];
-    __shared__ double ssum[GRAD_SPLIT][4];
-    __shared__ int last;
-    const int T = threadIdx.x, t = T & 255, sl = T >> 8, rw = t >> 6, l = T & 63;
-    const int k = blockIdx.x, HC = f.H * C;
-    // 32-bit indexing (weights_finish_eligible: R <= SM_LARGE_R, eps under 2 GB): the loads take one
-    // VGPR offset each from the arrays' SGPR bases
-    const int R = (int)a.R, chunk = (R + GRAD_SPLIT - 1) / GRAD_SPLIT;
-    const unsigned kb = (unsigned)k * (unsigned)a.Rpad;
-    int r0[WF_NJ], r1[WF_NJ];
-#pragma unroll
-    for (int j = 0; j < WF_NJ; j++) {
-        r0[j] = (sl + SS * j) * chunk;
-        r1[j] = (r0[j] + chunk < R) ? r0[j] + chunk : R;
-    }
-    // one memory trip: the statistics' slots, the first rows' eps and costs (the finish's inputs
-    // follow the sums)
-    const unsigned long long kmn = a.stats->kmin[16 * l], kmx = a.stats->kmax[16 * l];
-    const unsigned int kct = a.stats->count[32 * l];
-    const int wt = f.status->wait_timeouts;   // unsharded: update_wait_timeouts
-    double ne[WF_NJ][WF_GR][C], cpre[WF_NJ][WF_GR];
-#pragma unroll
-    for (int j = 0; j < WF_NJ; j++)
-#pragma unroll
-        for (int m = 0; m < WF_GR; m++) {
-            const int r = r0[j] + t + 256 * m, rr = r < r1[j] ? r : 0;
-            const double *n = a.noise + (kb + (unsigned)rr) * (unsigned)C;
-#pragma unroll
-            for (int c = 0; c < C; c++) ne[j][m][c] = n[c];
-            cpre[j][m] = a.cost[rr];
-        }
-    __builtin_amdgcn_sched_barrier(0);   // every load above is issued before the reductions wait for any
-    const int cc = T < C ? T : 0, e = k * C + cc;
-    // min / max / count (weights_gradient_kernel's stats path)
-    static_assert(CS_SLOTS == 64, "one slot per lane");
-    const unsigned long long kn = mppi_dev::wave_umin64_dpp(kmn), kx = mppi_dev::wave_umax64_dpp(kmx);
-    const unsigned int nv = (unsigned int)mppi_dev::wave_sum_dpp((double)kct);
-    const double minimum = nv ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
-    const double maximum = nv ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
-    const bool all_nan = (double)nv <= 1.0;   // minmax_element over <= 1 element: it1 == it2 -> throw
-    const double difference = maximum - minimum;
-    const bool early = all_nan || difference < 1e-6;   // early return (mppi.cpp:373-375)
-    WfFinishIn fin;
-    if (early) fin.load(f, e, cc, T);
-    if (!early) {
-        auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
-        double acc[WF_NJ][C], part[WF_NJ];
-#pragma unroll
-        for (int j = 0; j < WF_NJ; j++) {
-            {   // the first row starts the sums (0 + x is x: the same values as from zero), so the
-                // sums take over its eps registers
-                const int r = r0[j] + t;
-                const bool in = r < r1[j];
-                const double wr = expw(cpre[j][0]);
-                if (k == 0 && in) a.wexp[r] = wr;
-                part[j] = in ? wr : 0.0;
-#pragma unroll
-                for (int c = 0; c < C; c++) acc[j][c] = in ? wr * ne[j][0][c] : 0.0;
-            }
-#pragma unroll
-            for (int m = 1; m < WF_GR; m++) {
-                const int r = r0[j] + t + 256 * m;
-                if (r < r1[j]) {
-                    const double wr = expw(cpre[j][m]);
-                    if (k == 0) a.wexp[r] = wr;
-                    part[j] += wr;
-#pragma unroll
-                    for (int c = 0; c < C; c++) acc[j][c] += wr * ne[j][m][c];
-                }
-            }
-            for (int r = r0[j] + t + 256 * WF_GR; r < r1[j]; r += 256) {
-                const double wr = expw(a.cost[r]);
-                if (k == 0) a.wexp[r] = wr;
-                part[j] += wr;
-                const double *n = a.noise + (kb + (unsigned)r) * (unsigned)C;
-#pragma unroll
-                for (int c = 0; c < C; c++) acc[j][c] += wr * n[c];
-            }
-        }
-        fin.load(f, e, cc, T);   // behind the sums (their eps registers are free), ahead of the butterflies
-#pragma unroll
-        for (int j = 0; j < WF_NJ; j++) {
-            part[j] = wave_sum(part[j]);
-#pragma unroll
-            for (int c = 0; c < C; c++) acc[j][c] = wave_sum(acc[j][c]);
-            if (l == 0) {
-                ssum[sl + SS * j][rw] = part[j];
-#pragma unroll
-                for (int c = 0; c < C; c++) red[sl + SS * j][rw][c] = acc[j][c];
-            }
-        }
-    }
-    __syncthreads();
-    const bool upd = !early && !wt, ok = !all_nan && !wt;   // no filter: no SG error
-    double total = 0.0;
-    if (T < C || (k == 0 && T < GRAD_SPLIT)) {
-        // the normaliser: the eight slice sums (four wave sums each) in order (softmin_total)
-#pragma unroll
-        for (int s = 0; s < GRAD_SPLIT; s++) {
-            const double ts = (ssum[s][0] + ssum[s][1]) + (ssum[s][2] + ssum[s][3]);
-            total = s == 0 ? ts : total + ts;
-        }
-    }
-    if (T < C) {   // finish_flat_kernel's element (k, T)
-        double g = 0.0;
-#pragma unroll
-        for (int s = 0; s < GRAD_SPLIT; s++) {
-            const double p = (red[s][0][T] + red[s][1][T]) + (red[s][2][T] + red[s][3][T]);
-            g = s == 0 ? p : g + p;
-        }
-        g /= total;   // sum_r e_r eps_r / sum_r e_r
-        double u = fin.us;
-        if (upd) {
-            f.gradient[e] = g;
-            u += g * f.gradient_step;
-            if (f.control_bound) {
-                u = smin(u, fin.hi);
-                u = smax(u, fin.lo);
-            }
-            f.Ushift[e] = u;
-        }
-        const double v = ok ? u : fin.uo;
-        if (ok) f.U[e] = v;
-        pub(f.out + e, v);
-    }
-    if (k == 0) {   // the weights kernel's lead and slice blocks, finish's x0 copy
-        Status *st = a.status;
-        if (T == 0) {
-            st->all_nan = all_nan;
-            st->early = early;
-            st->minimum = minimum;
-            st->maximum = maximum;
-            if (upd) f.status_w->total = total;
-        }
-        if (!early && T < GRAD_SPLIT) st->tsplit[T] = (ssum[T][0] + ssum[T][1]) + (ssum[T][2] + ssum[T][3]);
-        if (T < f.X) f.x0_opt[T] = fin.x0;
-    }
-    for (int64_t i = (int64_t)k * WF_NT + T; i < f.rank_n; i += (int64_t)gridDim.x * WF_NT) f.rank_zero[i] = 0;
-    __builtin_amdgcn_s_waitcnt(0);   // this wave's host-block stores acknowledged, its statistics read
-    __syncthreads();
-    if (T == 0) last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x;
-    __syncthreads();
-    if (!last) return;
-    // every block has stored its step and read the statistics: the status words, the reset, the flag
-    if (T == 0) {
-        f.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
-        pub(f.out + HC + 0, fin.oc);
-        pub(f.out + HC + 1, (double)all_nan);
-        pub(f.out + HC + 2, (double)early);
-        pub(f.out + HC + 3, 0.0);
-        pub(f.out + HC + 4, minimum);
-        pub(f.out + HC + 5, maximum);
-        pub(f.out + HC + 7, (double)wt);
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next update
-    }
-    if (f.stats_reset) mppi_sample::reset_cost_stats(f.stats_reset, T);
-    publish_block(f);
-}
 
 
 
@@ -1778,9 +1102,6 @@ namespace mppi_eng {
 
 hipError_t launch_rank(const double *cost, int64_t S, int *rank, uint64_t *sorted, hipStream_t s)
 {
-#ifdef DIAG_SKIP_RANK   // timing diagnostics only: the kept rollouts are then not the best ones
-    return hipSuccess;
-#endif
     if (S <= 0) return hipSuccess;
     if (S <= RANK_TILED_MAX) {   // rank[] zeroed by the finish kernel (or at create)
         const unsigned nb = (unsigned)((S + RANK_T - 1) / RANK_T);
@@ -1813,14 +1134,6 @@ hipError_t launch_sample(const SampleArgs &a, bool tdiag, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s)
-{
-    const unsigned nb = (unsigned)((a.count + FR_NT - 1) / FR_NT);
-    if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(fr_rollout_kernel, dim3(nb), dim3(FR_NT), 0, s, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 {
     const unsigned nb = (unsigned)((a.count + 255) / 256);
@@ -1831,9 +1144,8 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s)
 {
-    const dim3 grid((unsigned)a.H, GRAD_SPLIT, a.C == FR_C ? GRAD_CSPLIT : 1);
+    const dim3 grid((unsigned)a.H, GRAD_SPLIT);
     if (a.C != FR_C && a.C != 3) return hipErrorInvalidValue;
-    static_assert(FR_C % GRAD_CSPLIT == 0, "whole component splits");
     if (a.R > SM_LARGE_R) {
         hipLaunchKernelGGL(softmin_minmax_kernel, dim3(SM_NB), dim3(256), 0, s, a);
         hipLaunchKernelGGL(softmin_exp_kernel, dim3(SM_NB), dim3(256), 0, s, a);
@@ -1848,20 +1160,6 @@ hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_s
     const int HC = a.H * a.C;
     hipLaunchKernelGGL(gradient_sum_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, a.gsplit, GRAD_SPLIT, HC,
                        (const Status *)a.status, gpart);
-    return hipGetLastError();
-}
-
-bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f)
-{
-    return a.C == FR_C && f.C == FR_C && a.stats != nullptr && a.R <= SM_LARGE_R && a.begin == 0 && a.count == a.R &&
-           f.sg_window == 0 && f.wait_all == nullptr && f.ns == GRAD_SPLIT && f.H == a.H && f.X <= WF_NT &&
-           a.Rpad >= a.R && (int64_t)a.H * a.Rpad * a.C * (int64_t)sizeof(double) < ((int64_t)1 << 31);
-}
-
-hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, unsigned *ticket, hipStream_t s)
-{
-    if (!weights_finish_eligible(a, f) || ticket == nullptr) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(weights_finish_kernel<FR_C>, dim3((unsigned)a.H), dim3(WF_NT), 0, s, a, f, ticket);
     return hipGetLastError();
 }
 

@@ -7,10 +7,6 @@
 #include "engine_types.hpp"
 #include "../../include/mppi_amd.h"
 
-#ifndef GRAD_SPLIT_DEF
-#define GRAD_SPLIT_DEF 8
-#endif
-
 namespace mppi_eng {
 
 // Device-side outcome of optimise() (mppi.cpp:344-375) and of the smoothing filter.
@@ -18,13 +14,13 @@ struct Status {
     int all_nan;     // <= 1 valid rollout: "all nan rollouts" (mppi.cpp:369-370)
     int early;       // max - min < 1e-6 (or all_nan): weights / gradient / U* untouched
     int sg_error;    // SavitzkyGolay window threw (filter.cpp:37-44, 73-82)
-    int handover;    // fr_coop_x_kernel: step at which the fifth wave's rows moved (take_over), or -1
+    int handover;    // fr_coop_x_kernel: the step relay stage 1 starts at (relay_stage), or -1 without the relay
     // fr_coop_x_kernel: bounded in-launch waits that gave up in this update's rollout launch (some
     // rows' costs were then never written): the finish kernels fail the update on it and reset it
     int wait_timeouts;
     int pad[3];
     double minimum, maximum, total;   // total: the softmin normaliser, summed by the finish kernels
-    double tsplit[GRAD_SPLIT_DEF];    // its GRAD_SPLIT partial sums (weights_gradient_kernel)
+    double tsplit[8];           // its GRAD_SPLIT partial sums (weights_gradient_kernel)
 };
 
 // min / max / count of the update's non-NaN costs, accumulated with order-independent atomics on
@@ -118,12 +114,6 @@ struct FinishArgs {
     double *wait_local;
 };
 
-struct EpArgs {
-    WGradArgs wg;
-    FinishArgs fin;
-};
-constexpr int EP_STAMPS = 8;   // epilogue stamps: barrier arrival, barrier passed, units stored, published (finisher);
-                                // the finisher's ticket, loads done, stores issued, stores acknowledged
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;
@@ -151,13 +141,13 @@ struct FrRolloutArgs {
     // one rollout's records are contiguous), and the folded / standalone filter() row's [H][FR_NREC]
     double *rec, *frec;
     // U*_shifted row k is Ushift row min(k + ush, H - 1): ush = 0 with U*_shifted itself, the
-    // update's shift with U* (fused sampling)
+    // update's shift with U* (draws made ahead)
     int ush;
-    // fuse_sample: the launch samples its own rows' eps (samp, sample_device.hpp) before the
-    // horizon loop instead of a sample_kernel launch ahead of it (1), or only copies the kept
-    // rollouts' columns into draws made ahead (2, draw_ahead_kernel); x0 comes from samp.x0v.
-    // Block 0 writes U*_shifted and x0 back for the kernels after it.
-    int fuse_sample;
+    // drawn_ahead: the eps tensor holds this update's draws, made behind the previous update
+    // (rank_draw_kernel, the previous launch's tail draws); the launch only copies the kept
+    // rollouts' columns into it (samp), and x0 comes from samp.x0v.  Block 0 writes U*_shifted and
+    // x0 back for the kernels after it.
+    int drawn_ahead;
     SampleArgs samp;
     // costs_in_launch (set by launch_fr_coop_update): the waves evaluate the objective of the rows
     // after their horizon loops (fr_coop.hip launch_costs) instead of fr_step_cost_kernel; stats as
@@ -167,33 +157,15 @@ struct FrRolloutArgs {
     // the next update's draws for the main waves' own rows, made in the launch's idle tail into
     // this buffer (fr_coop.hip tail_draws; null: none): rank_draw_kernel then draws only the rest
     double *ahead_noise;
-    // fr_coop_x_kernel: the fifth wave's rows move to the first of waves 1..3 to end its own rows
-    // (fr_coop.hip take_over; MPPI_HANDOVER=0 keeps them on the doubled SIMD)
+    // fr_coop_x_kernel: the rows left over travel through four relay stages (fr_coop.hip
+    // relay_stage; MPPI_HANDOVER=0 keeps them on one wave beside main wave 0)
     int handover;
-    // relay2 (fr_coop_x_kernel): the relay's eight stages over two workgroups, block 0 (stages 0..3,
-    // steps before the split) and block 8 (4..7): the state crosses once, with the first half's
-    // step-cost sums, through relay_buf (write-through) behind relay_flag[0] / [1] == relay_epoch
-    int relay2;
-    unsigned relay_epoch;
-    double *relay_buf;            // [64 * 3] the lanes' (q, qd, E) at the split, then [4] the rows' J so far
-    unsigned *relay_flag;         // [2] monotonic: the state handed over, the first half's sums written
     // sharded over RCCL: the rank's slot R of the cost vector the engine all-reduces, to which every
     // in-launch wait that gives up adds 1 (so every rank's finish kernel sees any rank's), or null
     double *wait_sum;
     // MPPI_DEBUG_* fault injection (mppi_debug_inject; 0 in production): bit 0, relay stage 1 of
     // the workgroup with rows left over never signals stage 2 (tests the wait-timeout failure)
     int debug;
-    // epilogue (fr_coop_x_kernel, one round, draws ahead, no smoothing, unsharded): after an
-    // in-launch grid barrier the workgroups run weights_gradient_kernel's (step, split) units and
-    // the last to arrive runs finish_flat_kernel's publish, in place of those two launches
-    int epilogue;
-    unsigned *ep_sync;            // [2] barrier and ticket counters (monotonic)
-    unsigned ep_target;           // their value once every workgroup of this launch has added 1
-    uint64_t *ep_stamps;          // diagnostics (MPPI_EP_STAMPS=1): [groups][EP_STAMPS] s_memrealtime, or null
-    // the epilogue's weights_gradient_kernel and finish_flat_kernel arguments, in device memory (the
-    // launch's kernel arguments stay small: the launch call's host cost grows with their size,
-    // ~1.8 us more for 1144 bytes than for 16, tools/probe/launch_cost.hip)
-    const EpArgs *ep;
 };
 
 // Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
@@ -313,9 +285,8 @@ struct RankDrawLaunch {
 hipError_t launch_draw_ahead(const SampleArgs &a, const double *cost, int64_t S, int *rank, uint64_t *sorted,
                              hipStream_t s, int sub_nxb = 0, int64_t sub_xbase = 0, int64_t sub_row0 = 0,
                              RankDrawLaunch *out = nullptr, bool dry = false);
-hipError_t launch_fr_rollout(const FrRolloutArgs &a, hipStream_t s);
 hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s);
-constexpr int GRAD_SPLIT = GRAD_SPLIT_DEF;   // rollout ranges per step in the gradient's first stage
+constexpr int GRAD_SPLIT = 8;   // rollout ranges per step in the gradient's first stage
 static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser partials");
 
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
@@ -339,31 +310,26 @@ struct CoopTail {
     int nxb = 0;         // workgroups of that launch whose first wave's rows rank_draw_kernel draws
     int launches = 1;
 };
-hipError_t launch_fr_coop_update(const FrRolloutArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
+struct EnvSwitches;
+hipError_t launch_fr_coop_update(const FrRolloutArgs &a, const EnvSwitches &env, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final = nullptr, bool *x_kernel = nullptr,
                                  bool dry = false, CoopTail *tail = nullptr, FrRolloutArgs *final2 = nullptr);
-bool fr_coop_update_fusable(int64_t count);
-bool fr_coop_update_split(int64_t count);   // the two-launch case of launch_fr_coop_update
-bool fr_coop_costs_in_launch();   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
-// A/B switches from the environment, read once per mppi_create (tests set them before creating a
-// handle) instead of by getenv on every update (~80 ns each on the host's path between updates)
+bool fr_coop_update_fusable(int64_t count, const EnvSwitches &env);
+bool fr_coop_update_split(int64_t count, const EnvSwitches &env);   // the two-launch case of launch_fr_coop_update
+bool fr_coop_costs_in_launch(const EnvSwitches &env);   // the objective runs in the update launch (MPPI_COSTS_IN_LAUNCH != 0)
+// A/B switches from the environment, read once per mppi_create into the handle (tests set them
+// before creating a handle): a handle's launch paths never change under it, and no getenv runs on
+// the update path (~80 ns each)
 struct EnvSwitches {
-    bool draw_ahead_off, tail_draws_off, fuse_sample, epilogue, pm_fused_off, costs_in_launch_off, handover_off, split_off,
-        relay2_off, weights_finish, stream_prio_off;
+    bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off;
 };
-const EnvSwitches &env_switches();
-void env_switches_refresh();
+EnvSwitches env_switches_read();
 // Whether a pending filter() folds into the update launch of `count` rows with the objective in
 // the launch (fr_coop_x_kernel, one launch or the split's two): the hipGraph path's launch shape
-bool fr_coop_update_folds(int64_t count, int H);
+bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
-hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);   // one round of four-wave groups: a.fuse_sample allowed
+hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
-// optimise() + finish() as one launch of H blocks (weights_finish_kernel, bit-identical to the two
-// launches); eligible: unsharded, cost statistics from the rollout launch, no Savitzky-Golay,
-// R <= SM_LARGE_R, FrankaRidgeback's C.  ticket: a device counter at zero (left at zero).
-bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f);
-hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, unsigned *ticket, hipStream_t s);
 
 // FrankaRidgeback::PinocchioDynamics as one device-resident object (fr_object.hip): the members of
 // pinocchio_dynamics.hpp:380-425 the methods read and write.
@@ -402,7 +368,10 @@ constexpr int PM_FUSED_MAX_BLOCKS = 256;          // one per CU: the grid barrie
 // rollouts per block: the fewest of 16, 32, 64 whose grid (at most 256 blocks) and LDS (the
 // finisher stages every block's partials) fit, so that the rank and the draws spread over the most
 // CUs; 0 when none does
+// (every block must be resident at once for the in-launch grid barrier: pm_fused_set_device gives
+// the device's CUs and LDS, and a shape that does not fit takes the five launches)
 int pm_fused_rows(int64_t R, int H);
+void pm_fused_set_device(int device);
 struct PmFusedArgs {
     DevPointMass pm;
     const StepConst *steps;     // [H] gamma_k

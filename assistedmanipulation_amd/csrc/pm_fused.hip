@@ -55,10 +55,7 @@ constexpr int PC = 3;                  // control dimension of the point mass
 __device__ __forceinline__ void pub(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 constexpr int BAR_SPINS = 1 << 22;     // about a second of s_sleep 1
 constexpr int IB = 8;                  // phase A items per thread per batch of loads
-#ifndef PM_SB
-#define PM_SB 32
-#endif
-constexpr int SB = PM_SB;              // sc1 loads per thread per batch (the finisher's and the rank's staging)
+constexpr int SB = 32;              // sc1 loads per thread per batch (the finisher's and the rank's staging)
 
 __device__ __forceinline__ double ld_sc1(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -300,7 +297,8 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     if (t == 0) {
         __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int i = 0;
-        while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && i < BAR_SPINS) {
+        // wrap-safe: the counter and target = epoch * nb both wrap at 2^32 (every 2^32 / nb updates)
+        while ((int)(__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0 && i < BAR_SPINS) {
             __builtin_amdgcn_s_sleep(1);
             i++;
         }
@@ -351,9 +349,6 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     // the rank's keys (every block's tail), and in the finishing block every block's partials
     // (gradient [nb][HC], then normalisers [nb]) over the eps rows: one batch of sc1 loads, SB per
     // thread in flight at once (the other blocks stored them this launch)
-#ifdef PM_STAGE_PLAIN
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (A/B) one invalidate, then plain loads
-#endif
     double *Lst = Leps;
     const int G = nb * HC, np = (s_last && !early) ? G + nb : 0, n = np + S;
     // with the batch, unconditionally (a branch or a loop header here makes their wait a trip)
@@ -420,19 +415,12 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             pub(a.out + HC + 7, (double)wt);
         }
         if (t < CS_SLOTS) mppi_sample::reset_cost_stats(a.stats, t);   // every block has read them (ticket)
-#ifndef PUB_FENCE   // the host block's stores acknowledged, then the flag (kernels.hip publish_block)
         __builtin_amdgcn_s_waitcnt(0);
-#endif
         __syncthreads();
         stamp(7);
         if (t == 0) {
             st->wait_timeouts = 0;
-#ifdef PUB_FENCE
-            __threadfence_system();
-            __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
             __hip_atomic_store(a.out + HC + 6, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
         }
         stamp(8);
     }
@@ -485,14 +473,40 @@ static size_t lds_bytes(int PR, int64_t R, int H)
     return (size_t)((HC + H + 2 * PR + (R - 2) + pm_region(PR, HC, nb) + HC + 6) * 8 + (PT / PR - 1) * PR * 4);
 }
 
+// The in-launch grid barrier needs every block resident at once: the most blocks of each variant
+// the device holds together (occupancy per CU at the variant's LDS, times the CUs), set at create
+// (pm_fused_set_device); until then the grid's bound alone
+static int g_pm_cus = 0, g_pm_lds_max = 0;
+
+static int resident_blocks(int PR, size_t lds)
+{
+    if (g_pm_cus <= 0) return PM_FUSED_MAX_BLOCKS;
+    if (lds > (size_t)g_pm_lds_max) return 0;
+    int per_cu = 0;
+    hipError_t e = hipErrorInvalidValue;
+    if (PR == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<16>, PT, lds);
+    else if (PR == 32) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<32>, PT, lds);
+    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<64>, PT, lds);
+    return e == hipSuccess ? per_cu * g_pm_cus : 0;
+}
+
+void pm_fused_set_device(int device)
+{
+    int cus = 0, lds = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 0;
+    g_pm_cus = cus;
+    g_pm_lds_max = lds;
+}
+
 int pm_fused_rows(int64_t R, int H)
 {
     if (R < 4 || H < 1 || R > PM_FUSED_MAX_R) return 0;
-#ifndef PM_MIN_ROWS
-#define PM_MIN_ROWS 16
-#endif
-    for (int PR = PM_MIN_ROWS; PR <= 64; PR *= 2)
-        if ((R + PR - 1) / PR <= PM_FUSED_MAX_BLOCKS && lds_bytes(PR, R, H) <= 150 * 1024) return PR;
+    for (int PR = 16; PR <= 64; PR *= 2) {
+        const int64_t nb = (R + PR - 1) / PR;
+        const size_t lds = lds_bytes(PR, R, H);
+        if (nb <= PM_FUSED_MAX_BLOCKS && lds <= 150 * 1024 && nb <= resident_blocks(PR, lds)) return PR;
+    }
     return 0;
 }
 

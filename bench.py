@@ -363,22 +363,19 @@ def run(args, world, rank, local_rank, dist):
             roofline["traffic_source"] = recorded_label(PMC_PM_JSON)
         survey_bytes = BYTES_SURVEY_PM
     else:
-        lane = info["cooperative"] == 0   # MPPI_FR_KERNEL=lane A/B: the fused one-lane-per-rollout kernel
         in_launch = info["objective_in_launch"] == 1
-        flops_unit = FLOPS_PER_ROLLOUT_STEP if (in_launch or lane) else FLOPS_DYN_PER_ROLLOUT_STEP
+        flops_unit = FLOPS_PER_ROLLOUT_STEP if in_launch else FLOPS_DYN_PER_ROLLOUT_STEP
         rows_units = info["rows"] * traj.H   # rollout rows of the launch (+ a folded filter() row)
         achieved_tflops = flops_unit * rows_units / (dyn_ms * 1e-3) / 1e12
         traffic = None
-        if os.path.exists(PMC_JSON) and world == 1 and default_workload and not lane:
+        if os.path.exists(PMC_JSON) and world == 1 and default_workload:
             with open(PMC_JSON) as f:
                 traffic = json.load(f)["traffic_bytes"]
         # the launch's HBM bytes by design: eps read, step records written and (objective in the
         # launch) read back, the next update's eps written in the tail (tail draws)
         launch_bytes = ((BYTES_EPS_FR + BYTES_REC * (2 if in_launch else 1)) * rows_units
-                        + (BYTES_EPS_FR * units if info["tail_draws"] else 0.0)) if not lane else BYTES_EPS_FR * units
-        roofline = {"bound": "valu", "kernel": "fr_rollout_kernel" if lane else (
-                        ("fr_coop_x_kernel (dynamics + objective + optimise/finish epilogue)" if info.get("fused_update")
-                         else "fr_coop_x_kernel (dynamics + objective)") if in_launch else "fr_coop_kernel"),
+                        + (BYTES_EPS_FR * units if info["tail_draws"] else 0.0))
+        roofline = {"bound": "valu", "kernel": "fr_coop_x_kernel (dynamics + objective)" if in_launch else "fr_coop_kernel",
                     "compute": "fp64 VALU, issue-bound at one wave per SIMD (no dense contraction for MFMA)",
                     "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
@@ -401,13 +398,10 @@ def run(args, world, rank, local_rank, dist):
     # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
     # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
     # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
-    # (with optimise() and finish() as one launch, weights_finish_kernel, that launch is the
-    # breakdown's reduce phase kt[2]: the weight reduce plus the finish's few hundred bytes)
-    wf = not pm and info.get("fused_update") == 2
-    wg_ms = kt[2] if wf else kt[6]
+    wg_ms = kt[6]
     if wg_ms > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
         wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
-        wg = {"kernel": "weights_finish_kernel (optimise + finish)" if wf else "weights_gradient_kernel", "bound": "hbm",
+        wg = {"kernel": "weights_gradient_kernel", "bound": "hbm",
               "ms": wg_ms, "bytes_per_launch": wg_bytes,
               "achieved_GBs": wg_bytes / (wg_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
         wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS

@@ -333,12 +333,14 @@ mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count);
 
 /* Phase-split update for callers that run the collectives themselves (multi-GPU with an
  * external communicator, or two shards on one device in tests).  Between phase 1 and 2 the
- * caller all-reduces (sum) mppi_device_costs(h); between phase 2 and 3 it all-reduces (sum)
- * mppi_device_gradient(h).  Buffers are fp64 device pointers on mppi_stream(h). */
+ * caller all-reduces (sum) the R + 1 doubles of mppi_device_costs(h) - the R costs and slot R,
+ * the ranks' in-launch wait timeouts, so that every rank fails an update whose costs some rank
+ * lost (MPPI_ERR_DEVICE); between phase 2 and 3 it all-reduces (sum) mppi_device_gradient(h).
+ * Buffers are fp64 device pointers on mppi_stream(h). */
 mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time);
 mppi_status mppi_update_phase2(mppi_handle *h);
 mppi_status mppi_update_phase3(mppi_handle *h);
-void *mppi_device_costs(mppi_handle *h);     /* R doubles */
+void *mppi_device_costs(mppi_handle *h);     /* R + 1 doubles (the costs, then the wait-timeout count) */
 void *mppi_device_gradient(mppi_handle *h);  /* C*H doubles */
 void *mppi_stream(mppi_handle *h);           /* hipStream_t */
 
@@ -378,23 +380,20 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 
 /* What the last update's rollout launch did (diagnostics for bench / tests; the engine decides it
  * from the device's CU count and the workload): info[i] for i < n (n <= MPPI_UPDATE_INFO_N). */
-#define MPPI_INFO_COOPERATIVE 0           /* 16-lane cooperative kernel (else one lane per rollout) */
+#define MPPI_INFO_COOPERATIVE 0           /* 1: the 16-lane cooperative kernel (FrankaRidgeback), 0: the point mass */
 #define MPPI_INFO_FOLDED_FILTER 1         /* the previous update's filter() rode in the launch */
 #define MPPI_INFO_OBJECTIVE_IN_LAUNCH 2   /* the objective ran in the launch (no cost kernel) */
 #define MPPI_INFO_TAIL_DRAWS 3            /* the launch drew the next update's eps (main rows) */
-#define MPPI_INFO_SAMPLING 4              /* 0 sample kernel, 1 sampled in launch, 2 drawn ahead */
+#define MPPI_INFO_SAMPLING 4              /* 0 sample kernel, 1 sampled in the launch (point mass), 2 drawn ahead */
 #define MPPI_INFO_ROWS 5                  /* rows rolled out (local rollouts + a folded filter()) */
-#define MPPI_INFO_HANDOVER 6              /* step at which the fifth wave's rows moved off the doubled
-                                             SIMD (take_over), -1 none; read from the device */
+#define MPPI_INFO_HANDOVER 6              /* step at which relay stage 1 took the rows left over
+                                             (relay_stage), -1 none; read from the device */
 #define MPPI_INFO_WAIT_TIMEOUTS 7         /* in-launch waits that gave up in the last update's
                                              rollout launch (a bug if nonzero: that update then
                                              failed with MPPI_ERR_DEVICE and published nothing) */
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
-#define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass), or
-                                             optimise() and finish() ran in the rollout launch
-                                             (FrankaRidgeback, opt-in MPPI_EPILOGUE=1); 2: optimise()
-                                             and finish() ran as one launch after it (opt-in
-                                             MPPI_WEIGHTS_FINISH=1, weights_finish_kernel) */
+#define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass,
+                                             pm_update_kernel) */
 #define MPPI_UPDATE_INFO_N 10
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 

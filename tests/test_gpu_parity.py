@@ -212,7 +212,7 @@ def test_two_shards_on_one_device_equal_unsharded(S, hor):
             sh.inject_noise(eps)
             sh.update_phase1(x, t)
         hip.hipDeviceSynchronize()
-        allreduce([sh.device_costs_ptr() for sh in shards], R)
+        allreduce([sh.device_costs_ptr() for sh in shards], R + 1)   # + slot R: wait timeouts
         for sh in shards:
             sh.update_phase2()
         hip.hipDeviceSynchronize()
@@ -358,36 +358,6 @@ def test_device_against_golden_fixtures(fixture):
         assert abs(dev.get_optimal_total_cost() - g["opt_cost"][j]) <= 1e-11 * abs(g["opt_cost"][j])
 
 
-@pytest.mark.parametrize("rollouts,injected", [(2046, False), (1000, False), (2046, True)])
-def test_fused_sampling_matches_sample_kernel(rollouts, injected, monkeypatch):
-    """The update launch's own sampling (MPPI_FUSE_SAMPLE=1: eps drawn in the rollout kernel's
-    prologue, U*_shifted read from U* with the shift) gives the same bits as the separate
-    sample_kernel over several shifted updates with kept rollouts (R = 2048: the fifth-wave rows
-    and the folded filter() row; R = 1002: leftover rows in several workgroups)."""
-    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.32, keep_best_rollouts=20, threads=8)
-    out = {}
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("MPPI_FUSE_SAMPLE", fuse)
-        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
-        rng = np.random.default_rng(11)
-        if injected:
-            t.set_noise_source(abi.MPPI_NOISE_HOST_INJECTED)
-        else:
-            t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
-        t.set_forecast(am.constant_forecast(t.H))
-        x = am.huddled_state()
-        rec = []
-        for j in range(4):
-            if injected:
-                t.inject_noise(rng.standard_normal((t.noise_draws(0.05 * j), t.C)) * 0.1)
-            t.update(x, 0.05 * j)
-            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
-        out[fuse] = rec
-    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
-        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
-            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
-
-
 @pytest.mark.parametrize("rollouts,objective", [(2046, "am"), (1000, "am"), (4096, "am"), (2046, "energy"),
                                                 (1000, "track_point"), (4096, "track_point")])
 def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
@@ -488,7 +458,7 @@ def test_two_philox_shards_draw_ahead_equal_unsharded():
         for sh in shards:
             sh.update_phase1(x, t)
         hip.hipDeviceSynchronize()
-        allreduce([sh.device_costs_ptr() for sh in shards], R)
+        allreduce([sh.device_costs_ptr() for sh in shards], R + 1)   # + slot R: wait timeouts
         for sh in shards:
             sh.update_phase2()
         hip.hipDeviceSynchronize()
@@ -687,6 +657,61 @@ def test_in_launch_wait_timeout_fails_the_update():
         step_both(dev, orc, x, 0.05 * j, rng, sd)
         assert dev.update_info()["wait_timeouts"] == 0
         assert_update_parity(dev, orc, "after timeout %d" % j)
+
+
+def test_wait_timeout_on_one_shard_fails_every_shard():
+    """Phase-split shards (an external communicator's view): the caller all-reduces the
+    R + 1 doubles of mppi_device_costs, slot R being each rank's in-launch wait timeouts.  A relay
+    stage of shard 0 that never signals (mppi_debug_inject) loses shard 0's relay rows, so both
+    shards fail the update with MPPI_ERR_DEVICE - shard 1 from the all-reduced count alone - and
+    both publish nothing; the next update succeeds on both with no timeout."""
+    conf = am.frankaridgeback_configuration(rollouts=4096, horison=0.32, keep_best_rollouts=20, threads=8)
+    shards = []
+    for r in range(2):
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=7)
+        t.set_forecast(am.constant_forecast(t.H))
+        t.set_shard(2, r)
+        shards.append(t)
+    hip = _hip()
+    R, HC = shards[0].R, shards[0].H * shards[0].C
+    x = am.huddled_state()
+
+    def allreduce(ptrs, n):
+        bufs = [np.zeros(n) for _ in ptrs]
+        for p, b in zip(ptrs, bufs):
+            assert hip.hipMemcpy(b.ctypes.data, p, n * 8, 2) == 0   # D2H
+        s = bufs[0] + bufs[1]
+        for p in ptrs:
+            assert hip.hipMemcpy(p, s.ctypes.data, n * 8, 1) == 0   # H2D
+        return s
+
+    def update(t, expect_fail):
+        for sh in shards:
+            sh.update_phase1(x, t)
+        hip.hipDeviceSynchronize()
+        s = allreduce([sh.device_costs_ptr() for sh in shards], R + 1)
+        for sh in shards:
+            sh.update_phase2()
+        hip.hipDeviceSynchronize()
+        allreduce([sh.device_gradient_ptr() for sh in shards], HC)
+        for sh in shards:
+            if expect_fail:
+                with pytest.raises(am.EngineError, match="wait timed out"):
+                    sh.update_phase3(t)
+            else:
+                sh.update_phase3(t)
+        return s[R]
+
+    assert update(0.0, False) == 0.0
+    u0 = [sh.get_optimal_rollout().copy() for sh in shards]
+    np.testing.assert_array_equal(u0[0], u0[1])
+    shards[0].debug_inject(abi.MPPI_DEBUG_RELAY_NO_SIGNAL, 1)
+    assert update(0.05, True) > 0   # shard 0's lost rows, counted in slot R
+    for sh, u in zip(shards, u0):
+        np.testing.assert_array_equal(sh.get_optimal_rollout(), u)   # nothing published
+    assert update(0.10, False) == 0.0
+    np.testing.assert_array_equal(shards[0].get_optimal_rollout(), shards[1].get_optimal_rollout())
 
 
 def test_folded_filter_row_against_oracle():

@@ -116,7 +116,7 @@ def test_eight_shards_equal_unsharded(S, horison, window):
         for sh in shards:
             sh.update_phase1(x, t)
         hip.hipDeviceSynchronize()
-        allreduce([sh.device_costs_ptr() for sh in shards], R)
+        allreduce([sh.device_costs_ptr() for sh in shards], R + 1)   # + slot R: wait timeouts
         for sh in shards:
             sh.update_phase2()
         hip.hipDeviceSynchronize()

@@ -21,7 +21,6 @@
 #                      built by tools/ab_build.sh; "tree" = the in-tree library); BENCH_ARGS and
 #                      AB_ENV_<V> (extra env for variant V, e.g. AB_ENV_tree0="MPPI_HANDOVER=0") apply
 #   pmstamps[:VARIANT] the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1), in-tree or a variant
-#   epstamps           the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1)
 #   wtrace:VARIANT     per-wave trace of VARIANT's COOP_TRACE build (tools/wave_trace_r03.py)
 # Output: gpurun_out/$TAG/.
 set -o pipefail
@@ -144,12 +143,6 @@ step_pmstamps() {   # [variant]: the fused point-mass kernel's phase stamps (MPP
     summary $O/$n.json $n
 }
 
-step_epstamps() {   # the rollout launch's epilogue phase stamps (MPPI_EP_STAMPS=1, printed at destroy)
-    MPPI_EPILOGUE=1 MPPI_EP_STAMPS=1 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline $BENCH_ARGS \
-        > $O/epstamps.json 2> $O/epstamps.err || { echo "epstamps rc=$?"; tail -20 $O/epstamps.err; return 1; }
-    grep "epilogue" $O/epstamps.err
-    summary $O/epstamps.json epstamps
-}
 
 step_wtrace() {   # variant
     local lib=$PWD/gpurun_variants/$1/libmppi_amd.so
@@ -175,7 +168,6 @@ for s in "$@"; do
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;
         pmstamps) step_pmstamps "$arg" ;;
-        epstamps) step_epstamps ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac || { echo "step $s failed"; exit 1; }
 done
