@@ -31,6 +31,7 @@ PROTOTYPES = {
     "mppi_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, _i64p, _i64p]),
     "mppi_comm_unique_id": (C.c_int, [C.c_char_p]),
     "mppi_comm_init": (C.c_int, [_h, C.c_int, C.c_int, C.c_char_p]),
+    "mppi_comm_info": (C.c_int, [_h, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "mppi_set_shard": (C.c_int, [_h, C.c_int, C.c_int]),
     "mppi_set_noise_source": (C.c_int, [_h, C.c_int, C.c_uint64]),
     "mppi_inject_noise": (C.c_int, [_h, _dp, C.c_int64]),
@@ -97,8 +98,16 @@ def load():
             "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
             "assistedmanipulation_amd/csrc`" % LIB_PATH)
     L = C.CDLL(LIB_PATH)
+    # a library chosen by MPPI_AMD_LIB (an older build under an A/B run) may lack later entry points:
+    # those stay unbound and fail when called; the in-tree library must export every one
+    ab = "MPPI_AMD_LIB" in os.environ
     for name, (res, args) in PROTOTYPES.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            if not ab:
+                raise
+            continue
         f.restype = res
         f.argtypes = args
     _lib = L

@@ -43,6 +43,7 @@ EnvSwitches env_switches_read()
     e.handover_off = is("MPPI_HANDOVER", '0');
     e.split_off = is("MPPI_SPLIT", '0');
     e.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
+    e.fused_finish_off = is("MPPI_FUSED_FINISH", '0');
     return e;
 }
 }  // namespace mppi_eng
@@ -61,6 +62,11 @@ struct DeviceBuf {
 struct mppi_handle {
     int device = 0;
     EnvSwitches env{};   // the A/B switches as the environment held them at create (env_switches_read)
+    // optimise() and finish() as one launch this update (weights_finish_kernel): its normaliser
+    // partials [GRAD_SPLIT][H] and its step / last-step tickets [H + 1] (left at zero by the kernel)
+    bool wf_fused = false;
+    double *d_tpart = nullptr;
+    unsigned *d_fin_tick = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
 
@@ -181,9 +187,10 @@ struct mppi_handle {
     double *h_opt = nullptr;     // pinned: optimal cost copied back on the side stream
     std::vector<void *> allocations;
     std::string err;
-    // hipGraph path (mppi_set_graph / MPPI_GRAPH=1): the steady-state update's four launches
-    // (rollout, weights + gradient, finish, rank + draws ahead) captured once and replayed with each
-    // update's arguments written into the executable graph's kernel nodes
+    // hipGraph path (mppi_set_graph / MPPI_GRAPH=1): the steady-state update's launches (rollout,
+    // weights + gradient, finish, rank + draws ahead; sharded, the two RCCL all-reduces between
+    // them) captured once and replayed with each update's arguments written into the executable
+    // graph's kernel nodes
     int graph_mode = 0;
     bool graph_dry = false;             // phases fill `gargs` instead of launching
     struct GraphArgs {
@@ -196,8 +203,13 @@ struct mppi_handle {
     } gargs;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    hipGraphNode_t gnode[5] = {};   // rollout launch(es), weights + gradient, finish, rank + draws
-    hipKernelNodeParams gparams[5] = {};
+    struct GraphNode {
+        hipGraphNode_t node;
+        int kind;   // GraphKernel; GK_ROLLOUT nodes in capture order: the split's first, then its second
+        int index;  // the kind's node count before this one
+        hipKernelNodeParams params;
+    };
+    std::vector<GraphNode> gnodes;   // the kernel nodes whose arguments each update rewrites
     int64_t graph_updates = 0;          // updates that ran as the graph (diagnostics)
     // in-launch waits that gave up (fr_coop.hip note_wait_timeout), summed over the updates
     int64_t wait_timeouts_total = 0;
@@ -959,6 +971,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
+    CREATE_TRY(dalloc(h, &h->d_tpart, (size_t)h->H * GRAD_SPLIT));
+    CREATE_TRY(dalloc(h, &h->d_fin_tick, (size_t)h->H + 1));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_cstats, 1));
     // the first update's statistics start empty (later ones are reset by the finish kernel)
@@ -1158,6 +1172,21 @@ mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char uniqu
     HIP_TRY(hipSetDevice(h->device));
     NCCL_TRY(ncclCommInitRank(&h->comm, world, id, rank));
     if (!h->d_costs_local) HIP_TRY(dalloc(h, &h->d_costs_local, (size_t)h->R + 1));   // + the wait-timeout slot
+    return MPPI_OK;
+}
+
+mppi_status mppi_comm_info(mppi_handle *h, int *nranks, int *rank, int *device, char *pci_bus_id, int len)
+{
+    if (!h || !nranks || !rank) return MPPI_ERR_INVALID;
+    if (h->comm) {   // what the communicator itself says, not what the caller asked for
+        NCCL_TRY(ncclCommCount(h->comm, nranks));
+        NCCL_TRY(ncclCommUserRank(h->comm, rank));
+    } else {
+        *nranks = 0;
+        *rank = -1;
+    }
+    if (device) *device = h->device;
+    if (pci_bus_id && len > 0) HIP_TRY(hipDeviceGetPCIBusId(pci_bus_id, len, h->device));
     return MPPI_OK;
 }
 
@@ -1783,9 +1812,17 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.wpart = h->d_wpart;
     w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     h->gargs.wg = w;
+    // optimise() and finish() as one launch where it applies (unsharded, no smoothing, the
+    // objective's statistics): phase 3 then launches no finish.  Sharded, the partial gradient is
+    // summed here and all-reduced before phase 3.  (MPPI_FUSED_FINISH=0: the two launches, A/B)
+    h->wf_fused = !h->env.fused_finish_off && weights_finish_eligible(w, finish_args(h));
+    if (h->wf_fused) h->gargs.fin = finish_args(h);   // its publish sequence: phase 3's
+    h->info[MPPI_INFO_FUSED_UPDATE] = h->wf_fused ? 2 : 0;
     if (h->graph_dry) return MPPI_OK;
-    // sharded: the partial gradient is summed here and all-reduced before phase 3
-    HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
+    // a filter() launched by itself on the side stream reads the d_U / d_x0_opt the finish rewrites
+    if (h->wf_fused && h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
+    if (h->wf_fused) HIP_TRY(launch_weights_finish(w, h->gargs.fin, h->d_tpart, h->d_fin_tick, h->stream));
+    else HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_wg, h->stream));
     return MPPI_OK;
 }
@@ -1797,7 +1834,7 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     h->gargs.fin = finish_args(h);
-    if (!h->graph_dry) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
+    if (!h->graph_dry && !h->wf_fused) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
     const double seq = (double)(++h->publish_seq);
     *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
@@ -1926,17 +1963,21 @@ mppi_status mppi_update_phase3(mppi_handle *h)
 
 // The hipGraph path: the steady-state update (FrankaRidgeback on the cooperative kernel, device
 // Philox with the draws made ahead, the previous filter() folded into the rollout launch, the
-// objective and the next draws in its tail, no smoothing, no device forecast, one device) is the
-// chain rollout -> weights + gradient -> finish -> rank + draws ahead.  It is captured from the
-// first such update's launches; later updates write their arguments (the same structs the eager
-// launches take: state and shift by value, the swapped eps buffers, the update index, the publish
-// sequence) into the executable graph's four kernel nodes and launch it once.  Anything else runs
-// the eager launches.
+// objective and the next draws in its tail, no device forecast) is the chain rollout(s) -> weights +
+// gradient -> finish -> rank + draws ahead, with or without the Savitzky-Golay finish; sharded over
+// the engine's RCCL communicator, ncclAllReduce of the costs after the rollouts and of the partial
+// gradient before the finish (configs[4]: "8 x MI355X ... hipGraph-captured control step").  It is
+// captured from the first such update's launches, RCCL's included; later updates write their
+// arguments (the same structs the eager launches take: state and shift by value, the swapped eps
+// buffers, the update index, the publish sequence) into the executable graph's kernel nodes and
+// launch it once.  Every rank captures at the same update and replays the graph once per update,
+// so the collectives stay matched.  Anything else runs the eager launches.
 static bool graph_eligible(const mppi_handle *h)
 {
-    if (!h->graph_mode || sharded(h) || h->timing != 0 || h->d_trace || h->host_trace) return false;
+    if (!h->graph_mode || h->timing != 0 || h->d_trace || h->host_trace) return false;
+    if (sharded(h) && !h->comm) return false;   // the phase-split API: the caller's collectives
     if (!draw_ahead_possible(h) || tail_draws_disabled(h) || !fr_coop_costs_in_launch(h->env)) return false;
-    if (h->fc.type != FC_NONE || h->S > RANK_TILED_MAX) return false;   // SG: sg_finish_kernel is the finish node
+    if (h->fc.type != FC_NONE) return false;   // (the device forecast's sampling launch is not a node)
     if (h->opt_state != mppi_handle::OPT_PENDING) return false;   // the previous filter() folds in
     // the launch path the replayed nodes assume: fr_coop_x_kernel with the filter() row folded and
     // the objective in the launch (a rollout count that is a multiple of 16 takes fr_coop_kernel<4>
@@ -1946,45 +1987,79 @@ static bool graph_eligible(const mppi_handle *h)
            h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
 }
 
+// The captured graph's kernel nodes in stream order (a topological order of the chain), classified
+// by kernel function; RCCL's nodes and the kernels with fixed arguments are left as captured
 static mppi_status graph_nodes(mppi_handle *h)
 {
     size_t n = 0;
-    const size_t want = 3 + (size_t)h->gargs.nroll;   // the split's two rollout launches (fr_coop.hip)
     HIP_TRY(hipGraphGetNodes(h->graph, nullptr, &n));
-    if (n != want || want > 5)
-        return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(n) + " nodes, expected " + std::to_string(want));
-    hipGraphNode_t nodes[5];
-    HIP_TRY(hipGraphGetNodes(h->graph, nodes, &n));
-    hipGraphNode_t cur = nullptr;
-    for (size_t i = 0; i < n; i++) {   // the chain's root
-        size_t deps = 0;
-        HIP_TRY(hipGraphNodeGetDependencies(nodes[i], nullptr, &deps));
-        if (deps == 0) cur = nodes[i];
-    }
-    for (int i = 0; i < (int)n; i++) {
-        if (!cur) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a kernel chain");
-        hipGraphNodeType ty;
-        HIP_TRY(hipGraphNodeGetType(cur, &ty));
-        if (ty != hipGraphNodeTypeKernel) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a kernel chain");
-        h->gnode[i] = cur;
-        HIP_TRY(hipGraphKernelNodeGetParams(cur, &h->gparams[i]));
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n) HIP_TRY(hipGraphGetNodes(h->graph, nodes.data(), &n));
+    std::vector<size_t> indeg(n, 0);
+    for (size_t i = 0; i < n; i++) HIP_TRY(hipGraphNodeGetDependencies(nodes[i], nullptr, &indeg[i]));
+    std::vector<bool> done(n, false);
+    h->gnodes.clear();
+    int count[6] = {0, 0, 0, 0, 0, 0};
+    for (size_t visited = 0; visited < n;) {   // Kahn's order over the dependency counts
+        size_t i = 0;
+        while (i < n && (done[i] || indeg[i] != 0)) i++;
+        if (i == n) return fail(h, MPPI_ERR_DEVICE, "captured update graph has a cycle");
+        done[i] = true;
+        visited++;
         size_t nd = 0;
-        HIP_TRY(hipGraphNodeGetDependentNodes(cur, nullptr, &nd));
-        if (i + 1 < (int)n && nd != 1) return fail(h, MPPI_ERR_DEVICE, "captured update graph is not a chain");
-        hipGraphNode_t next = nullptr;
-        if (nd == 1) HIP_TRY(hipGraphNodeGetDependentNodes(cur, &next, &nd));
-        cur = next;
+        HIP_TRY(hipGraphNodeGetDependentNodes(nodes[i], nullptr, &nd));
+        std::vector<hipGraphNode_t> next(nd);
+        if (nd) HIP_TRY(hipGraphNodeGetDependentNodes(nodes[i], next.data(), &nd));
+        for (hipGraphNode_t d : next)
+            for (size_t k = 0; k < n; k++)
+                if (nodes[k] == d && indeg[k] > 0) indeg[k]--;
+        hipGraphNodeType ty;
+        HIP_TRY(hipGraphNodeGetType(nodes[i], &ty));
+        if (ty != hipGraphNodeTypeKernel) continue;
+        mppi_handle::GraphNode g{nodes[i], GK_OTHER, 0, {}};
+        HIP_TRY(hipGraphKernelNodeGetParams(nodes[i], &g.params));
+        g.kind = fr_coop_is_update_kernel(g.params.func) ? GK_ROLLOUT : graph_kernel_kind(g.params.func);
+        if (g.kind == GK_OTHER) continue;
+        g.index = count[g.kind]++;
+        h->gnodes.push_back(g);
     }
+    // the launches the arguments are kept for: the rollout launch(es), one weights kernel (and the
+    // large-R softmin pair ahead of it), one finish, one rank + draws
+    const bool wf = h->wf_fused;   // optimise() and finish() as one node (weights_finish_kernel)
+    if (count[GK_ROLLOUT] != h->gargs.nroll || count[GK_RANKDRAW] != 1 ||
+        (wf ? (count[GK_WGFIN] != 1 || count[GK_WGRAD] != 0 || count[GK_FINISH] != 0)
+            : (count[GK_WGFIN] != 0 || count[GK_WGRAD] < 1 || count[GK_FINISH] != 1)))
+        return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(count[GK_ROLLOUT]) + " rollout, " +
+                                            std::to_string(count[GK_WGRAD]) + " weights, " + std::to_string(count[GK_FINISH]) +
+                                            " finish, " + std::to_string(count[GK_WGFIN]) + " weights + finish and " +
+                                            std::to_string(count[GK_RANKDRAW]) + " rank nodes");
+    return MPPI_OK;
+}
+
+// The eager path's collectives (mppi_update), captured with the launches
+static mppi_status allreduce_costs(mppi_handle *h)
+{
+    // R costs and slot R, every rank's in-launch wait timeouts (the finish kernels fail the
+    // update on all ranks alike when any rank's launch lost rows)
+    NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R + 1, ncclDouble, ncclSum, h->comm, h->stream));
+    return MPPI_OK;
+}
+static mppi_status allreduce_gradient(mppi_handle *h)
+{
+    NCCL_TRY(ncclAllReduce(h->d_gpart, h->d_gpart, (size_t)(h->H * h->C), ncclDouble, ncclSum, h->comm, h->stream));
     return MPPI_OK;
 }
 
 static mppi_status update_graph(mppi_handle *h, const double *state, double time)
 {
     const bool capture = h->graph_exec == nullptr;
+    const bool coll = h->comm != nullptr;
     if (capture) HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     else h->graph_dry = true;
     mppi_status st = mppi_update_phase1(h, state, time);
+    if (st == MPPI_OK && coll && capture) st = allreduce_costs(h);
     if (st == MPPI_OK) st = mppi_update_phase2(h);
+    if (st == MPPI_OK && coll && capture) st = allreduce_gradient(h);
     double seq = 0.0;
     if (st == MPPI_OK) st = phase3_launch(h, &seq);
     h->graph_dry = false;
@@ -2011,21 +2086,22 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
             return fail(h, MPPI_ERR_DEVICE, "graph update took another launch path");
         }
         RankDrawLaunch &rd = h->gargs.rd;
-        void *a0[] = {&h->gargs.roll};
-        void *a0b[] = {&h->gargs.roll2};
-        void *a1[] = {&h->gargs.wg};
-        void *a2[] = {&h->gargs.fin};
-        void *a3[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase, &rd.sub_row0};
-        void **args1[4] = {a0, a1, a2, a3};
-        void **args2[5] = {a0, a0b, a1, a2, a3};
-        const int nn = 3 + h->gargs.nroll;
-        void ***args = h->gargs.nroll == 2 ? args2 : args1;
-        for (int i = 0; i < nn; i++) {
-            hipKernelNodeParams p = h->gparams[i];
-            p.kernelParams = args[i];
+        void *aroll[2][1] = {{&h->gargs.roll}, {&h->gargs.roll2}};
+        void *awg[] = {&h->gargs.wg};
+        void *afin[] = {&h->gargs.fin};
+        void *awf[] = {&h->gargs.wg, &h->gargs.fin, &h->d_tpart, &h->d_fin_tick};
+        void *ard[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase, &rd.sub_row0};
+        for (const mppi_handle::GraphNode &g : h->gnodes) {
+            hipKernelNodeParams p = g.params;
             p.extra = nullptr;
-            if (i == nn - 1) p.gridDim = dim3(rd.grid);
-            HIP_TRY(hipGraphExecKernelNodeSetParams(h->graph_exec, h->gnode[i], &p));
+            switch (g.kind) {
+            case GK_ROLLOUT: p.kernelParams = aroll[g.index]; break;
+            case GK_WGRAD: p.kernelParams = awg; break;
+            case GK_FINISH: p.kernelParams = afin; break;
+            case GK_WGFIN: p.kernelParams = awf; break;
+            default: p.kernelParams = ard; p.gridDim = dim3(rd.grid); break;
+            }
+            HIP_TRY(hipGraphExecKernelNodeSetParams(h->graph_exec, g.node, &p));
         }
     }
     HIP_TRY(hipGraphLaunch(h->graph_exec, h->stream));
@@ -2190,18 +2266,13 @@ mppi_status mppi_update(mppi_handle *h, const double *state, double time)
     if (h && state && pm_fused_eligible(h)) return update_pm_fused(h, state, time);
     if (h) h->info[MPPI_INFO_FUSED_UPDATE] = 0;
     if (h && state && graph_eligible(h)) return update_graph(h, state, time);
+    if (h && sharded(h) && !h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
     mppi_status st = mppi_update_phase1(h, state, time);
     if (st != MPPI_OK) return st;
-    if (sharded(h)) {
-        if (!h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
-        // R costs and slot R, every rank's in-launch wait timeouts (the finish kernels fail the
-        // update on all ranks alike when any rank's launch lost rows)
-        NCCL_TRY(ncclAllReduce(h->d_costs_local, h->d_costs, (size_t)h->R + 1, ncclDouble, ncclSum, h->comm, h->stream));
-    }
+    if (sharded(h) && (st = allreduce_costs(h)) != MPPI_OK) return st;
     st = mppi_update_phase2(h);
     if (st != MPPI_OK) return st;
-    if (sharded(h))
-        NCCL_TRY(ncclAllReduce(h->d_gpart, h->d_gpart, (size_t)(h->H * h->C), ncclDouble, ncclSum, h->comm, h->stream));
+    if (sharded(h) && (st = allreduce_gradient(h)) != MPPI_OK) return st;
     return mppi_update_phase3(h);
 }
 

@@ -2034,6 +2034,13 @@ bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env)
     return extra > 0 && groups > 0 && groups <= (int64_t)g_cu_count && extra + 1 <= groups * ROWS_PER_WAVE;
 }
 
+bool fr_coop_is_update_kernel(const void *f)
+{
+    return f == (const void *)&fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, false> ||
+           f == (const void *)&fr_coop_x_kernel<CK_ASSISTED_MANIPULATION, true> ||
+           f == (const void *)&fr_coop_x_kernel<CK_TRACK_POINT, false>;
+}
+
 static void launch_x_any(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
     if (a.cost_kind == CK_TRACK_POINT) launch_x<CK_TRACK_POINT, false>(a, nb, s);

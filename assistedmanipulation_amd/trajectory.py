@@ -223,6 +223,14 @@ class Trajectory:
     def comm_init(self, world, rank, unique_id):
         self._check(self._L.mppi_comm_init(self._h, world, rank, unique_id))
 
+    def comm_info(self):
+        """The engine communicator as RCCL reports it: {"nranks", "rank"} (0 / -1 without one), and
+        the handle's HIP device and PCI bus id (mppi_comm_info)."""
+        n, r, d = C.c_int(), C.c_int(), C.c_int()
+        bus = C.create_string_buffer(64)
+        self._check(self._L.mppi_comm_info(self._h, C.byref(n), C.byref(r), C.byref(d), bus, 64))
+        return {"nranks": n.value, "rank": r.value, "device": d.value, "pci_bus_id": bus.value.decode()}
+
     def set_shard(self, world, rank):
         self._check(self._L.mppi_set_shard(self._h, world, rank))
 

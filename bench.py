@@ -217,16 +217,41 @@ def launch_ranks(n):
     return rc if rc >= 0 else 128 - rc
 
 
+def rccl_check(infos, world):
+    """Proof that the run was what it says: every rank's engine communicator reports `world` ranks
+    (ncclCommCount) and its own rank (ncclCommUserRank), and the ranks sit on `world` distinct GPUs
+    (PCI bus ids).  Returns the bench line's "rccl" entry; exits non-zero on any mismatch."""
+    bad = []
+    for i, x in enumerate(infos):
+        if world > 1 and (x["nranks"] != world or x["rank"] != i):
+            bad.append("rank %d: communicator reports %d ranks, rank %d" % (i, x["nranks"], x["rank"]))
+    buses = [x["pci_bus_id"] for x in infos]
+    if len(set(buses)) != len(buses):
+        bad.append("ranks share a device: %s" % buses)
+    if bad:
+        sys.stderr.write("bench.py: RCCL check failed: %s\n" % "; ".join(bad))
+        sys.exit(3)
+    return {"ranks": world, "communicator_ranks": [x["nranks"] for x in infos],
+            "devices": [{"rank": i, "hip_device": x["device"], "pci_bus_id": x["pci_bus_id"]} for i, x in enumerate(infos)]}
+
+
 def bootstrap_only(world, rank, local_rank, dist):
     """MPPI_BENCH_BOOTSTRAP_ONLY=1 (CPU tests): stop after the gloo rendezvous and the broadcast of
-    a stand-in for the RCCL unique id, before the engine loads; rank 0 prints what it saw."""
+    a stand-in for the RCCL unique id, before the engine loads; rank 0 prints what it saw.  The
+    RCCL check runs on stand-ins for each rank's mppi_comm_info (MPPI_BENCH_STUB_NRANKS /
+    MPPI_BENCH_STUB_SAME_DEVICE=1 make them wrong, to test the refusal)."""
     uid = [os.urandom(128) if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
+    stub_n = int(os.environ.get("MPPI_BENCH_STUB_NRANKS", world))
+    same = os.environ.get("MPPI_BENCH_STUB_SAME_DEVICE") == "1"
     seen = [None] * world
     dist.all_gather_object(seen, {"rank": rank, "local_rank": local_rank, "uid": uid[0].hex(), "pid": os.getpid(),
-                                  "engine_loaded": "assistedmanipulation_amd" in sys.modules})
+                                  "engine_loaded": "assistedmanipulation_amd" in sys.modules,
+                                  "comm": {"nranks": stub_n, "rank": rank, "device": local_rank,
+                                           "pci_bus_id": "0000:%02x:00.0" % (0 if same else local_rank)}})
     if rank == 0:
-        print(json.dumps({"bootstrap_only": True, "n_gpus": world, "ranks": seen}))
+        rccl = rccl_check([x["comm"] for x in seen], world)
+        print(json.dumps({"bootstrap_only": True, "n_gpus": world, "ranks": seen, "rccl": rccl}))
     dist.destroy_process_group()
 
 
@@ -278,6 +303,14 @@ def run(args, world, rank, local_rank, dist):
         uid = [am.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         traj.comm_init(world, rank, uid[0])
+        infos = [None] * world
+        dist.all_gather_object(infos, traj.comm_info())
+    else:
+        try:
+            infos = [traj.comm_info()]
+        except AttributeError:   # an older library under an A/B run (MPPI_AMD_LIB) lacks mppi_comm_info
+            infos = [{"nranks": 0, "rank": -1, "device": local_rank, "pci_bus_id": "unknown"}]
+    rccl = rccl_check(infos, world)   # (every rank checks: a bad run stops before the timed loop)
     traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
     if args.graph >= 0:
         traj.set_graph(args.graph)
@@ -397,11 +430,14 @@ def run(args, world, rank, local_rank, dist):
                                                "step_record_round_trip": 2 * BYTES_REC if info["objective_in_launch"] else BYTES_REC}
     # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
     # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
-    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
+    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set; with
+    # optimise() and finish() as one launch (weights_finish_kernel) that launch, whose finish adds a
+    # few KB to the ε tensor's bytes
+    wf = not pm and info.get("fused_update") == 2
     wg_ms = kt[6]
     if wg_ms > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
         wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
-        wg = {"kernel": "weights_gradient_kernel", "bound": "hbm",
+        wg = {"kernel": "weights_finish_kernel (optimise + finish)" if wf else "weights_gradient_kernel", "bound": "hbm",
               "ms": wg_ms, "bytes_per_launch": wg_bytes,
               "achieved_GBs": wg_bytes / (wg_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
         wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS
@@ -449,6 +485,7 @@ def run(args, world, rank, local_rank, dist):
                       "optimal_rollout": kt[3], "update": kt[4]}},
         "roofline": roofline,
         "hbm": hbm,
+        "rccl": rccl,
     }
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(args, pm)

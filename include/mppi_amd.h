@@ -254,6 +254,10 @@ mppi_status mppi_shard_range(int64_t rollout_count, int world, int rank, int64_t
  * the caller (e.g. torch.distributed) before mppi_comm_init on every rank. */
 mppi_status mppi_comm_unique_id(char out[128]);
 mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char unique_id[128]);
+/* The engine communicator as RCCL reports it (ncclCommCount / ncclCommUserRank; 0 and -1 without
+ * one), the handle's HIP device and its PCI bus id (hipDeviceGetPCIBusId, len bytes; may be null):
+ * bench.py checks that N ranks form one N-rank communicator on N distinct devices. */
+mppi_status mppi_comm_info(mppi_handle *h, int *nranks, int *rank, int *device, char *pci_bus_id, int len);
 /* Shard without an engine communicator: the caller runs the two all-reduces between the
  * update phases (mppi_update_phase1..3).  Must precede the first update. */
 mppi_status mppi_set_shard(mppi_handle *h, int world, int rank);
@@ -393,7 +397,8 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
                                              failed with MPPI_ERR_DEVICE and published nothing) */
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
 #define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass,
-                                             pm_update_kernel) */
+                                             pm_update_kernel); 2: optimise() and finish() ran as
+                                             one launch (weights_finish_kernel) */
 #define MPPI_UPDATE_INFO_N 10
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 

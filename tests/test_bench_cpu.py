@@ -37,6 +37,18 @@ def test_bench_spawns_its_ranks(n):
     assert len({x["pid"] for x in ranks}) == n
     assert len({x["uid"] for x in ranks}) == 1 and len(bytes.fromhex(ranks[0]["uid"])) == 128
     assert not any(x["engine_loaded"] for x in ranks)   # nothing touched HIP before the ranks existed
+    rccl = out["rccl"]   # the communicator check, on stand-ins for mppi_comm_info
+    assert rccl["ranks"] == n and rccl["communicator_ranks"] == [n] * n
+    assert [d["rank"] for d in rccl["devices"]] == list(range(n))
+    assert len({d["pci_bus_id"] for d in rccl["devices"]}) == n
+
+
+@pytest.mark.parametrize("stub", [{"MPPI_BENCH_STUB_NRANKS": "1"}, {"MPPI_BENCH_STUB_SAME_DEVICE": "1"}])
+def test_bench_refuses_a_run_that_is_not_n_ranks_on_n_devices(stub):
+    """A communicator whose rank count is not --gpus, or two ranks on one device: exit non-zero."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"], env=_env(MPPI_BENCH_BOOTSTRAP_ONLY="1", **stub),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode != 0 and "RCCL check failed" in r.stderr, (r.returncode, r.stderr[-2000:])
 
 
 def test_bench_refuses_gpus_that_disagree_with_world_size():

@@ -7,6 +7,11 @@ ncclCommInitRank, the rollout launch writing the local cost vector, ncclAllReduc
 the engine stream, the weights from a pass over the all-reduced costs (not the rollout launch's
 cost statistics), ncclAllReduce of the partial gradient, then the publish.  It must equal the unsharded handle: the noise and the costs bit for
 bit, U* to the gradient's summation order (mppi.cpp:344-448).
+
+The sharded update as a captured hipGraph (configs[4]: "8 x MI355X ... hipGraph-captured control
+step"): the rollout launch(es), ncclAllReduce of the costs, the weight reduce, ncclAllReduce of the
+partial gradient, the finish and the rank + next draws captured once, RCCL's nodes included, and
+replayed with each update's arguments: bit-identical to the eager sharded launches.
 """
 import numpy as np
 import pytest
@@ -23,6 +28,9 @@ def test_one_rank_rccl_equals_unsharded(rollouts, horison):
     mk = lambda: am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
     plain, rccl = mk(), mk()
     rccl.comm_init(1, 0, am.comm_unique_id())
+    info = rccl.comm_info()   # what RCCL reports (ncclCommCount / ncclCommUserRank), and the device
+    assert info["nranks"] == 1 and info["rank"] == 0 and info["pci_bus_id"], info
+    assert plain.comm_info()["nranks"] == 0 and plain.comm_info()["pci_bus_id"] == info["pci_bus_id"]
     for t in (plain, rccl):
         t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
         t.set_forecast(am.constant_forecast(t.H))
@@ -44,3 +52,42 @@ def test_one_rank_rccl_equals_unsharded(rollouts, horison):
         assert rccl.argmin() == plain.argmin()
         np.testing.assert_allclose(rccl.get_weights(), plain.get_weights(), rtol=0, atol=1e-12)
         np.testing.assert_allclose(rccl.get_optimal_rollout(), plain.get_optimal_rollout(), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (8192, 1.28, 10), (8200, 0.32, 0)])
+def test_sharded_graph_equals_eager(rollouts, horison, window):
+    """Through a one-rank communicator: the graph path (mppi_set_graph) against the eager sharded
+    launches, over updates with varying shifts (5, 2, 5, 0 steps), a state change and an
+    interruption (reading the optimal cost runs filter() by itself; the next update is eager).
+    8192 x 128 with the Savitzky-Golay filter is configs[4]'s share per GPU (the two-launch split,
+    sg_finish_kernel); 8200 rollouts rank past RANK_TILED_MAX (the chunk + merge rank launches stay
+    in the graph with their captured arguments)."""
+    sg = am.Smoothing(window, 1) if window else None
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
+                                            smoothing=sg)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17, 0.22, 0.27, 0.32]
+    out = {}
+    for graph in (0, 1):
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.comm_init(1, 0, am.comm_unique_id())
+        t.set_graph(graph)
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for j, tm in enumerate(times):
+            if j == 5:
+                x = x.copy()
+                x[12 + 4] = 0.3
+            t.update(x, tm)
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+            if j == 6:
+                rec.append(t.get_optimal_total_cost())
+        out[graph] = (rec, t.graph_updates())
+    assert out[0][1] == 0 and out[1][1] >= 5, out[1][1]
+    for j, (a, b) in enumerate(zip(out[0][0], out[1][0])):
+        if isinstance(a, float):
+            assert a == b
+            continue
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))

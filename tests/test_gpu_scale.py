@@ -176,7 +176,7 @@ def test_config4_savitzky_golay_h128(S, updates):
 
 
 @pytest.mark.parametrize("rollouts,horison,window", [(4096, 0.64, 0), (1000, 0.64, 0), (4096, 1.28, 10), (8192, 1.28, 10),
-                                                     (4094, 0.64, 0)])
+                                                     (4094, 0.64, 0), (8200, 0.32, 0)])
 def test_graph_path_equals_eager_launches(rollouts, horison, window):
     """The hipGraph path of update() (mppi_set_graph: the steady-state update captured once and
     replayed with each update's arguments written into its kernel nodes) gives the eager launches'
@@ -186,7 +186,8 @@ def test_graph_path_equals_eager_launches(rollouts, horison, window):
     the graph's finish node; 8192 x 128 with it is configs[4]'s share per GPU, whose rollouts are
     the two-launch split (five kernel nodes).  4094 rollouts (R = 4096, a multiple of 16 rows)
     leave filter() pending in a four-wave launch, a shape the graph does not replay: every update
-    runs eagerly (such a handle once failed every other update)."""
+    runs eagerly (such a handle once failed every other update).  8200 rollouts rank
+    past RANK_TILED_MAX: the chunk + merge rank launches replay with their captured arguments."""
     sg = am.Smoothing(window, 1) if window else None
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
                                             smoothing=sg)
