@@ -43,7 +43,6 @@ EnvSwitches env_switches_read()
     e.handover_off = is("MPPI_HANDOVER", '0');
     e.split_off = is("MPPI_SPLIT", '0');
     e.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
-    e.fused_finish_off = is("MPPI_FUSED_FINISH", '0');
     return e;
 }
 }  // namespace mppi_eng
@@ -62,11 +61,6 @@ struct DeviceBuf {
 struct mppi_handle {
     int device = 0;
     EnvSwitches env{};   // the A/B switches as the environment held them at create (env_switches_read)
-    // optimise() and finish() as one launch this update (weights_finish_kernel): its normaliser
-    // partials [GRAD_SPLIT][H] and its step / last-step tickets [H + 1] (left at zero by the kernel)
-    bool wf_fused = false;
-    double *d_tpart = nullptr;
-    unsigned *d_fin_tick = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t stream_opt = nullptr;   // filter(): optimal rollout, overlapped with the next update
 
@@ -971,8 +965,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_gpart, HC));
     CREATE_TRY(dalloc(h, &h->d_grad, HC));
     CREATE_TRY(dalloc(h, &h->d_gsplit, HC * GRAD_SPLIT));
-    CREATE_TRY(dalloc(h, &h->d_tpart, (size_t)h->H * GRAD_SPLIT));
-    CREATE_TRY(dalloc(h, &h->d_fin_tick, (size_t)h->H + 1));
     CREATE_TRY(dalloc(h, &h->d_wexp, (size_t)h->R));
     CREATE_TRY(dalloc(h, &h->d_cstats, 1));
     // the first update's statistics start empty (later ones are reset by the finish kernel)
@@ -1812,17 +1804,9 @@ mppi_status mppi_update_phase2(mppi_handle *h)
     w.wpart = h->d_wpart;
     w.stats = cost_stats_used(h) ? h->d_cstats : nullptr;
     h->gargs.wg = w;
-    // optimise() and finish() as one launch where it applies (unsharded, no smoothing, the
-    // objective's statistics): phase 3 then launches no finish.  Sharded, the partial gradient is
-    // summed here and all-reduced before phase 3.  (MPPI_FUSED_FINISH=0: the two launches, A/B)
-    h->wf_fused = !h->env.fused_finish_off && weights_finish_eligible(w, finish_args(h));
-    if (h->wf_fused) h->gargs.fin = finish_args(h);   // its publish sequence: phase 3's
-    h->info[MPPI_INFO_FUSED_UPDATE] = h->wf_fused ? 2 : 0;
     if (h->graph_dry) return MPPI_OK;
-    // a filter() launched by itself on the side stream reads the d_U / d_x0_opt the finish rewrites
-    if (h->wf_fused && h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
-    if (h->wf_fused) HIP_TRY(launch_weights_finish(w, h->gargs.fin, h->d_tpart, h->d_fin_tick, h->stream));
-    else HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
+    // sharded: the partial gradient is summed here and all-reduced before phase 3
+    HIP_TRY(launch_weights_gradient(w, h->d_gpart, sharded(h), h->stream));
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_wg, h->stream));
     return MPPI_OK;
 }
@@ -1834,7 +1818,7 @@ static mppi_status phase3_launch(mppi_handle *h, double *seq_out)
     // the previous update's optimal rollout reads d_U / d_x0_opt: wait for it before rewriting
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
     h->gargs.fin = finish_args(h);
-    if (!h->graph_dry && !h->wf_fused) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
+    if (!h->graph_dry) HIP_TRY(launch_finish(h->gargs.fin, h->stream));
     const double seq = (double)(++h->publish_seq);
     *seq_out = seq;
     if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev[3], h->stream));
@@ -1999,7 +1983,7 @@ static mppi_status graph_nodes(mppi_handle *h)
     for (size_t i = 0; i < n; i++) HIP_TRY(hipGraphNodeGetDependencies(nodes[i], nullptr, &indeg[i]));
     std::vector<bool> done(n, false);
     h->gnodes.clear();
-    int count[6] = {0, 0, 0, 0, 0, 0};
+    int count[5] = {0, 0, 0, 0, 0};
     for (size_t visited = 0; visited < n;) {   // Kahn's order over the dependency counts
         size_t i = 0;
         while (i < n && (done[i] || indeg[i] != 0)) i++;
@@ -2025,14 +2009,10 @@ static mppi_status graph_nodes(mppi_handle *h)
     }
     // the launches the arguments are kept for: the rollout launch(es), one weights kernel (and the
     // large-R softmin pair ahead of it), one finish, one rank + draws
-    const bool wf = h->wf_fused;   // optimise() and finish() as one node (weights_finish_kernel)
-    if (count[GK_ROLLOUT] != h->gargs.nroll || count[GK_RANKDRAW] != 1 ||
-        (wf ? (count[GK_WGFIN] != 1 || count[GK_WGRAD] != 0 || count[GK_FINISH] != 0)
-            : (count[GK_WGFIN] != 0 || count[GK_WGRAD] < 1 || count[GK_FINISH] != 1)))
+    if (count[GK_ROLLOUT] != h->gargs.nroll || count[GK_WGRAD] < 1 || count[GK_FINISH] != 1 || count[GK_RANKDRAW] != 1)
         return fail(h, MPPI_ERR_DEVICE, "captured update graph has " + std::to_string(count[GK_ROLLOUT]) + " rollout, " +
                                             std::to_string(count[GK_WGRAD]) + " weights, " + std::to_string(count[GK_FINISH]) +
-                                            " finish, " + std::to_string(count[GK_WGFIN]) + " weights + finish and " +
-                                            std::to_string(count[GK_RANKDRAW]) + " rank nodes");
+                                            " finish and " + std::to_string(count[GK_RANKDRAW]) + " rank nodes");
     return MPPI_OK;
 }
 
@@ -2089,7 +2069,6 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
         void *aroll[2][1] = {{&h->gargs.roll}, {&h->gargs.roll2}};
         void *awg[] = {&h->gargs.wg};
         void *afin[] = {&h->gargs.fin};
-        void *awf[] = {&h->gargs.wg, &h->gargs.fin, &h->d_tpart, &h->d_fin_tick};
         void *ard[] = {&rd.cost, &rd.S, &rd.rank, &rd.nr, &rd.a, &rd.nx, &rd.sub_nxb, &rd.sub_xbase, &rd.sub_row0};
         for (const mppi_handle::GraphNode &g : h->gnodes) {
             hipKernelNodeParams p = g.params;
@@ -2098,7 +2077,6 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
             case GK_ROLLOUT: p.kernelParams = aroll[g.index]; break;
             case GK_WGRAD: p.kernelParams = awg; break;
             case GK_FINISH: p.kernelParams = afin; break;
-            case GK_WGFIN: p.kernelParams = awf; break;
             default: p.kernelParams = ard; p.gridDim = dim3(rd.grid); break;
             }
             HIP_TRY(hipGraphExecKernelNodeSetParams(h->graph_exec, g.node, &p));

@@ -476,107 +476,12 @@ __global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
     if (t == 0) a.wpart[3 * SM_NB + blockIdx.x] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
-// optimise() and finish() in one launch (weights_finish_kernel: unsharded, no Savitzky-Golay filter,
-// the objective's cost statistics).  Block (k, s) is weights_gradient_kernel's block; it stores its
-// partials - step k's gradient part and its slice's normaliser, which every block forms as block
-// (0, s) does (the same rollouts, the same order, the same bits) - write-through (another XCD's block
-// may read them), and takes step k's ticket.  The last of the GRAD_SPLIT to arrive finishes step k
-// as finish_flat_kernel finishes every element: the partials added in split order, divided by the
-// normaliser, the gradient step, the clamp, U* and the host block.  The last step to finish (a second
-// ticket) writes the status words, the rank reset, the statistics reset and the flag.  Tickets are
-// agent-scope adds after the stores they publish are acknowledged (no waits, so no block can hang);
-// each ticket is left at zero for the next update by the block that drew the last number.  Every
-// result is bit-identical to weights_gradient_kernel + finish_flat_kernel.
-template <int C>
-__device__ __forceinline__ void fin_step(const WGradArgs &a, const FinishArgs &f, double *tpart, unsigned *tick, int k, int s,
-                                         bool all_nan, bool early, double minimum, double maximum, int &sfin)
-{
-    const int t = threadIdx.x;
-    const int H = a.H, HC = H * C;
-    __builtin_amdgcn_s_waitcnt(0);   // this thread's partials (write-through) have left it
-    __syncthreads();
-    if (t == 0) {
-        const unsigned n = __hip_atomic_fetch_add(tick + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sfin = n + 1 == (unsigned)gridDim.y;
-        if (sfin) __hip_atomic_store(tick + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every split has arrived
-    }
-    __syncthreads();
-    if (!sfin) return;
-    (void)s;
-    const int wt = f.wait_all ? (int)*f.wait_all : a.status->wait_timeouts;   // update_wait_timeouts
-    const bool upd = !early && !all_nan && !wt, ok = !all_nan && !wt;
-    double total = 0.0;
-    if (t < C) {   // step k's C elements: every load first (one trip), then the arithmetic
-        const int e = k * C + t;
-        double p[GRAD_SPLIT], tp[GRAD_SPLIT];
-#pragma unroll
-        for (int i = 0; i < GRAD_SPLIT; i++) {
-            p[i] = upd ? __hip_atomic_load(a.gsplit + ((int64_t)i * H + k) * C + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-            tp[i] = upd ? __hip_atomic_load(tpart + (int64_t)i * H + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-        }
-        double u = f.Ushift[e];
-        const double uo = f.U[e];
-        const double hi = f.control_bound ? f.cmax[t] : 0.0, lo = f.control_bound ? f.cmin[t] : 0.0;
-        total = tp[0];   // softmin_total: the slice partials in split order
-#pragma unroll
-        for (int i = 1; i < GRAD_SPLIT; i++) total += tp[i];
-        double g = p[0];
-#pragma unroll
-        for (int i = 1; i < GRAD_SPLIT; i++) g += p[i];
-        g /= total;   // sum_r e_r eps_r / sum_r e_r
-        if (upd) {
-            f.gradient[e] = g;
-            u += g * f.gradient_step;
-            if (f.control_bound) {
-                u = smin(u, hi);
-                u = smax(u, lo);
-            }
-            f.Ushift[e] = u;
-        }
-        const double v = ok ? u : uo;
-        if (ok) f.U[e] = v;
-        __hip_atomic_store(f.out + e, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // pub
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // this step's host-block stores are acknowledged
-    __syncthreads();
-    if (t == 0) {
-        const unsigned n = __hip_atomic_fetch_add(tick + H, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sfin = n + 1 == (unsigned)H;
-        if (sfin) __hip_atomic_store(tick + H, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!sfin) return;
-    // the last step: every block has read the statistics and every step's U* is in the host block
-    const double oc = *f.opt_cost;
-    if (t < f.X) f.x0_opt[t] = f.x0[t];
-    for (int64_t i = t; i < f.rank_n; i += blockDim.x) f.rank_zero[i] = 0;   // for rank_draw_kernel's tiles
-    if (t == 0) {
-        f.status_w->sg_error = wt != 0;   // read by the filter() row as "the update threw"
-        __hip_atomic_store(f.out + HC + 0, oc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 1, (double)all_nan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 2, (double)(early || all_nan), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 3, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 4, minimum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 5, maximum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.out + HC + 7, (double)wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (t == 0 && upd) f.status_w->total = total;   // the normaliser, for mppi_weights
-    if (f.stats_reset) mppi_sample::reset_cost_stats(f.stats_reset, t);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (t == 0) {
-        f.status_w->wait_timeouts = 0;   // read above by every finisher: reset for the next launch
-        __hip_atomic_store(f.out + HC + 6, f.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-template <int C, bool LARGE, bool FIN>
-__device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArgs &f, double *tpart, unsigned *tick)
+template <int C, bool LARGE>
+__global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
     constexpr int CP = C;
     __shared__ double red[4 * CP];
     __shared__ double smn[WV], smx[WV], ssum[WV];
-    __shared__ int sfin;
     const int t = threadIdx.x, rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
     const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
@@ -623,9 +528,6 @@ __device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArg
     // unsharded, the normaliser slice of block (0, s) is its own rollout range [r0, r1): its e_r come
     // from the gradient loop below, in the same per-thread order as the separate slice pass
     const bool own_slice = !LARGE && k == 0 && a.begin == 0 && a.count == R;
-    // FIN: every block sums its slice's e_r the way block (0, s) does (the same rollouts, the same
-    // order: the same bits), so step k's finisher has the normaliser from its own splits' partials
-    const bool slice_sum = own_slice || FIN;
     double minimum, maximum, valid, total;
     if constexpr (LARGE) {
         if (rw == 0) {
@@ -703,13 +605,11 @@ __device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArg
     Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
         if (lead) { st->all_nan = 1; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
-        if constexpr (FIN) fin_step<C>(a, f, tpart, tick, k, s, true, false, minimum, maximum, sfin);
         return;
     }
     const double difference = maximum - minimum;
     if (difference < 1e-6) {   // early return, weights/gradient stale (mppi.cpp:373-375)
         if (lead) { st->all_nan = 0; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
-        if constexpr (FIN) fin_step<C>(a, f, tpart, tick, k, s, false, true, minimum, maximum, sfin);
         return;
     }
     auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
@@ -743,8 +643,8 @@ __device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArg
         if constexpr (LARGE) wr[m] = cpre[m];
         else wr[m] = expw(cpre[m]);
         wr[m] = r < r1 ? wr[m] : 0.0;
-        if (slice_sum && r < r1) {
-            if (own_slice) a.wexp[r] = wr[m];
+        if (own_slice && r < r1) {
+            a.wexp[r] = wr[m];
             part += wr[m];
         }
     }
@@ -758,15 +658,15 @@ __device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArg
     }
     for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
         const double wr = wexp(a.begin + r);
-        if (slice_sum) {
-            if (own_slice) a.wexp[r] = wr;
+        if (own_slice) {
+            a.wexp[r] = wr;
             part += wr;
         }
         const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
 #pragma unroll
         for (int c = 0; c < CP; c++) acc[c] += wr * n[c];
     }
-    if (slice_sum) {   // as the slice pass: butterflies, then the four wave sums in order
+    if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
         part = wave_sum(part);
         if (l == 0) ssum[rw] = part;
     }
@@ -777,28 +677,9 @@ __device__ __forceinline__ void weights_body(const WGradArgs &a, const FinishArg
 #pragma unroll
         for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
     __syncthreads();
-    const double gs = t < CP ? (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]) : 0.0;
-    const double sl = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
-    if (own_slice && t == 0) st->tsplit[s] = sl;
-    if constexpr (FIN) {   // the partials write-through (another XCD's block may finish the step)
-        if (t < CP) __hip_atomic_store(a.gsplit + ((int64_t)s * a.H + k) * C + t, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == 0) __hip_atomic_store(tpart + (int64_t)s * a.H + k, sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fin_step<C>(a, f, tpart, tick, k, s, false, false, minimum, maximum, sfin);
-    } else if (t < CP) {
-        a.gsplit[((int64_t)s * a.H + k) * C + t] = gs;
-    }
-}
-
-template <int C, bool LARGE>
-__global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
-{
-    weights_body<C, LARGE, false>(a, FinishArgs{}, nullptr, nullptr);
-}
-
-template <int C>
-__global__ __launch_bounds__(256) void weights_finish_kernel(WGradArgs a, FinishArgs f, double *tpart, unsigned *tick)
-{
-    weights_body<C, false, true>(a, f, tpart, tick);
+    if (t < CP)
+        a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
+    if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
 __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
@@ -1325,21 +1206,7 @@ int graph_kernel_kind(const void *f)
     if (is((const void *)&finish_flat_kernel) || is((const void *)&sg_finish_kernel) || is((const void *)&finish_kernel))
         return GK_FINISH;
     if (is((const void *)&rank_draw_kernel<FR_C>)) return GK_RANKDRAW;
-    if (is((const void *)&weights_finish_kernel<FR_C>)) return GK_WGFIN;
     return GK_OTHER;
-}
-
-bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f)
-{
-    return a.C == FR_C && f.C == FR_C && a.stats != nullptr && a.R <= SM_LARGE_R && a.begin == 0 && a.count == a.R &&
-           f.sg_window == 0 && f.wait_all == nullptr && f.ns == GRAD_SPLIT && f.H == a.H && f.X <= 256;
-}
-
-hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, double *tpart, unsigned *tick, hipStream_t s)
-{
-    if (!weights_finish_eligible(a, f) || !tpart || !tick) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((weights_finish_kernel<FR_C>), dim3((unsigned)a.H, GRAD_SPLIT), dim3(256), 0, s, a, f, tpart, tick);
-    return hipGetLastError();
 }
 
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s)

@@ -321,8 +321,7 @@ bool fr_coop_costs_in_launch(const EnvSwitches &env);   // the objective runs in
 // before creating a handle): a handle's launch paths never change under it, and no getenv runs on
 // the update path (~80 ns each)
 struct EnvSwitches {
-    bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off,
-        fused_finish_off;
+    bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off;
 };
 EnvSwitches env_switches_read();
 // Whether a pending filter() folds into the update launch of `count` rows with the objective in
@@ -331,17 +330,11 @@ bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env);
 constexpr int FR_BODY_TABLE = 13 * 46;   // doubles of the cooperative kernels' body table (>= LDS_MODEL)
 hipError_t launch_fr_body_table(const DevModel *model, const DevCost *cost, double *table, hipStream_t s);
 hipError_t launch_finish(const FinishArgs &a, hipStream_t s);
-// optimise() and finish() as one launch (weights_finish_kernel, kernels.hip): weights_gradient_kernel's
-// grid, and the last block of each step finishes that step (unsharded, no Savitzky-Golay filter,
-// the objective's cost statistics, R <= SM_LARGE_R); bit-identical to the two launches.  tpart:
-// [GRAD_SPLIT][H] scratch; tick: [H + 1] counters at zero (left at zero).
-bool weights_finish_eligible(const WGradArgs &a, const FinishArgs &f);
-hipError_t launch_weights_finish(const WGradArgs &a, const FinishArgs &f, double *tpart, unsigned *tick, hipStream_t s);
 // The kernel nodes of a captured update graph (engine.cpp update_graph) by their kernel function:
 // the ones whose arguments change per update (the rollout launches, the weight reduce, the finish,
 // the rank + next draws) and the rest (RCCL's, the gradient sum, the O(S log S) rank), which replay
 // with their captured arguments
-enum GraphKernel : int { GK_OTHER = 0, GK_ROLLOUT = 1, GK_WGRAD = 2, GK_FINISH = 3, GK_RANKDRAW = 4, GK_WGFIN = 5 };
+enum GraphKernel : int { GK_OTHER = 0, GK_ROLLOUT = 1, GK_WGRAD = 2, GK_FINISH = 3, GK_RANKDRAW = 4 };
 int graph_kernel_kind(const void *func);          // kernels.hip's kernels
 bool fr_coop_is_update_kernel(const void *func);  // fr_coop.hip: an fr_coop_x_kernel instantiation
 

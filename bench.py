@@ -430,14 +430,11 @@ def run(args, world, rank, local_rank, dist):
                                                "step_record_round_trip": 2 * BYTES_REC if info["objective_in_launch"] else BYTES_REC}
     # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
     # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
-    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set; with
-    # optimise() and finish() as one launch (weights_finish_kernel) that launch, whose finish adds a
-    # few KB to the ε tensor's bytes
-    wf = not pm and info.get("fused_update") == 2
+    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
     wg_ms = kt[6]
     if wg_ms > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
         wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
-        wg = {"kernel": "weights_finish_kernel (optimise + finish)" if wf else "weights_gradient_kernel", "bound": "hbm",
+        wg = {"kernel": "weights_gradient_kernel", "bound": "hbm",
               "ms": wg_ms, "bytes_per_launch": wg_bytes,
               "achieved_GBs": wg_bytes / (wg_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
         wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS

@@ -397,8 +397,7 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
                                              failed with MPPI_ERR_DEVICE and published nothing) */
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
 #define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass,
-                                             pm_update_kernel); 2: optimise() and finish() ran as
-                                             one launch (weights_finish_kernel) */
+                                             pm_update_kernel) */
 #define MPPI_UPDATE_INFO_N 10
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 

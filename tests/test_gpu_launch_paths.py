@@ -11,8 +11,6 @@
 - Rows just past two waves per SIMD (R = S + 2 at S = 8192, configs[4]'s share per GPU) run as
   two fr_coop_x_kernel launches (fr_coop_update_split) instead of one-wave workgroups whose last
   wave runs alone (MPPI_SPLIT=0): bit-identical noise, costs, U*, weights and filter() cost.
-- optimise() and finish() as one launch (weights_finish_kernel, the default where it applies)
-  against weights_gradient_kernel + finish_flat_kernel (MPPI_FUSED_FINISH=0).
 """
 import numpy as np
 import pytest
@@ -99,42 +97,3 @@ def test_split_launch_equals_one_wave_launch(rollouts, horison, window, monkeypa
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
 
-
-@pytest.mark.parametrize("rollouts,horison", [(4096, 0.64), (1000, 0.64), (4097, 0.32), (20000, 0.32)])
-def test_fused_finish_equals_two_launches(rollouts, horison, monkeypatch):
-    """optimise() and finish() as one launch (weights_finish_kernel, the default where it applies):
-    weights_gradient_kernel's blocks, each of which also forms its slice's normaliser, and the last
-    block of each step finishing that step - against weights_gradient_kernel + finish_flat_kernel
-    (MPPI_FUSED_FINISH=0).  The sums are formed in the same order, so costs, U*, weights and the
-    gradient are bit-identical, including an update that throws (every cost NaN) and the updates
-    after it; past SM_LARGE_R (20000 rollouts) the two launches run in both."""
-    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8)
-    times = [0.0, 0.05, 0.07, 0.12, None, 0.17, 0.22]   # None: a NaN state (every cost NaN: the update throws)
-    out = {}
-    for ff in ("0", "1"):
-        monkeypatch.setenv("MPPI_FUSED_FINISH", ff)
-        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
-        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
-        t.set_forecast(am.constant_forecast(t.H))
-        x = am.huddled_state()
-        rec = []
-        for j, tm in enumerate(times):
-            if tm is None:
-                bad = x.copy()
-                bad[0] = np.nan
-                with pytest.raises(am.EngineError, match="ALL_NAN"):
-                    t.update(bad, 0.15)
-                rec.append((t.get_optimal_rollout().copy(),))
-                continue
-            t.update(x, tm)
-            info = t.update_info()
-            assert info["wait_timeouts"] == 0, info
-            fused = ff == "1" and rollouts + 2 <= 16384
-            assert info["fused_update"] == (2 if fused else 0), info
-            rec.append((t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy(),
-                        t.get_gradient().copy()))
-            x = x + 0.001
-        out[ff] = rec + [(np.float64(t.get_optimal_total_cost()),)]
-    for j, (a, b) in enumerate(zip(out["0"], out["1"])):
-        for i, (u, v) in enumerate(zip(a, b)):
-            np.testing.assert_array_equal(u, v, err_msg="update %d item %d" % (j, i))
