@@ -166,7 +166,7 @@ struct mppi_handle {
     // per update (a fill launch and its gap)
     double *d_costs_local = nullptr;   // the update's cost min / max / count (cost kernel atomics)
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
-    // cooperative kernel's step records [H][Rpad][FR_NREC] and the filter() row's [H][FR_NREC]
+    // cooperative kernel's step records [Rpad][H][FR_REC] and the filter() row's [H][FR_REC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
@@ -546,7 +546,7 @@ mppi_status alloc_shard_buffers(mppi_handle *h)
     HIP_TRY(dalloc(h, &h->d_noise_prev, (size_t)(h->H * h->C * h->Rpad)));
     if (h->dyn_kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {
         dfree(h, h->d_rec);
-        HIP_TRY(dalloc(h, &h->d_rec, (size_t)(h->H * h->Rpad * FR_NREC)));
+        HIP_TRY(dalloc(h, &h->d_rec, (size_t)(h->H * h->Rpad * FR_REC)));
     }
     return MPPI_OK;
 }
@@ -972,7 +972,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_wpart, 4 * 64));
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
-    CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_NREC)));
+    CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_REC)));
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));

@@ -751,10 +751,10 @@ __device__ __forceinline__ void inertia_mul(double m, const double *c, const dou
 }
 
 // What the cost of the next step needs from a calculate() (row-uniform): EE and arm-mount
-// positions, the EE frame velocity J v and J_a J_a^T.  Written to the step record.
+// positions, written to the step record.  (The EE frame velocity J v and J_a J_a^T are formed by
+// the objective from the record's motion subspaces: store_kin.)
 struct CoopKin {
     double ee[3], am[3];
-    double ks;   // lane m = min(j, 8): kinematic sum m, J v (m < 3) or J_a J_a^T (packed, m - 3)
     double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
 };
 
@@ -770,10 +770,7 @@ struct LaneConst {
     bool is_rz;
     double rz, nrz;   // is_rz as 1.0 / 0.0 and its complement: the joint rotation's (cos, sin) by one FMA
                       // and one multiply instead of four v_cndmask_b32
-    int ka, kb;     // kinematic sum min(j, 8): S component x, y slot (S component or qd)
-    bool vsum;      // the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
     // opaque lane masks (0 / -1) for msel, built once before the horizon loop
-    int m_vsum;     // vsum
     int m_j0, m_j1, m_j2, m_j12, m_j13, m_j14, m_j15;   // j == n
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
@@ -839,11 +836,12 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
             bd.S[k] = S[k];
         }
     }
-#pragma unroll
-    for (int k = 0; k < 6; k++) Lk[L_S + L.slot * S_STR + k] = S[k];
-    Lk[L_S + L.slot * S_STR + 6] = qd;
     kin.pw = 0.0;
     if constexpr (EN) {
+        // coop_aba's motion subspaces (the mass-matrix solve takes them from registers)
+#pragma unroll
+        for (int k = 0; k < 6; k++) Lk[L_S + L.slot * S_STR + k] = S[k];
+        Lk[L_S + L.slot * S_STR + 6] = qd;
         // The energy tank's power needs tau = tau_u + nonLinearEffects(q, v) (pinocchio_dynamics.cpp:
         // 156, 248-251).  With W_j = sum_{i <= j} S_i v_new,i, NLE . v_new = sum_j f_j . W_j where
         // f_j = I_j A_j + V_j x* I_j V_j is body j's RNEA force (world frame, at the origin):
@@ -894,20 +892,20 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
         kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
     }
-    kin.ks = 0.0;
+}
+
+// The record's motion subspaces for the objective's J v and J_a J_a^T (kernels.hpp REC_S01 /
+// REC_S2Q, fr_cost_terms.hpp kin_sums): the lane's S linear part and the qd its calculate() used,
+// two 16-byte stores per lane (lanes 12..15 and the fingers into slots nobody reads).  Until r05 the
+// row formed the nine sums itself after the FK - S and qd through LDS, ten LDS-read FMAs and the
+// base's selects per lane, ~45 instructions on the dynamics chain of every step; the objective's
+// waves now run the same FMA chains beside the loops, in the issue slots one wave leaves idle.
+template <int CK>
+__device__ __forceinline__ void store_kin(double *rp, int j, const CoopBody &bd, double qd)
+{
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
-    // The frame velocity J v over the EE chain (bodies 0..9) and J_a J_a^T over the arm (bodies
-    // 3..9): nine sums, lane m computes sum m from the S / qd slots the row just wrote to LDS
-    // (ten LDS-read FMAs per lane instead of 72 DPP-broadcast FMAs that every lane repeats).
-    const double *xs = Lk + L_S + L.ka, *ys = Lk + L_S + L.kb;
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i <= FR_EE_PARENT; i++) {
-        double y = ys[i * S_STR];
-        if (i < FR_ARM0) y = msel(L.m_vsum, 0.0, y);
-        acc = __builtin_fma(xs[i * S_STR], y, acc);
-    }
-    kin.ks = acc;
+    *reinterpret_cast<double2 *>(rp + REC_S01 + 2 * j) = double2{bd.S[0], bd.S[1]};
+    *reinterpret_cast<double2 *>(rp + REC_S2Q + 2 * j) = double2{bd.S[2], qd};
 }
 
 // Articulated-body passes over the world inertias / S staged in LDS (energy-tank rollouts, whose
@@ -1251,10 +1249,10 @@ __device__ __forceinline__ void stage_body_table(const FrRolloutArgs &a, double 
     for (int t = threadIdx.x; t < LDS_MODEL; t += nt) Lmodel[t] = a.table[t];
 }
 
-// Step record store (layout: kernels.hpp FR_NREC), the whole row active (no branch splits the
+// Step record store (layout: kernels.hpp FR_REC), the whole row active (no branch splits the
 // step's basic block): lanes 0..11 write (q_j, qd_j) and lanes 12..15 the EE / arm-mount
 // positions and the tank energy (one 16-byte store), then lane j writes kinematic sum min(j, 8)
-// (lanes 9..15 repeat lane 8: same address, same value).
+// (the motion subspaces for the objective's sums: store_kin, after the FK).
 template <bool EN>
 __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst &L, double q, double qd, const CoopKin &kin,
                                              double E)
@@ -1271,7 +1269,6 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
         e[1] = double2{kin.ee[2], kin.am[0]};
         e[2] = double2{kin.am[1], kin.am[2]};
         e[3] = double2{0.0, 0.0};
-        rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
         return;
     }
     double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
@@ -1282,9 +1279,8 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
     a0 = msel(L.m_j15, a0, E);
     a1 = msel(L.m_j15, a1, 0.0);
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
-    rp[REC_VL + (j < 9 ? j : 8)] = kin.ks;
 }
-static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_VL == 32 && REC_JJ == 35 && FR_NREC == 42, "record layout");
+static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_S01 == 32 && REC_S2Q == 64 && FR_REC == 96, "record layout");
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / frec).  The
@@ -1331,8 +1327,8 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     const double *x0p = FROW && frow ? a.fx0 : Lx0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
     const int ush = FROW && frow ? 0 : a.ush;
-    double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_NREC;   // [rollout][step][FR_NREC]
-    auto recp = [&](int k) -> double * { return rp + (int64_t)k * FR_NREC; };
+    double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_REC;   // [rollout][step][FR_REC]
+    auto recp = [&](int k) -> double * { return rp + (int64_t)k * FR_REC; };
     const bool jl = j < FR_NB;   // lane owns a body / control component
     const int jb = jl ? j : 0;
     const double *M = Lmodel + (jl ? j : FR_NB) * MB;
@@ -1345,13 +1341,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         L.nrz = nrz;
     }
     L.slot = jl ? j : FR_NB;
-    {
-        const int m = j < 9 ? j : 8;   // kinematic sum of the lane: a, b component nibbles
-        L.ka = (int)((0x211000210ull >> (4 * m)) & 0xF);
-        L.kb = (int)((0x221210666ull >> (4 * m)) & 0xF);
-        L.vsum = m < 3;
-    }
-    L.m_vsum = opaque_mask(L.vsum);
     L.m_j0 = opaque_mask(j == 0);
     L.m_j1 = opaque_mask(j == 1);
     L.m_j2 = opaque_mask(j == 2);
@@ -1404,8 +1393,10 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
-    if (kb == 0)
+    if (kb == 0) {
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
+        store_kin<CK>(recp(0), j, bd, qd);
+    }
 
     // eps and U*_shifted of step k: loaded at the top of the step
     const bool sampled = !opt_row && jl;
@@ -1441,6 +1432,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         if constexpr (EN)
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
+        store_kin<CK>(recp(k + 1), j, bd, qd);   // the next record's kinematics (the one-step lag)
         double pe = 0.0;
         double qdd;
         if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe);
@@ -1484,7 +1476,7 @@ __device__ __forceinline__ void launch_row_cost(const FrRolloutArgs &a, int64_t 
     if (!(lr < a.count || frow)) return;
     if (frow && (a.status->all_nan || a.status->sg_error)) return;   // no filter() when the update threw
     const double J = mppi_cost::rollout_cost<CK, EN, MB>(*a.cost, frow ? a.fsteps : a.steps,
-                                                          frow ? a.frec : a.rec + lr * a.H * FR_NREC, a.H, lane,
+                                                          frow ? a.frec : a.rec + lr * a.H * FR_REC, a.H, lane,
                                                           Lmodel + T_LO);
     if (lane == 0) {
         if (frow) *a.fcost = J;
@@ -1623,10 +1615,10 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     const bool rl = row_live(a, lr), live = rl && k < H;
     const bool frow = a.fcost != nullptr && lr == a.count;
     const int64_t lrv = rl ? lr : lr0;   // any live row's records when unused
-    const double *rec = frow ? a.frec : a.rec + lrv * H * FR_NREC;
+    const double *rec = frow ? a.frec : a.rec + lrv * H * FR_REC;
     const StepConst *stp = frow ? a.fsteps : a.steps;
     const int kk = live ? k : 0;
-    const double cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_NREC, Lmodel + T_LO);
+    const double cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO);
     if (live) Lcs[(g * ROWS_PER_WAVE + i) * HC_MAX + k] = cs;
     // the stores before the count: the wave that completes the group reads every chunk's costs
     const int n = __builtin_amdgcn_readfirstlane(
@@ -2057,7 +2049,7 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
     b.begin += r0;
     b.count = n;
     b.noise += r0 * FR_C;   // [H][Rpad][C]: row lr of step k at (k Rpad + lr) C
-    b.rec += r0 * a.H * FR_NREC;
+    b.rec += r0 * a.H * FR_REC;
     b.samp.begin += r0;
     b.samp.count = n;
     b.samp.noise += r0 * FR_C;

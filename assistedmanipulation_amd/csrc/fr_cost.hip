@@ -1,7 +1,7 @@
 // fr_cost.hip — the rollout costs of the cooperative FrankaRidgeback kernel, from its step records.
 //
 // fr_coop_kernel writes, for every (rollout, step k), the state x_k and the kinematics of the
-// calculate() before it (kernels.hpp FR_NREC layout, rollout-major).  This kernel evaluates the
+// calculate() before it (kernels.hpp FR_REC layout, rollout-major).  This kernel evaluates the
 // objective on all of them at once: one wave per rollout, one lane per step, so every lane does distinct work
 // (inside the rollout kernel the workspace, trajectory and manipulability terms are row-uniform
 // and all 16 lanes of a row would repeat them).  The step costs are then summed in step order,
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             Lj[i] = *src;
         }
     __syncthreads();
-    const double J = rollout_cost<CK, EN>(Cs, stp, frow ? a.frec : a.rec + row * H * FR_NREC, H, lane, Lj);
+    const double J = rollout_cost<CK, EN>(Cs, stp, frow ? a.frec : a.rec + row * H * FR_REC, H, lane, Lj);
     if (lane != 0) return;
     if (frow) *a.fcost = J;
     else if (a.optimal) *a.cost_out = J;
@@ -75,9 +75,9 @@ __global__ __launch_bounds__(64) void fr_terms_kernel(const DevCost *cost, const
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
-        double t[7];
-        const double *rk = rec + (int64_t)k * FR_NREC;
-        assisted_manipulation_terms(*cost, steps[k], rk, rk[REC_QQD + 4], t);
+        double t[7], r[FR_NREC];
+        derive_record(rec + (int64_t)k * FR_REC, r);
+        assisted_manipulation_terms(*cost, steps[k], r, r[REC_QQD + 4], t);
 #pragma unroll
         for (int m = 0; m < 7; m++)
             for (int i = 0; i < n; i++) tot[m] += readlane_f64(t[m], i);

@@ -1,5 +1,5 @@
 // fr_cost_terms.hpp — the FrankaRidgeback objectives evaluated on one step record (kernels.hpp
-// FR_NREC layout).  Shared by fr_step_cost_kernel (fr_cost.hip) and the rollout kernel's consumer
+// FR_REC stored layout, FR_NREC derived layout).  Shared by fr_step_cost_kernel (fr_cost.hip) and the rollout kernel's consumer
 // waves (fr_coop.hip).
 //
 // AssistedManipulation::get_cost (assisted_manipulation.cpp:58-128) and TrackPoint::get_cost
@@ -79,6 +79,54 @@ __device__ __forceinline__ double manipulability_term(const DevCost &Cs, const d
     return (Cs.manip_c + Cs.manip_l * fabs(iv)) + Cs.manip_q * iv * iv;
 }
 
+// J v and J_a J_a^T of a stored record (kernels.hpp REC_S01 / REC_S2Q) by the chains the rollout
+// kernel's lanes ran before r05, term for term: lane m of a row summed over the bodies i = 0..9, in
+// order, acc = fma(x_i, y_i, acc) from acc = 0, with x_i = S_i[m] and y_i = qd_i for J v (m < 3),
+// and x_i = S_i[a], y_i = S_i[b] (y_i = 0 for the base, i < 3) for the packed J_a J_a^T entry (a, b)
+// - so the sums, and every cost, keep their bits.
+__device__ __forceinline__ void kin_sums(const double2 *rec2, double *vl, double *jj)
+{
+    double s0[10], s1[10], s2[10], qd[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const double2 a = rec2[REC_S01 / 2 + i], b = rec2[REC_S2Q / 2 + i];
+        s0[i] = a.x;
+        s1[i] = a.y;
+        s2[i] = b.x;
+        qd[i] = b.y;
+    }
+    const double *S[3] = {s0, s1, s2};
+    constexpr int ja[6] = {0, 0, 0, 1, 1, 2}, jb[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int m = 0; m < 3; m++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) acc = __builtin_fma(S[m][i], qd[i], acc);
+        vl[m] = acc;
+    }
+#pragma unroll
+    for (int p = 0; p < 6; p++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) acc = __builtin_fma(S[ja[p]][i], i < 3 ? 0.0 : S[jb[p]][i], acc);
+        jj[p] = acc;
+    }
+}
+
+// The derived record (FR_NREC) of a stored one (FR_REC)
+__device__ __forceinline__ void derive_record(const double *rk, double *r)
+{
+    const double2 *src = reinterpret_cast<const double2 *>(rk);
+#pragma unroll
+    for (int i = 0; i < REC_VL / 2; i++) {
+        const double2 v = src[i];
+        r[2 * i] = v.x;
+        r[2 * i + 1] = v.y;
+    }
+    kin_sums(src, r + REC_VL, r + REC_JJ);
+    r[FR_NREC - 1] = 0.0;
+}
+
 // AssistedManipulation::get_cost at the record's state with its kinematics
 template <bool EN, int JS>
 __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
@@ -103,17 +151,19 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
     // the rest of the record (r holds the (q, qd) pairs only) is loaded through a pointer that
     // waits for the joint sums: the remaining terms start after them instead of interleaving with
     // them and holding their values live (two waves per SIMD instead of four)
-    static_assert(REC_EE == 2 * FR_NB && FR_NREC - REC_EE == 18, "record tail");
-    double rest[FR_NREC - REC_EE], yaw = r[REC_QQD + 4];
-    const double2 *tp = src + REC_EE / 2;
+    static_assert(REC_EE == 2 * FR_NB && REC_VL - REC_EE == 8, "record tail");
+    double rest[REC_VL - REC_EE], yaw = r[REC_QQD + 4];
+    const double2 *tp = src;
     asm volatile("" : "+v"(tp), "+v"(yaw) : "v"(joint), "v"(vel));
 #pragma unroll
-    for (int i = 0; i < (FR_NREC - REC_EE) / 2; i++) {
-        const double2 v = tp[i];
+    for (int i = 0; i < (REC_VL - REC_EE) / 2; i++) {
+        const double2 v = tp[REC_EE / 2 + i];
         rest[2 * i] = v.x;
         rest[2 * i + 1] = v.y;
     }
-    r = rest - REC_EE;   // r[REC_EE ..] from here on
+    double vl[3], jj[6];   // from the stored record's motion subspaces (kin_sums)
+    kin_sums(tp, vl, jj);
+    r = rest - REC_EE;   // r[REC_EE .. REC_VL) from here on
     double s, c;
     fsincos(yaw, &s, &c, sincos_constants());   // base yaw q_2
     const double *ee = r + REC_EE, *am = r + REC_AM;
@@ -146,8 +196,8 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
         cost += left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);
     }
     cost += Cs.en_vel ? vel : 0.0;
-    cost += Cs.en_traj ? trajectory_term(Cs, sc, r + REC_VL) : 0.0;
-    cost += Cs.en_manip ? manipulability_term(Cs, r + REC_JJ) : 0.0;
+    cost += Cs.en_traj ? trajectory_term(Cs, sc, vl) : 0.0;
+    cost += Cs.en_manip ? manipulability_term(Cs, jj) : 0.0;
     return cost;
 }
 
@@ -242,7 +292,7 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
 }
 
 // gamma_k times the objective at step record r (AssistedManipulation: r holds the record's (q, qd)
-// pairs, the rest is read from src; TrackPoint: r holds the whole record)
+// pairs, the rest is read from the stored record src; TrackPoint: r holds the record up to REC_VL)
 template <int CK, bool EN, int JS = JT_STRIDE>
 __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
                                            const double2 *src)
@@ -251,14 +301,13 @@ __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &
     else return sc.gamma_k * assisted_manipulation_cost<EN, JS>(Cs, sc, r, Lj, src);
 }
 
-// gamma_k times the objective at the step record rk (FR_NREC doubles, 16-byte aligned)
+// gamma_k times the objective at the stored step record rk (FR_REC doubles, 16-byte aligned)
 template <int CK, bool EN, int JS = JT_STRIDE>
 __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const StepConst &sc, const double *rk, const double *Lj)
 {
-    constexpr int NREC2 = FR_NREC / 2;
     double r[FR_NREC];
     const double2 *src = reinterpret_cast<const double2 *>(rk);
-    constexpr int NLOAD = CK == CK_TRACK_POINT ? NREC2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
+    constexpr int NLOAD = CK == CK_TRACK_POINT ? REC_VL / 2 : FR_NB;   // AssistedManipulation: the (q, qd) pairs
 #pragma unroll
     for (int i = 0; i < NLOAD; i++) {
         const double2 v = src[i];
@@ -268,7 +317,7 @@ __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const Step
     return step_cost<CK, EN, JS>(Cs, sc, r, Lj, src);
 }
 
-// J of one rollout from its H step records (rollout-major, FR_NREC doubles each) by one wave:
+// J of one rollout from its H stored step records (rollout-major, FR_REC doubles each) by one wave:
 // lane k evaluates step k (64 steps a pass) and the wave sums the step costs in step order, as the
 // reference accumulates J += cost (mppi.cpp:322-337); a NaN step makes the sum NaN (the reference's
 // early stop), canonicalised to the quiet NaN it stores.  The same value on every lane.
@@ -276,12 +325,11 @@ template <int CK, bool EN, int JS = JT_STRIDE>
 __device__ __forceinline__ double rollout_cost(const DevCost &Cs, const StepConst *stp, const double *rec, int H, int lane,
                                                const double *Lj)
 {
-    constexpr int NREC2 = FR_NREC / 2;
     double J = 0.0;
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
-        const double c = record_step_cost<CK, EN, JS>(Cs, stp[k], rec + (int64_t)k * (2 * NREC2), Lj);
+        const double c = record_step_cost<CK, EN, JS>(Cs, stp[k], rec + (int64_t)k * FR_REC, Lj);
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
     }
     return isnan(J) ? (double)NAN : J;

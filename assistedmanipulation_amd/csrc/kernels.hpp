@@ -137,8 +137,8 @@ struct FrRolloutArgs {
     const StepConst *fsteps;
     double *fcost;
     int64_t xbase, xrows;     // fr_coop_x_kernel: the fifth waves' rows [xbase, xbase + xrows)
-    // cooperative kernel: per-step records for the cost kernel, [count][H][FR_NREC] (rollout-major:
-    // one rollout's records are contiguous), and the folded / standalone filter() row's [H][FR_NREC]
+    // cooperative kernel: per-step records for the cost kernel, [count][H][FR_REC] (rollout-major:
+    // one rollout's records are contiguous), and the folded / standalone filter() row's [H][FR_REC]
     double *rec, *frec;
     // U*_shifted row k is Ushift row min(k + ush, H - 1): ush = 0 with U*_shifted itself, the
     // update's shift with U* (draws made ahead)
@@ -168,22 +168,32 @@ struct FrRolloutArgs {
     int debug;
 };
 
-// Per (step k, rollout) record the cooperative rollout kernel writes for fr_step_cost_kernel:
-// the state x_k the cost is evaluated at and the kinematics of the calculate() before it.
+// What the objective reads at (step k, rollout): the state x_k the cost is evaluated at and the
+// kinematics of the calculate() before it - the "derived record", FR_NREC doubles.
 constexpr int FR_NREC = 42;   // 41 used, padded to 16 bytes
 constexpr int REC_QQD = 0;    // [2j], [2j + 1]: q_j, qd_j (j < 12)
 constexpr int REC_EE = 24;    // EE position (world)
 constexpr int REC_AM = 27;    // arm-mount position (world)
 constexpr int REC_E = 30;     // energy tank level (enable_energy_limit)
 constexpr int REC_VL = 32;    // EE linear frame velocity J v (bodies 0..9)
-constexpr int REC_JJ = 35;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11 12 22     // energy tank level (enable_energy_limit)
+constexpr int REC_JJ = 35;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11 12 22
+// What the cooperative rollout kernel stores per (rollout, step) - the "stored record", FR_REC
+// doubles: the derived record's first 32 doubles as they are, then two planes of one 16-byte slot
+// per lane of the row instead of J v and J_a J_a^T: (S_j linear x, y) and (S_j linear z, qd_j) of
+// the calculate() the kinematics come from (lanes 12..15 and the fingers' slots unused).  The
+// objective forms J v = sum_j S_j qd_j and J_a J_a^T from them (fr_cost_terms.hpp kin_sums) with
+// the FMA chains the rollout kernel's lanes used to run on every step (r05: 50 instructions off the
+// dynamics chain, the objective's waves doing them in the slots it leaves idle).
+constexpr int REC_S01 = 32;   // [32 + 2j], [33 + 2j]: S_j linear x, y (j < 10 read)
+constexpr int REC_S2Q = 64;   // [64 + 2j], [65 + 2j]: S_j linear z, the calculate()'s qd_j (j < 10 read)
+constexpr int FR_REC = 96;    // 768 B: sixteen records are 96 whole 128-byte lines
 
 // The rollout costs from the records (fr_cost.hip): one wave per rollout, one lane per step, the
 // step costs summed in step order (the reference's J += cost, mppi.cpp:322-337).
 struct FrCostArgs {
     const DevCost *cost;
     const StepConst *steps;   // [H]
-    const double *rec;        // [count][H][FR_NREC]
+    const double *rec;        // [count][H][FR_REC]
     int64_t begin, count;
     double *cost_out;         // [R] (global index begin + row) or the optimal-cost scalar
     const Status *status;
@@ -421,7 +431,7 @@ constexpr int PM_STAMPS = 12;
 bool pm_fused_fits(int64_t R, int H);
 size_t pm_fused_lds_bytes(int64_t R, int H);
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);
-// AssistedManipulation's seven per-term totals of one rollout from its [H][FR_NREC] records
+// AssistedManipulation's seven per-term totals of one rollout from its [H][FR_REC] records
 hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s);
 
 

@@ -53,9 +53,9 @@ FLOPS_DYN_PER_ROLLOUT_STEP = FLOPS_PER_ROLLOUT_STEP - FLOPS_COST_PER_ROLLOUT_STE
 BYTES_SURVEY_FR = 2 * 12 * 8.0    # 192 B (FrankaRidgeback, C = 12)
 BYTES_SURVEY_PM = 2 * 3 * 8.0     # 48 B (point mass, C = 3)
 # What the device's rollout launch moves beyond that: it reads the eps column (96 B),
-# and the cooperative kernel writes a 336-B step record that the objective reads back.
+# and the cooperative kernel writes a 768-B step record that the objective reads back.
 BYTES_EPS_FR = 96.0
-BYTES_REC = 336.0
+BYTES_REC = 768.0   # the stored step record (kernels.hpp FR_REC; 336 B until r05)
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
 PMC_JSON = os.path.join(HERE, "profiles", "r04", "pmc_rollout.json")
 PMC_WG_JSON = os.path.join(HERE, "profiles", "r04", "pmc_weights.json")   # weights_gradient_kernel's traffic
