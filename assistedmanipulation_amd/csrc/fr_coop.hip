@@ -257,7 +257,9 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
     m[1] = F[1];
 #pragma unroll
     for (int i = 2; i < 11; i++) m[i] = 0.0;
-    asm("s_nop 1\n\t"
+    // no leading s_nop: S (the DPP sources) was formed long before (tools/dpp_hazard_check.py
+    // checks every build's assembly)
+    asm(""
         "v_fmac_f64_dpp %0, %9, %15 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %9, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
@@ -315,294 +317,211 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
         : "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
         : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
 }
-// pivot 0: eleven FMAs with pivot 0's quotient, and pivot 1's quotient computed between them
-__device__ __forceinline__ double gj_pivot_0(double *Mc, double nt, double inv_next)
+// The twelve pivots of the Gauss-Jordan elimination, software-pipelined (pivot k's block
+// updates row k + 1 first and interleaves pivot k + 1's reciprocal chain between its other
+// FMAs), in one asm statement: nt is pivot 0's quotient, inv_next 1 / M[1][1]
+__device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
 {
-    double nn;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %11, -%0, %13\n\t"
-        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn)
+    double qa, qb, d, r, t, e;
+    // s_nop 1: nt (a source of pivot 0's DPP FMAs) may be written right before the block
+    asm("s_nop 1\n\t"
+        /* pivot 0 */
+        "v_fmac_f64_dpp %1, %1, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %12, -%1, %19\n\t"
+        "v_fmac_f64_dpp %4, %4, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 1 */
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%2, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %13, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 2 */
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %3 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%3, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %12, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 3 */
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %4 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%4, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %13, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %12 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 4 */
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %5 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%5, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %12, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 5 */
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %6 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%6, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %13, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 6 */
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %7 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%7, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %12, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 7 */
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %8 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%8, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %13, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 8 */
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%9, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %12, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 9 */
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%10, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %13, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 10 */
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %14, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %2, %2, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mul_f64 %16, -%11, %15\n\t"
+        "v_fma_f64 %17, -%14, %15, 1.0\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %12, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 11 */
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(qa), "=&v"(qb), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
         : "v"(nt), "v"(inv_next));
-    return nn;
-}
-// pivot 1: eleven FMAs with pivot 1's quotient, and pivot 2's quotient computed between them
-__device__ __forceinline__ double gj_pivot_1(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[0]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 2: eleven FMAs with pivot 2's quotient, and pivot 3's quotient computed between them
-__device__ __forceinline__ double gj_pivot_2(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 3: eleven FMAs with pivot 3's quotient, and pivot 4's quotient computed between them
-__device__ __forceinline__ double gj_pivot_3(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 4: eleven FMAs with pivot 4's quotient, and pivot 5's quotient computed between them
-__device__ __forceinline__ double gj_pivot_4(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 5: eleven FMAs with pivot 5's quotient, and pivot 6's quotient computed between them
-__device__ __forceinline__ double gj_pivot_5(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 6: eleven FMAs with pivot 6's quotient, and pivot 7's quotient computed between them
-__device__ __forceinline__ double gj_pivot_6(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 7: eleven FMAs with pivot 7's quotient, and pivot 8's quotient computed between them
-__device__ __forceinline__ double gj_pivot_7(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[11]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 8: eleven FMAs with pivot 8's quotient, and pivot 9's quotient computed between them
-__device__ __forceinline__ double gj_pivot_8(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 9: eleven FMAs with pivot 9's quotient, and pivot 10's quotient computed between them
-__device__ __forceinline__ double gj_pivot_9(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[10]), "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 10: eleven FMAs with pivot 10's quotient, and pivot 11's quotient computed between them
-__device__ __forceinline__ double gj_pivot_10(double *Mc, double nt)
-{
-    double nn, d, r, t, e;
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b64_dpp %12, %0 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %13, %12\n\t"
-        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_mul_f64 %14, -%0, %13\n\t"
-        "v_fma_f64 %15, -%12, %13, 1.0\n\t"
-        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fma_f64 %11, %14, %15, %14\n\t"
-        "v_fmac_f64_dpp %9, %9, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[11]), "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "=&v"(nn), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
-        : "v"(nt));
-    return nn;
-}
-// pivot 11: eleven FMAs with pivot 11's quotient
-__device__ __forceinline__ void gj_pivot_11(double *Mc, double nt)
-{
-    asm(""
-        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %9, %9, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %10, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10])
-        : "v"(nt));
 }
 // ---- END generated by tools/gen_gj.py ----
 
@@ -1023,7 +942,8 @@ __device__ __forceinline__ void composite_dpp(const double *x, const double *des
 {
 #pragma unroll
     for (int c = 0; c < 9; c++) v[c] = 0.0;
-    asm("s_nop 1\n\t"
+    asm(""   // (no leading s_nop: the checker, above)
+        
         "v_fmac_f64_dpp %0, %9, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %10, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %11, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
@@ -1168,16 +1088,12 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     double *Row = Lk + L_COL + j * CSTR;
 #pragma unroll
     for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Row + i) = double2{Mc[i], Mc[i + 1]};
-    *reinterpret_cast<double2 *>(Row + 12) = double2{tau_l, 0.0};
-    *reinterpret_cast<double2 *>(Row + 14) = double2{0.0, 0.0};
+    Row[12] = tau_l;   // (slots 13..15: zeros for good, coop_rows' entry)
     Row[j] = diag;
 #pragma unroll
     for (int i = 0; i < 12; i++) Mc[i] += Lk[L_COL + i * CSTR + j];
     double nt = -Mc[0] * L.inv_m0;   // each pivot's block returns the next pivot's quotient
-    nt = gj_pivot_0(Mc, nt, L.inv_m1);
-    nt = gj_pivot_1(Mc, nt); nt = gj_pivot_2(Mc, nt); nt = gj_pivot_3(Mc, nt); nt = gj_pivot_4(Mc, nt);
-    nt = gj_pivot_5(Mc, nt); nt = gj_pivot_6(Mc, nt); nt = gj_pivot_7(Mc, nt); nt = gj_pivot_8(Mc, nt);
-    nt = gj_pivot_9(Mc, nt); nt = gj_pivot_10(Mc, nt); gj_pivot_11(Mc, nt);
+    gj_solve(Mc, nt, L.inv_m1);
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
     // tau' at L_TP and every other lane its column in its own block row (read above, dead now), so
     // lane j reads M'_jj back at slot j of that row: no per-lane register select, no branch.
@@ -1263,13 +1179,15 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
         // the record.  The EE / arm-mount / E slots are row-uniform values that every lane of the row
         // stores alike (the same bytes to the same addresses): four stores instead of sixteen
         // v_bfi_b32.
-        *reinterpret_cast<double2 *>(rp + L.rec_off) = double2{q, qd};
+        // two 8-byte stores (relaxed wavefront-scope atomics: plain stores the vectorizer leaves
+        // apart) - a 16-byte one needs (q, qd) in adjacent registers, two v_mov_b32 per step
+        __hip_atomic_store(rp + L.rec_off, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_store(rp + L.rec_off + 1, qd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         double2 *e = reinterpret_cast<double2 *>(rp + REC_EE);
         e[0] = double2{kin.ee[0], kin.ee[1]};
         e[1] = double2{kin.ee[2], kin.am[0]};
         e[2] = double2{kin.am[1], kin.am[2]};
-        e[3] = double2{0.0, 0.0};
-        return;
+        return;   // (slots 30, 31 - E, pad: the dummy lanes' zero pair)
     }
     double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
     a0 = msel(L.m_j13, a0, kin.ee[2]);
@@ -1393,6 +1311,11 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
     CoopKin kin;
     CoopBody bd;
+    // coop_solve's block rows: slots 13..15 hold zeros for good (slot 12 is tau, rewritten per step)
+    if constexpr (!EN) {
+        Lk[L_COL + j * CSTR + 13] = 0.0;
+        *reinterpret_cast<double2 *>(Lk + L_COL + j * CSTR + 14) = double2{0.0, 0.0};
+    }
     if (kb == 0) {
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
         store_kin<CK>(recp(0), j, bd, qd);

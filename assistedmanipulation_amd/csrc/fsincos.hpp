@@ -19,7 +19,11 @@ __device__ __forceinline__ SinCosK sincos_constants()
               {4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
                -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11}};
 #pragma unroll
-    for (int i = 0; i < 6; i++) asm volatile("" : "+s"(k.s[i]), "+s"(k.c[i]));
+    for (int i = 0; i < 6; i++)
+        if (i != 4) asm volatile("" : "+s"(k.s[i]), "+s"(k.c[i]));
+    // the innermost Horner FMAs fma(z, s5, s4) would read two scalar operands (one allowed): s4 and
+    // c4 live in VGPRs, instead of a v_mov_b64 of each per use (two per rollout step, r05)
+    asm volatile("" : "+v"(k.s[4]), "+v"(k.c[4]));
     return k;
 }
 

@@ -19,7 +19,7 @@ def regs(tok):
     return {int(m.group(1))} if m else set()
 
 
-def check(path, prefix=""):
+def check(path, prefix="", strict=True):
     bad = 0
     inside = False
     recent = []   # (wait states since the write, registers)
@@ -43,9 +43,15 @@ def check(path, prefix=""):
         if "_dpp" in op or " row_" in s or "quad_perm" in s:
             ops = s[len(op):].split(",")
             src0 = regs(ops[1]) if len(ops) > 1 else set()
+            # the other sources too, as LLVM's hazard recognizer counts them (conservative: the
+            # documented hazard is the operand read through the DPP network, src0)
+            srcs = set().union(*[regs(o.split()[0]) for o in ops[1:] if o.strip()]) if len(ops) > 1 else set()
             for dist, w in recent:
                 if dist < 2 and (w & src0):
                     print("hazard (%d wait states): %s" % (dist, s))
+                    bad += 1
+                elif dist < 2 and (w & srcs) and strict:
+                    print("hazard on a non-DPP source (%d wait states): %s" % (dist, s))
                     bad += 1
         recent = [(d + ws, w) for d, w in recent if d + ws < 2]
         if op.startswith("v_") and op != "v_nop":
