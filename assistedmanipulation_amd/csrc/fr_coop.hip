@@ -695,7 +695,7 @@ struct LaneConst {
     int m_live;     // j < 12: the lane owns a body
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
-    double desc[10];   // composite_dpp: 1.0 when body i + 2 is in the subtree of body j (lanes 0, 1: all)
+    double cmask[9];   // composite_scan: 1.0 when body j is the parent of step s's child (edges 11-9, 10-9, 9-8, .., 3-2)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
 };
@@ -926,119 +926,102 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 }
 
 
-// Composite inertia (h, Ib) of the lane's subtree as broadcast FMAs: v_c = sum over the source
-// lanes i = 2..11 of x_c[lane i] desc_i, desc_i = 1.0 when body i is in the lane's subtree (i >= j
-// on the chain 2..9, itself on the fingers 10 and 11).  Bodies 0 and 1 (the base's prismatic
-// joints) are in no subtree but their own and need no composite: their columns of M are the
-// constant composite mass on the diagonal (S_0, S_1 unit translations), whatever h and Ib hold.
-// Ninety v_fmac_f64_dpp in nine interleaved chains replace the four-level suffix scan (72 DPP
-// moves, 36 adds) and finger 10's select (18).  (r04)
-// The second asm block has no leading s_nop: the scheduler may place it right behind the first, and
-// a VALU write the compiler puts between them to one of its sources would be a VALU-write ->
-// DPP-read hazard the compiler does not see.  tools/dpp_hazard_check.py scans every build's
-// assembly for exactly that (fewer than two wait states between a VALU write and a DPP read of the
-// same VGPR) and fails the build, so the nop is only spent where a build would need it.
-__device__ __forceinline__ void composite_dpp(const double *x, const double *desc, double *v)
+// Composite inertia (h, Ib) of the lane's subtree, summed in place from the leaves up: each edge
+// (child i -> parent p) of the tree is one step v_c += v_c[lane i] m, m = 1.0 on lane p only, in an
+// order that finishes every child before it is read (fingers 11 and 10 into body 9, then 9 into 8,
+// ..., 3 into 2).  Nine steps of nine v_fmac_f64_dpp, the components interleaved, so each read of a
+// lane's value comes nine instructions after its write (two wait states are the DPP rule; the
+// dependency waits out the rest).  Bodies 0 and 1 (the base's prismatic joints) need no composite:
+// their columns of M are the constant composite mass on the diagonal (S_0, S_1 unit translations),
+// whatever h and Ib hold.  (r04: the whole subtree of each lane by broadcasts from lanes 2..11, ninety
+// FMAs plus nine zeroed accumulators; r05: 81 FMAs into the lanes' own values, nothing to zero.)
+__device__ __forceinline__ void composite_scan(double *v, const double *m)
 {
-#pragma unroll
-    for (int c = 0; c < 9; c++) v[c] = 0.0;
-    asm(""   // (no leading s_nop: the checker, above)
-        
-        "v_fmac_f64_dpp %0, %9, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %21 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %22 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        : "+&v"(v[0]), "+&v"(v[1]), "+&v"(v[2]), "+&v"(v[3]), "+&v"(v[4]), "+&v"(v[5]), "+&v"(v[6]), "+&v"(v[7]), "+&v"(v[8])
-        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]), "v"(desc[0]), "v"(desc[1]), "v"(desc[2]), "v"(desc[3]), "v"(desc[4]));
-    asm(""
-        "v_fmac_f64_dpp %0, %9, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %21 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %9, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %11, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %12, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %13, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %15, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %16, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %17, %22 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
-        : "+&v"(v[0]), "+&v"(v[1]), "+&v"(v[2]), "+&v"(v[3]), "+&v"(v[4]), "+&v"(v[5]), "+&v"(v[6]), "+&v"(v[7]), "+&v"(v[8])
-        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]), "v"(desc[5]), "v"(desc[6]), "v"(desc[7]), "v"(desc[8]), "v"(desc[9]));
+    // s_nop 1: the lanes' own (h, Ib) may be written right before the block (DPP sources)
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %0, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, %0, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %1, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %2, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8])
+        : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(m[5]), "v"(m[6]), "v"(m[7]), "v"(m[8]));
 }
 
 // Mass-matrix solve for the rollouts without the energy tank: qdd = M(q)^-1 tau_u, M by the
@@ -1057,10 +1040,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 {
     // (h, Ib) summed over the subtree; the subtree's mass is a per-lane constant of the body table (T_MC)
     double v[9] = {bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
-    {
-        const double x[9] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
-        composite_dpp(x, L.desc, v);
-    }
+    composite_scan(v, L.cmask);
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
     const double m = L.mc, h0 = v[0], h1 = v[1], h2 = v[2];
@@ -1281,12 +1261,12 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
             L.ancd[i] = d;
         }
+        constexpr int parent[9] = {9, 9, 8, 7, 6, 5, 4, 3, 2};   // of composite_scan's children 11, 10, 9, .., 3
 #pragma unroll
-        for (int i = 2; i < FR_NB; i++) {
-            const bool in = j < 2 || (j < FR_NB - 2 && i >= j) || i == j;   // fingers: themselves
-            double d = in ? 1.0 : 0.0;
-            asm volatile("" : "+v"(d));
-            L.desc[i - 2] = d;
+        for (int e = 0; e < 9; e++) {
+            double d = j == parent[e] ? 1.0 : 0.0;
+            asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
+            L.cmask[e] = d;
         }
     }
     L.mc = M[T_MC];
