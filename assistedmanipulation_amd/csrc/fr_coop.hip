@@ -525,42 +525,53 @@ __device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
 }
 // ---- END generated by tools/gen_gj.py ----
 
-// The third column of a rotation in delta form (D = R - I, row-major) from its first two, r2 = r0 x r1:
-// d2 = e0 x d1 + d0 x e1 + d0 x d1 (the zero delta gives zero).
-__device__ __forceinline__ void delta_col2(double *D)
+// A rotation's third column from its first two, r2 = r0 x r1 (R row-major).
+__device__ __forceinline__ void rot_col2(double *R)
 {
-    D[2] = __builtin_fma(D[3], D[7], __builtin_fma(-D[6], D[4], -D[6]));
-    D[5] = __builtin_fma(D[6], D[1], __builtin_fma(-D[0], D[7], -D[7]));
-    D[8] = __builtin_fma(D[0], D[4], __builtin_fma(-D[3], D[1], D[4] + D[0]));
+    R[2] = R[3] * R[7] - R[6] * R[4];
+    R[5] = R[6] * R[1] - R[0] * R[7];
+    R[8] = R[0] * R[4] - R[3] * R[1];
 }
 
-// One level of the delta-form prefix scan: (I + Da)(I + D) = I + Da + D + Da D,
-// pa + (I + Da) p = pa + p + Da p - with the rotations' first two columns only: 9 doubles shifted
-// (18 moves) instead of 12, the partner's third column rebuilt by delta_col2 (7 ops), and only
-// columns 0 and 1 formed (1150 -> 1105 loop instructions).
+// One level of the prefix scan in delta form (D = R - I, p): the partner's pose (Da, pa) arrives by
+// row_shr S - its rotation's first two columns and translation, 9 doubles (18 moves) - and
+//   (I + Da)(I + D) = I + Da + Ra D,   pa + Ra p,   Ra = I + Da,
+// with Ra's third column the cross product of its first two.  Each entry is one FMA chain that
+// starts from the partner's term (3 operations), and only columns 0 and 1 are formed; the lane's own
+// third column is never read before the end of the scan.  Lanes the shift leaves without a partner
+// receive zeros: Ra = I, pa = 0, the identity.  (r04: Da + D + Da D with the partner's third column
+// rebuilt in delta form, 61 operations a level; r05: 53.)
 template <int S>
 __device__ __forceinline__ void scan_level2(double *D, double *p)
 {
-    double Da[9], pa[3];
+    double Ra[9], Da[6], pa[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-        Da[3 * r] = shr<S>(D[3 * r]);
-        Da[3 * r + 1] = shr<S>(D[3 * r + 1]);
+        Da[2 * r] = shr<S>(D[3 * r]);
+        Da[2 * r + 1] = shr<S>(D[3 * r + 1]);
         pa[r] = shr<S>(p[r]);
     }
-    delta_col2(Da);
-    double Dn[9], pn[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        Ra[3 * r] = Da[2 * r];
+        Ra[3 * r + 1] = Da[2 * r + 1];
+    }
+    Ra[0] += 1.0;
+    Ra[4] += 1.0;
+    rot_col2(Ra);
+    double Dn[6], pn[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
 #pragma unroll
         for (int c = 0; c < 2; c++)
-            Dn[3 * r + c] = Da[3 * r] * D[c] + (Da[3 * r + 1] * D[3 + c] + (Da[3 * r + 2] * D[6 + c] + (Da[3 * r + c] + D[3 * r + c])));
-        pn[r] = Da[3 * r] * p[0] + (Da[3 * r + 1] * p[1] + (Da[3 * r + 2] * p[2] + (pa[r] + p[r])));
+            Dn[2 * r + c] = __builtin_fma(Ra[3 * r], D[c], __builtin_fma(Ra[3 * r + 1], D[3 + c],
+                                          __builtin_fma(Ra[3 * r + 2], D[6 + c], Da[2 * r + c])));
+        pn[r] = __builtin_fma(Ra[3 * r], p[0], __builtin_fma(Ra[3 * r + 1], p[1], __builtin_fma(Ra[3 * r + 2], p[2], pa[r])));
     }
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-        D[3 * r] = Dn[3 * r];
-        D[3 * r + 1] = Dn[3 * r + 1];
+        D[3 * r] = Dn[2 * r];
+        D[3 * r + 1] = Dn[2 * r + 1];
         p[r] = pn[r];
     }
 }
@@ -568,22 +579,23 @@ __device__ __forceinline__ void scan_level2(double *D, double *p)
 // The scan's last level (row_shr 8) for this robot: what lanes 8..11 compose with is the world pose of
 // bodies 0..3 (the planar base and panda_joint1), which is a rotation about z and a translation
 // (check_topology rejects any model where it is not).  So only (cos - 1, sin) of that rotation and
-// its translation travel - 5 doubles (10 moves) instead of 9 - and the product takes 19 operations
-// instead of 43: (I + Dw) (I + D) = I + D + Dw + Dw D with Dw = [[dc, -s, 0], [s, dc, 0], [0, 0, 0]].
+// its translation travel - 5 doubles (10 moves) instead of 9 - and the product is
+// Dw + (I + Dw) D with Dw = [[dc, -s, 0], [s, dc, 0], [0, 0, 0]]: 14 operations.
 // Lanes 0..7 receive zeros, the identity.  (The partner's R11, -R01 are taken as its R00, R10: equal
 // for a z rotation up to the last bit of the scan's rounding.)
 __device__ __forceinline__ void scan_level_planar8(double *D, double *p)
 {
     const double dc = shr<8>(D[0]), sn = shr<8>(D[3]);
     const double pw0 = shr<8>(p[0]), pw1 = shr<8>(p[1]), pw2 = shr<8>(p[2]);
+    const double cw = dc + 1.0;
     const double d00 = D[0], d01 = D[1], d10 = D[3], d11 = D[4];
-    D[0] = __builtin_fma(dc, d00, __builtin_fma(-sn, d10, d00 + dc));
-    D[1] = __builtin_fma(dc, d01, __builtin_fma(-sn, d11, d01 - sn));
-    D[3] = __builtin_fma(sn, d00, __builtin_fma(dc, d10, d10 + sn));
-    D[4] = __builtin_fma(sn, d01, __builtin_fma(dc, d11, d11 + dc));
+    D[0] = __builtin_fma(cw, d00, __builtin_fma(-sn, d10, dc));
+    D[1] = __builtin_fma(cw, d01, __builtin_fma(-sn, d11, -sn));
+    D[3] = __builtin_fma(sn, d00, __builtin_fma(cw, d10, sn));
+    D[4] = __builtin_fma(sn, d01, __builtin_fma(cw, d11, dc));
     const double p0 = p[0], p1 = p[1];
-    p[0] = __builtin_fma(dc, p0, __builtin_fma(-sn, p1, p0 + pw0));
-    p[1] = __builtin_fma(sn, p0, __builtin_fma(dc, p1, p1 + pw1));
+    p[0] = __builtin_fma(cw, p0, __builtin_fma(-sn, p1, pw0));
+    p[1] = __builtin_fma(sn, p0, __builtin_fma(cw, p1, pw1));
     p[2] = p[2] + pw2;
 }
 
@@ -596,14 +608,18 @@ __host__ __device__ constexpr int pidx(int r, int c)
 // World spatial inertia of the lane's body, from its world pose (M = body table row): world com c,
 // rotational inertia about the com Iw, and Ib = Iw + m (|c|^2 E - c c^T), the angular block about
 // the origin (packed xx xy xz yy yz zz); with h = m c the 6x6 is [[m E, -[h]x], [[h]x, Ib]].
-// The energy variant's articulated-body pass reads it from LDS, packed upper triangle (21).
+// The energy variant's articulated-body pass reads it from LDS, packed upper triangle (21), and
+// its RNEA forces take Iw (IW); without it the diagonal of Ib is one FMA chain from the parallel-axis
+// term (Iw itself is not formed) and c one chain from p.
+template <bool IW>
 __device__ __forceinline__ void world_inertia(const double *M, const double *R, const double *p, double *c, double *Iw,
                                               double *Ib)
 {
     const double m = M[T_M];
     const double lc0 = M[T_C], lc1 = M[T_C + 1], lc2 = M[T_C + 2];
 #pragma unroll
-    for (int r = 0; r < 3; r++) c[r] = ((R[3 * r] * lc0 + R[3 * r + 1] * lc1) + R[3 * r + 2] * lc2) + p[r];
+    for (int r = 0; r < 3; r++)
+        c[r] = __builtin_fma(R[3 * r + 2], lc2, __builtin_fma(R[3 * r + 1], lc1, __builtin_fma(R[3 * r], lc0, p[r])));
     const double I00 = M[T_I], I01 = M[T_I + 1], I11 = M[T_I + 2], I02 = M[T_I + 3], I12 = M[T_I + 4], I22 = M[T_I + 5];
     double RI[9];
 #pragma unroll
@@ -613,19 +629,32 @@ __device__ __forceinline__ void world_inertia(const double *M, const double *R, 
         RI[3 * r + 2] = (R[3 * r] * I02 + R[3 * r + 1] * I12) + R[3 * r + 2] * I22;
     }
     const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
-    const double cc2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
-    Iw[0] = (RI[0] * R[0] + RI[1] * R[1]) + RI[2] * R[2];
-    Iw[1] = (RI[0] * R[3] + RI[1] * R[4]) + RI[2] * R[5];
-    Iw[2] = (RI[0] * R[6] + RI[1] * R[7]) + RI[2] * R[8];
-    Iw[3] = (RI[3] * R[3] + RI[4] * R[4]) + RI[5] * R[5];
-    Iw[4] = (RI[3] * R[6] + RI[4] * R[7]) + RI[5] * R[8];
-    Iw[5] = (RI[6] * R[6] + RI[7] * R[7]) + RI[8] * R[8];
-    Ib[0] = Iw[0] + (m * cc2 - mc0 * c[0]);
-    Ib[1] = Iw[1] - mc0 * c[1];
-    Ib[2] = Iw[2] - mc0 * c[2];
-    Ib[3] = Iw[3] + (m * cc2 - mc1 * c[1]);
-    Ib[4] = Iw[4] - mc1 * c[2];
-    Ib[5] = Iw[5] + (m * cc2 - mc2 * c[2]);
+    const double mcc = m * ((c[0] * c[0] + c[1] * c[1]) + c[2] * c[2]);
+    // (row a of RI) . (row b of R), from x: the chains of Iw's packed entries
+    auto rr = [&](int a, int b, double x) {
+        return __builtin_fma(RI[3 * a + 2], R[3 * b + 2], __builtin_fma(RI[3 * a + 1], R[3 * b + 1], __builtin_fma(RI[3 * a], R[3 * b], x)));
+    };
+    if constexpr (IW) {
+        Iw[0] = rr(0, 0, 0.0);
+        Iw[1] = rr(0, 1, 0.0);
+        Iw[2] = rr(0, 2, 0.0);
+        Iw[3] = rr(1, 1, 0.0);
+        Iw[4] = rr(1, 2, 0.0);
+        Iw[5] = rr(2, 2, 0.0);
+        Ib[0] = Iw[0] + (mcc - mc0 * c[0]);
+        Ib[1] = Iw[1] - mc0 * c[1];
+        Ib[2] = Iw[2] - mc0 * c[2];
+        Ib[3] = Iw[3] + (mcc - mc1 * c[1]);
+        Ib[4] = Iw[4] - mc1 * c[2];
+        Ib[5] = Iw[5] + (mcc - mc2 * c[2]);
+    } else {
+        Ib[0] = rr(0, 0, __builtin_fma(-mc0, c[0], mcc));
+        Ib[1] = rr(0, 1, -mc0 * c[1]);
+        Ib[2] = rr(0, 2, -mc0 * c[2]);
+        Ib[3] = rr(1, 1, __builtin_fma(-mc1, c[1], mcc));
+        Ib[4] = rr(1, 2, -mc1 * c[2]);
+        Ib[5] = rr(2, 2, __builtin_fma(-mc2, c[2], mcc));
+    }
 }
 __device__ __forceinline__ void inertia_to_lds(double m, const double *c, const double *Ib, double *dst)
 {
@@ -673,7 +702,8 @@ __device__ __forceinline__ void inertia_mul(double m, const double *c, const dou
 // positions, written to the step record.  (The EE frame velocity J v and J_a J_a^T are formed by
 // the objective from the record's motion subspaces: store_kin.)
 struct CoopKin {
-    double ee[3], am[3];
+    double fp[3];          // the lane's frame position (store_record)
+    double ee[3], am[3];   // broadcast from lanes FR_EE_PARENT / FR_AM_PARENT (the tank's record)
     double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
 };
 
@@ -694,6 +724,7 @@ struct LaneConst {
     int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
     int m_live;     // j < 12: the lane owns a body
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
+    int fp_off;     // store_record: REC_EE / REC_AM on lanes FR_EE_PARENT / FR_AM_PARENT, else REC_FP_SINK
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
     double cmask[9];   // composite_scan: 1.0 when body j is the parent of step s's child (edges 11-9, 10-9, 9-8, .., 3-2)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
@@ -708,42 +739,42 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     const double cz = __builtin_fma(L.rz, cq, L.nrz);   // cq on revolute lanes, 1 elsewhere
     const double sz = L.rz * sq;                         // sq on revolute lanes, 0 elsewhere
     const double qprev = shr<1>(q);
+    // delta form D = R - I (columns 0 and 1; the scan never reads the third): the diagonal's -1 is
+    // the seed of its FMA chain
     double D[9], p[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-        D[3 * r + 0] = M[T_R + 3 * r + 0] * cz + M[T_R + 3 * r + 1] * sz;
-        D[3 * r + 1] = M[T_R + 3 * r + 0] * (-sz) + M[T_R + 3 * r + 1] * cz;
-        D[3 * r + 2] = M[T_R + 3 * r + 2];
+        const double m0 = M[T_R + 3 * r + 0], m1 = M[T_R + 3 * r + 1];
+        D[3 * r + 0] = r == 0 ? __builtin_fma(m0, cz, __builtin_fma(m1, sz, -1.0)) : m0 * cz + m1 * sz;
+        D[3 * r + 1] = r == 1 ? __builtin_fma(m1, cz, __builtin_fma(-m0, sz, -1.0)) : m0 * (-sz) + m1 * cz;
+        D[3 * r + 2] = 0.0;
         p[r] = M[T_P + r] + M[T_MA + r] * q;
     }
     p[1] = p[1] + M[T_FIX] * qprev;
-    D[0] -= 1.0;
-    D[4] -= 1.0;
-    D[8] -= 1.0;
     scan_level2<1>(D, p);
     scan_level2<2>(D, p);
     scan_level2<4>(D, p);
     scan_level_planar8(D, p);
-    delta_col2(D);
     double R[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) R[k] = D[k];
     R[0] += 1.0;
     R[4] += 1.0;
-    R[8] += 1.0;
+    rot_col2(R);
     // motion subspace: revolute (p x w, w), prismatic (w, 0), w = R a
     double w[3], S[6];
 #pragma unroll
     for (int r = 0; r < 3; r++) w[r] = (R[3 * r] * M[T_AX] + R[3 * r + 1] * M[T_AX + 1]) + R[3 * r + 2] * M[T_AX + 2];
     const double rotf = M[T_ROT], nrotf = M[T_NROT];
-    S[0] = (p[1] * w[2] - p[2] * w[1]) * rotf + w[0] * nrotf;
-    S[1] = (p[2] * w[0] - p[0] * w[2]) * rotf + w[1] * nrotf;
-    S[2] = (p[0] * w[1] - p[1] * w[0]) * rotf + w[2] * nrotf;
     S[3] = w[0] * rotf;
     S[4] = w[1] * rotf;
     S[5] = w[2] * rotf;
+    // p x (w rotf) + w nrotf: the same bits as (p x w) rotf + w nrotf on both kinds of lane
+    S[0] = __builtin_fma(p[1], S[5], __builtin_fma(-p[2], S[4], w[0] * nrotf));
+    S[1] = __builtin_fma(p[2], S[3], __builtin_fma(-p[0], S[5], w[1] * nrotf));
+    S[2] = __builtin_fma(p[0], S[4], __builtin_fma(-p[1], S[3], w[2] * nrotf));
     double com[3], Iw[6], Ib[6];
-    world_inertia(M, R, p, com, Iw, Ib);
+    world_inertia<EN>(M, R, p, com, Iw, Ib);
     if constexpr (EN) inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);   // coop_aba's input
     {   // lanes 12..15: the table's dummy body has zero mass and inertia, so h = Ib = 0 there
         bd.m = M[T_M];
@@ -803,13 +834,17 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         for (int k = 0; k < 6; k++) Lk[L_F + L.slot * 6 + k] = f[k];
         kin.pw = ((f[0] * V[0] + f[1] * V[1]) + f[2] * V[2]) + ((f[3] * V[3] + f[4] * V[4]) + f[5] * V[5]);
     }
-    double fpos[3];
+    // the frame at offset T_F of the lane's body: the EE on lane FR_EE_PARENT, the arm mount on lane
+    // FR_AM_PARENT (zero offset elsewhere); without the tank those lanes store it (store_record)
 #pragma unroll
-    for (int r = 0; r < 3; r++) fpos[r] = p[r] + ((R[3 * r] * M[T_F] + R[3 * r + 1] * M[T_F + 1]) + R[3 * r + 2] * M[T_F + 2]);
+    for (int r = 0; r < 3; r++)
+        kin.fp[r] = __builtin_fma(R[3 * r + 2], M[T_F + 2], __builtin_fma(R[3 * r + 1], M[T_F + 1], __builtin_fma(R[3 * r], M[T_F], p[r])));
+    if constexpr (EN) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        kin.ee[k] = bcast<FR_EE_PARENT>(fpos[k]);
-        kin.am[k] = bcast<FR_AM_PARENT>(fpos[k]);
+        for (int k = 0; k < 3; k++) {
+            kin.ee[k] = bcast<FR_EE_PARENT>(kin.fp[k]);
+            kin.am[k] = bcast<FR_AM_PARENT>(kin.fp[k]);
+        }
     }
 }
 
@@ -1163,10 +1198,12 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
         // apart) - a 16-byte one needs (q, qd) in adjacent registers, two v_mov_b32 per step
         __hip_atomic_store(rp + L.rec_off, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __hip_atomic_store(rp + L.rec_off + 1, qd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        double2 *e = reinterpret_cast<double2 *>(rp + REC_EE);
-        e[0] = double2{kin.ee[0], kin.ee[1]};
-        e[1] = double2{kin.ee[2], kin.am[0]};
-        e[2] = double2{kin.am[1], kin.am[2]};
+        // the EE and arm-mount positions from the lanes that own them; the other lanes' frame
+        // positions go to slots nobody reads (REC_FP_SINK)
+        double *f = rp + L.fp_off;
+        f[0] = kin.fp[0];
+        f[1] = kin.fp[1];
+        f[2] = kin.fp[2];
         return;   // (slots 30, 31 - E, pad: the dummy lanes' zero pair)
     }
     double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
@@ -1178,7 +1215,10 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
     a1 = msel(L.m_j15, a1, 0.0);
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
 }
+// slots 88..90: S2Q's entries of the dummy lanes 12..15, written by store_kin and read by nobody
+constexpr int REC_FP_SINK = REC_S2Q + 2 * 12;
 static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_S01 == 32 && REC_S2Q == 64 && FR_REC == 96, "record layout");
+static_assert(REC_FP_SINK + 3 <= FR_REC, "frame-position sink");
 
 // One wave's rows: rollout lr of the launch per 16-lane row (lane j = body j), H steps.  FROW: the
 // row after the last rollout is the previous update's filter() (fx0 / fU / fsteps / frec).  The
@@ -1255,6 +1295,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         int ro = j < FR_NB ? 2 * j : REC_E;
         asm volatile("" : "+v"(ro));
         L.rec_off = ro;
+        int fo = j == FR_EE_PARENT ? REC_EE : (j == FR_AM_PARENT ? REC_AM : REC_FP_SINK);
+        asm volatile("" : "+v"(fo));
+        L.fp_off = fo;
 #pragma unroll
         for (int i = 0; i < 11; i++) {
             double d = ((anc >> i) & 1) ? 1.0 : 0.0;
