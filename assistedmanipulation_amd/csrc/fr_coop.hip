@@ -81,7 +81,8 @@ constexpr int L_QDD = L_DU + FR_NB * 2;
 constexpr int L_TAU = L_QDD + ROW;
 constexpr int LDS_SCR = 272;                // >= L_TAU + ROW, = 16 (mod 32) doubles
 static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * S_STR <= LDS_KIN && L_TAU + ROW <= LDS_SCR, "LDS row layout");
-static_assert(L_TP + 12 <= L_S && L_TP % 2 == 0, "LDS row layout (mass-matrix block)");
+// (L_TP + 12, 13: the dummy lanes' 0 / 1, over L_S, which only the tank's articulated-body pass uses)
+static_assert(L_TP + 14 <= LDS_KIN && L_TP % 2 == 0, "LDS row layout (mass-matrix block)");
 static_assert(L_S + NSLOT * S_STR <= L_F && L_F + NSLOT * 6 <= LDS_KIN_EN && L_F % 2 == 0, "LDS row layout (energy)");
 static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16, "row stride bank offset");
 
@@ -91,8 +92,8 @@ static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16,
 // frame, 1/0 for revolute / prismatic (and its complement), the joint-limit barriers and the
 // velocity weight of the cost, and the lane masks of the kinematic sums.  Row 12 serves lanes
 // 12..15: body 0's geometry with every mask and weight zero.
-constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_I = 16, T_F = 22, T_MA = 25, T_AX = 28, T_ROT = 31, T_NROT = 32;
-constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42, T_MC = 43;
+constexpr int T_R = 0, T_P = 9, T_M = 12, T_C = 13, T_IA = 16, T_IB = 19, T_F = 22, T_MA = 25, T_AX = 28, T_ROT = 31, T_NROT = 32;
+constexpr int T_LO = 33, T_UP = 36, T_VW = 39, T_WV = 40, T_WA = 41, T_FIX = 42, T_MC = 43, T_IL = 44;
 constexpr int MB = 45;   // odd: lanes reading their own body's entry hit distinct banks
 constexpr int LDS_MODEL = (FR_NB + 1) * MB;
 static_assert(LDS_MODEL <= FR_BODY_TABLE, "body table buffer");
@@ -608,39 +609,38 @@ __host__ __device__ constexpr int pidx(int r, int c)
 // World spatial inertia of the lane's body, from its world pose (M = body table row): world com c,
 // rotational inertia about the com Iw, and Ib = Iw + m (|c|^2 E - c c^T), the angular block about
 // the origin (packed xx xy xz yy yz zz); with h = m c the 6x6 is [[m E, -[h]x], [[h]x, Ib]].
-// The energy variant's articulated-body pass reads it from LDS, packed upper triangle (21), and
-// its RNEA forces take Iw (IW); without it the diagonal of Ib is one FMA chain from the parallel-axis
-// term (Iw itself is not formed) and c one chain from p.
+// The body inertia about the com is held in rank-2 form, I = l E + a a^T + b b^T (l its least
+// eigenvalue, a and b the other two eigenvectors scaled by the square roots of their excess over
+// l: inertia_rank2, in the body table), so R I R^T = l E + (R a)(R a)^T + (R b)(R b)^T: two
+// rotated vectors and two FMAs an entry (40 operations for Ib against 55 for R I R^T).  The energy
+// variant's articulated-body pass reads Ib from LDS, packed upper triangle (21), and its RNEA
+// forces take Iw (IW); without it the parallel-axis term seeds Ib's chains and Iw is not formed.
 template <bool IW>
 __device__ __forceinline__ void world_inertia(const double *M, const double *R, const double *p, double *c, double *Iw,
                                               double *Ib)
 {
     const double m = M[T_M];
     const double lc0 = M[T_C], lc1 = M[T_C + 1], lc2 = M[T_C + 2];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-        c[r] = __builtin_fma(R[3 * r + 2], lc2, __builtin_fma(R[3 * r + 1], lc1, __builtin_fma(R[3 * r], lc0, p[r])));
-    const double I00 = M[T_I], I01 = M[T_I + 1], I11 = M[T_I + 2], I02 = M[T_I + 3], I12 = M[T_I + 4], I22 = M[T_I + 5];
-    double RI[9];
+    double ra[3], rb[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-        RI[3 * r + 0] = (R[3 * r] * I00 + R[3 * r + 1] * I01) + R[3 * r + 2] * I02;
-        RI[3 * r + 1] = (R[3 * r] * I01 + R[3 * r + 1] * I11) + R[3 * r + 2] * I12;
-        RI[3 * r + 2] = (R[3 * r] * I02 + R[3 * r + 1] * I12) + R[3 * r + 2] * I22;
+        c[r] = __builtin_fma(R[3 * r + 2], lc2, __builtin_fma(R[3 * r + 1], lc1, __builtin_fma(R[3 * r], lc0, p[r])));
+        ra[r] = __builtin_fma(R[3 * r + 2], M[T_IA + 2], __builtin_fma(R[3 * r + 1], M[T_IA + 1], R[3 * r] * M[T_IA]));
+        rb[r] = __builtin_fma(R[3 * r + 2], M[T_IB + 2], __builtin_fma(R[3 * r + 1], M[T_IB + 1], R[3 * r] * M[T_IB]));
     }
+    const double l = M[T_IL];
     const double mc0 = m * c[0], mc1 = m * c[1], mc2 = m * c[2];
-    const double mcc = m * ((c[0] * c[0] + c[1] * c[1]) + c[2] * c[2]);
-    // (row a of RI) . (row b of R), from x: the chains of Iw's packed entries
-    auto rr = [&](int a, int b, double x) {
-        return __builtin_fma(RI[3 * a + 2], R[3 * b + 2], __builtin_fma(RI[3 * a + 1], R[3 * b + 1], __builtin_fma(RI[3 * a], R[3 * b], x)));
-    };
+    const double cc2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+    // entry (u, v) of (R a)(R a)^T + (R b)(R b)^T, from x
+    auto ab = [&](int u, int v, double x) { return __builtin_fma(ra[u], ra[v], __builtin_fma(rb[u], rb[v], x)); };
     if constexpr (IW) {
-        Iw[0] = rr(0, 0, 0.0);
-        Iw[1] = rr(0, 1, 0.0);
-        Iw[2] = rr(0, 2, 0.0);
-        Iw[3] = rr(1, 1, 0.0);
-        Iw[4] = rr(1, 2, 0.0);
-        Iw[5] = rr(2, 2, 0.0);
+        Iw[0] = ab(0, 0, l);
+        Iw[1] = ab(0, 1, 0.0);
+        Iw[2] = ab(0, 2, 0.0);
+        Iw[3] = ab(1, 1, l);
+        Iw[4] = ab(1, 2, 0.0);
+        Iw[5] = ab(2, 2, l);
+        const double mcc = m * cc2;
         Ib[0] = Iw[0] + (mcc - mc0 * c[0]);
         Ib[1] = Iw[1] - mc0 * c[1];
         Ib[2] = Iw[2] - mc0 * c[2];
@@ -648,12 +648,13 @@ __device__ __forceinline__ void world_inertia(const double *M, const double *R, 
         Ib[4] = Iw[4] - mc1 * c[2];
         Ib[5] = Iw[5] + (mcc - mc2 * c[2]);
     } else {
-        Ib[0] = rr(0, 0, __builtin_fma(-mc0, c[0], mcc));
-        Ib[1] = rr(0, 1, -mc0 * c[1]);
-        Ib[2] = rr(0, 2, -mc0 * c[2]);
-        Ib[3] = rr(1, 1, __builtin_fma(-mc1, c[1], mcc));
-        Ib[4] = rr(1, 2, -mc1 * c[2]);
-        Ib[5] = rr(2, 2, __builtin_fma(-mc2, c[2], mcc));
+        const double mcl = __builtin_fma(m, cc2, l);   // m |c|^2 + l, the diagonal's common part
+        Ib[0] = ab(0, 0, __builtin_fma(-mc0, c[0], mcl));
+        Ib[1] = ab(0, 1, -mc0 * c[1]);
+        Ib[2] = ab(0, 2, -mc0 * c[2]);
+        Ib[3] = ab(1, 1, __builtin_fma(-mc1, c[1], mcl));
+        Ib[4] = ab(1, 2, -mc1 * c[2]);
+        Ib[5] = ab(2, 2, __builtin_fma(-mc2, c[2], mcl));
     }
 }
 __device__ __forceinline__ void inertia_to_lds(double m, const double *c, const double *Ib, double *dst)
@@ -702,8 +703,7 @@ __device__ __forceinline__ void inertia_mul(double m, const double *c, const dou
 // positions, written to the step record.  (The EE frame velocity J v and J_a J_a^T are formed by
 // the objective from the record's motion subspaces: store_kin.)
 struct CoopKin {
-    double fp[3];          // the lane's frame position (store_record)
-    double ee[3], am[3];   // broadcast from lanes FR_EE_PARENT / FR_AM_PARENT (the tank's record)
+    double fp[3];   // the lane's frame position (store_record: EE on lane FR_EE_PARENT, arm mount on FR_AM_PARENT)
     double pw;   // energy tank: f . V of the lane's body (NLE power at the pre-step velocity)
 };
 
@@ -720,9 +720,10 @@ struct LaneConst {
     double rz, nrz;   // is_rz as 1.0 / 0.0 and its complement: the joint rotation's (cos, sin) by one FMA
                       // and one multiply instead of four v_cndmask_b32
     // opaque lane masks (0 / -1) for msel, built once before the horizon loop
-    int m_j0, m_j1, m_j2, m_j12, m_j13, m_j14, m_j15;   // j == n
-    int m_tau;      // 3 <= j < 10: the arm joints tau_u drives
-    int m_live;     // j < 12: the lane owns a body
+    int m_j12, m_j13, m_j14, m_j15;   // j == n
+    // lane coefficients (1.0 / 0.0, opaque): base_velocity's, and tau_u's (3 <= j < 10: the arm
+    // joints it drives)
+    double bA, bB, bnA, bC, bkeep, taud;
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     int fp_off;     // store_record: REC_EE / REC_AM on lanes FR_EE_PARENT / FR_AM_PARENT, else REC_FP_SINK
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
@@ -835,17 +836,10 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
         kin.pw = ((f[0] * V[0] + f[1] * V[1]) + f[2] * V[2]) + ((f[3] * V[3] + f[4] * V[4]) + f[5] * V[5]);
     }
     // the frame at offset T_F of the lane's body: the EE on lane FR_EE_PARENT, the arm mount on lane
-    // FR_AM_PARENT (zero offset elsewhere); without the tank those lanes store it (store_record)
+    // FR_AM_PARENT (zero offset elsewhere), for store_record
 #pragma unroll
     for (int r = 0; r < 3; r++)
         kin.fp[r] = __builtin_fma(R[3 * r + 2], M[T_F + 2], __builtin_fma(R[3 * r + 1], M[T_F + 1], __builtin_fma(R[3 * r], M[T_F], p[r])));
-    if constexpr (EN) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            kin.ee[k] = bcast<FR_EE_PARENT>(kin.fp[k]);
-            kin.am[k] = bcast<FR_AM_PARENT>(kin.fp[k]);
-        }
-    }
 }
 
 // The record's motion subspaces for the objective's J v and J_a J_a^T (kernels.hpp REC_S01 /
@@ -1059,6 +1053,29 @@ __device__ __forceinline__ void composite_scan(double *v, const double *m)
         : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(m[5]), "v"(m[6]), "v"(m[7]), "v"(m[8]));
 }
 
+// PinocchioDynamics::step's base velocity overwrite (pinocchio_dynamics.cpp): lane 0 takes
+// vx = c u0 - s u1, lane 1 vy = s u0 + c u1 (c, s: the base yaw's, lane 2; u0, u1: lanes 0, 1),
+// lane 2 u itself, the other lanes keep qd.  As lane coefficients: P = A c + B s, Q = B c - A s,
+// qd' = (C u + u0 P) + (keep qd + u1 Q), six broadcast FMAs in place of four broadcasts, four
+// products and three two-way selects.  The order keeps two instructions between a VGPR's write and
+// a DPP instruction's read of it (one s_nop where nothing else fits).
+__device__ __forceinline__ double base_velocity(const LaneConst &L, double u, double sq, double cq, double qd)
+{
+    double P = 0.0, Q = 0.0, X, Y;
+    asm("v_fmac_f64_dpp %0, %5, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // P = c A
+        "v_fmac_f64_dpp %1, %5, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // Q = c B
+        "v_mul_f64 %2, %11, %6\n\t"                                                  // X = C u
+        "v_mul_f64 %3, %12, %7\n\t"                                                  // Y = keep qd
+        "v_fmac_f64_dpp %0, %4, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // P += s B
+        "v_fmac_f64_dpp %1, %4, %10 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"   // Q += s (-A)
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %2, %6, %0 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"    // X += u0 P
+        "v_fmac_f64_dpp %3, %6, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf"          // Y += u1 Q
+        : "+&v"(P), "+&v"(Q), "=&v"(X), "=&v"(Y)
+        : "v"(sq), "v"(cq), "v"(u), "v"(qd), "v"(L.bA), "v"(L.bB), "v"(L.bnA), "v"(L.bC), "v"(L.bkeep));
+    return X + Y;
+}
+
 // Mass-matrix solve for the rollouts without the energy tank: qdd = M(q)^-1 tau_u, M by the
 // composite-rigid-body algorithm in world coordinates and eliminated by Gauss-Jordan, one column
 // per lane.  Equal to the zero-bias articulated-body pass in exact arithmetic; its serial chain is
@@ -1115,9 +1132,10 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     double *dst = (j == 12) ? Lk + L_TP : Row;
 #pragma unroll
     for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(dst + i) = double2{Mc[i], Mc[i + 1]};
-    const double tp = Lk[L_TP + (j < FR_NB ? j : 0)];
-    const double dj = Row[j];
-    return msel(L.m_live, 0.0, tp * frcp(dj));   // lanes 12..15 keep q = qd = 0
+    // Lanes 12..15 read 0 / 1 (L_TP + 12, 13, coop_rows' entry): qdd = 0, q = qd = 0 for good
+    const double tp = Lk[j < FR_NB ? L_TP + j : L_TP + 12];
+    const double dj = Lk[j < FR_NB ? L_COL + j * CSTR + j : L_TP + 13];
+    return tp * frcp(dj);
 }
 
 }  // namespace
@@ -1127,6 +1145,53 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 // (launch_fr_body_table, at create: the model and cost are constants of the handle).  Built in the
 // rollout kernels themselves, its chain of dependent, divergent loads of the model held every
 // workgroup for ~7 us before its first step (PRO_TRACE); a copy of the table is one load.
+// A symmetric 3x3 inertia (packed xx xy yy xz yz zz, DevBody::Ic) as l E + a a^T + b b^T: cyclic
+// Jacobi rotations to its eigenvalues / vectors, l the least eigenvalue, a and b the other two
+// eigenvectors times sqrt(lambda - l) (inertias are positive semi-definite, so l >= 0 and the two
+// excesses are >= 0; rounding is clamped).
+__device__ void inertia_rank2(const double *Ic, double *a, double *b, double *l)
+{
+    double A[3][3] = {{Ic[0], Ic[1], Ic[3]}, {Ic[1], Ic[2], Ic[4]}, {Ic[3], Ic[4], Ic[5]}};
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+    for (int sweep = 0; sweep < 32; sweep++) {
+        const double off = fabs(A[0][1]) + fabs(A[0][2]) + fabs(A[1][2]);
+        if (off == 0.0) break;
+        for (int pq = 0; pq < 3; pq++) {
+            const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
+            if (A[p][q] == 0.0) continue;
+            const double th = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+            const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+            for (int k = 0; k < 3; k++) {   // A <- A J (columns p, q)
+                const double akp = A[k][p], akq = A[k][q];
+                A[k][p] = c * akp - s * akq;
+                A[k][q] = s * akp + c * akq;
+            }
+            for (int k = 0; k < 3; k++) {   // A <- J^T A (rows p, q)
+                const double apk = A[p][k], aqk = A[q][k];
+                A[p][k] = c * apk - s * aqk;
+                A[q][k] = s * apk + c * aqk;
+            }
+            A[p][q] = A[q][p] = 0.0;
+            for (int k = 0; k < 3; k++) {   // V <- V J
+                const double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = c * vkp - s * vkq;
+                V[k][q] = s * vkp + c * vkq;
+            }
+        }
+    }
+    int lo = 0;
+    for (int i = 1; i < 3; i++)
+        if (A[i][i] < A[lo][lo]) lo = i;
+    const int i1 = lo == 0 ? 1 : 0, i2 = lo == 2 ? 1 : 2;
+    *l = A[lo][lo];
+    const double sa = sqrt(fmax(A[i1][i1] - *l, 0.0)), sb = sqrt(fmax(A[i2][i2] - *l, 0.0));
+    for (int k = 0; k < 3; k++) {
+        a[k] = sa * V[k][i1];
+        b[k] = sb * V[k][i2];
+    }
+}
+
 __global__ void fr_body_table_kernel(const DevModel *model, const DevCost *cost, double *table)
 {
     const DevModel &dm = *model;
@@ -1148,8 +1213,12 @@ __global__ void fr_body_table_kernel(const DevModel *model, const DevCost *cost,
         if (f < T_P) v = Rs[f];
         else if (f < T_M) v = ps[f - T_P];
         else if (f == T_M) v = live * db.mass;   // the dummy body (lanes 12..15) is massless:
-        else if (f < T_I) v = live * db.c[f - T_C];   // its world inertia, F and M column vanish
-        else if (f < T_F) v = live * db.Ic[f - T_I];
+        else if (f < T_IA) v = live * db.c[f - T_C];   // its world inertia, F and M column vanish
+        else if (f < T_F || f == T_IL) {   // the rotational inertia in rank-2 form (inertia_rank2)
+            double ia[3], ib[3], il;
+            inertia_rank2(db.Ic, ia, ib, &il);
+            v = live * (f == T_IL ? il : (f < T_IB ? ia[f - T_IA] : ib[f - T_IB]));
+        }
         else if (f < T_MA) v = (b == FR_EE_PARENT) ? dm.ee_p[f - T_F] : ((b == FR_AM_PARENT) ? dm.am_p[f - T_F] : 0.0);
         else if (f < T_AX) {
             const int r = f - T_MA;
@@ -1206,11 +1275,17 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
         f[2] = kin.fp[2];
         return;   // (slots 30, 31 - E, pad: the dummy lanes' zero pair)
     }
-    double a0 = msel(L.m_j12, q, kin.ee[0]), a1 = msel(L.m_j12, qd, kin.ee[1]);
-    a0 = msel(L.m_j13, a0, kin.ee[2]);
-    a1 = msel(L.m_j13, a1, kin.am[0]);
-    a0 = msel(L.m_j14, a0, kin.am[1]);
-    a1 = msel(L.m_j14, a1, kin.am[2]);
+    double ee[3], am[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        ee[k] = bcast<FR_EE_PARENT>(kin.fp[k]);
+        am[k] = bcast<FR_AM_PARENT>(kin.fp[k]);
+    }
+    double a0 = msel(L.m_j12, q, ee[0]), a1 = msel(L.m_j12, qd, ee[1]);
+    a0 = msel(L.m_j13, a0, ee[2]);
+    a1 = msel(L.m_j13, a1, am[0]);
+    a0 = msel(L.m_j14, a0, am[1]);
+    a1 = msel(L.m_j14, a1, am[2]);
     a0 = msel(L.m_j15, a0, E);
     a1 = msel(L.m_j15, a1, 0.0);
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
@@ -1279,15 +1354,21 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         L.nrz = nrz;
     }
     L.slot = jl ? j : FR_NB;
-    L.m_j0 = opaque_mask(j == 0);
-    L.m_j1 = opaque_mask(j == 1);
-    L.m_j2 = opaque_mask(j == 2);
     L.m_j12 = opaque_mask(j == 12);
     L.m_j13 = opaque_mask(j == 13);
     L.m_j14 = opaque_mask(j == 14);
     L.m_j15 = opaque_mask(j == 15);
-    L.m_tau = opaque_mask(j >= 3 && j < 10);
-    L.m_live = opaque_mask(jl);
+    {
+        double cA = j == 0 ? 1.0 : 0.0, cB = j == 1 ? 1.0 : 0.0, cC = j == 2 ? 1.0 : 0.0;
+        double ck = j > 2 ? 1.0 : 0.0, ct = (j >= 3 && j < 10) ? 1.0 : 0.0;
+        asm volatile("" : "+v"(cA), "+v"(cB), "+v"(cC), "+v"(ck), "+v"(ct));   // kept in registers
+        L.bA = cA;
+        L.bnA = -cA;
+        L.bB = cB;
+        L.bC = cC;
+        L.bkeep = ck;
+        L.taud = ct;
+    }
     {
         int anc = (1 << (j < 11 ? j : 11)) - 1;   // bodies i < j
         if (j == FR_NB - 1) anc &= ~(1 << (FR_NB - 2));   // finger 11 is not under finger 10
@@ -1338,6 +1419,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     if constexpr (!EN) {
         Lk[L_COL + j * CSTR + 13] = 0.0;
         *reinterpret_cast<double2 *>(Lk + L_COL + j * CSTR + 14) = double2{0.0, 0.0};
+        *reinterpret_cast<double2 *>(Lk + L_TP + 12) = double2{0.0, 1.0};   // coop_solve's dummy-lane reads
     }
     if (kb == 0) {
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
@@ -1346,8 +1428,8 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
 
     // eps and U*_shifted of step k: loaded at the top of the step
     const bool sampled = !opt_row && jl;
-    int smask = sampled ? -1 : 0, jmask = jl ? -1 : 0;
-    asm volatile("" : "+v"(smask), "+v"(jmask));   // opaque: kept as data, not folded into control flow
+    double sd = sampled ? 1.0 : 0.0, jd = jl ? 1.0 : 0.0;
+    asm volatile("" : "+v"(sd), "+v"(jd));   // opaque: kept as data, not folded into control flow
     int64_t nstride = sampled ? a.Rpad * FR_C : 0;   // unsampled rows re-read their first element
     asm volatile("" : "+v"(nstride));
     const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
@@ -1362,19 +1444,12 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
         ub_n = Up[min(k + 1 + ush, H - 1) * FR_C + jb];
-        // bit masks, not selects: a select here became a branch around the eps use, and the
-        // waitcnt pass then waited for every store in flight (vmcnt(0)) at the top of each step
-        const double eps = __hiloint2double(__double2hiint(eps_l) & smask, __double2loint(eps_l) & smask);
-        const double ub = __hiloint2double(__double2hiint(ub_l) & jmask, __double2loint(ub_l) & jmask);
+        // u = U*_shifted + eps as data (1.0 / 0.0 coefficients, not selects: a select here became a
+        // branch around the eps use, and the waitcnt pass then waited for every store in flight,
+        // vmcnt(0), at the top of each step); unsampled rows add 0 eps, lanes 12..15 hold u = 0
         // PinocchioDynamics::step: base velocity overwrite, tau = arm controls, calculate, Euler
-        const double u = ub + eps;
-        {
-            const double s = bcast<2>(sq), c = bcast<2>(cq);
-            const double u0 = bcast<0>(u), u1 = bcast<1>(u);
-            const double vx = c * u0 + (-s) * u1;
-            const double vy = s * u0 + c * u1;
-            qd = msel(L.m_j0, msel(L.m_j1, msel(L.m_j2, qd, u), vy), vx);
-        }
+        const double u = __builtin_fma(eps_l, sd, ub_l * jd);
+        qd = base_velocity(L, u, sq, cq, qd);
         if constexpr (EN)
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
@@ -1382,7 +1457,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         double pe = 0.0;
         double qdd;
         if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe);
-        else qdd = coop_solve(j, L, bd, msel(L.m_tau, 0.0, u), Lk);
+        else qdd = coop_solve(j, L, bd, u * L.taud, Lk);
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
         if constexpr (EN) {   // power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
