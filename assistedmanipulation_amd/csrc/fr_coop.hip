@@ -1736,9 +1736,8 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
     const int H = a.H;
     const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
     const int wblk = gridDim.x * 4 + blockIdx.x;
-    if (!a.handover) {   // every step on this wave (the stages' code with one stage)
-        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, 0, 0x7FFFFFFF);
-    } else {
+    int kb = 0, ke = 0x7FFFFFFF;   // without a.handover: every step on this wave (one stage)
+    if (a.handover) {
         // the next update's draws for main wave r's rows first (block 0's wave 0 rows are left to
         // rank_draw_kernel)
         if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
@@ -1754,7 +1753,12 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
             }
         }
         __builtin_amdgcn_s_setprio(3);   // above the main waves (1) and the objective's (0)
-        coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, relay_step(r, H), relay_step(r + 1, H));
+        kb = relay_step(r, H);
+        ke = relay_step(r + 1, H);
+    }
+    // one call site: one copy of the step loop for both shapes
+    coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke);
+    if (a.handover) {
         __builtin_amdgcn_s_setprio(0);
 #ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
         if (a.trace && blockIdx.x == 0 && lane == 0 && r < 4) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
