@@ -388,7 +388,7 @@ __device__ __forceinline__ double wave_sum(double v) { return mppi_dev::wave_sum
 // bits) and no second pass runs.  The block's eps and cost loads are issued first, together, and
 // land during the reductions.  Block (0, 0) writes the status words.
 constexpr int WV = 16;       // waves of the 1024-thread reduction order
-constexpr int WU = 8;        // costs per (virtual) thread and pass
+constexpr int WU = 2;        // costs per (virtual) thread and pass (min / max / count are exact in any order)
 constexpr int NV = WV / 4;   // virtual waves per real wave
 constexpr int GR = 3;     // rollouts per thread whose eps is loaded up front (R = 4098: 513 per block)
 
@@ -476,22 +476,40 @@ __global__ __launch_bounds__(256) void softmin_exp_kernel(WGradArgs a)
     if (t == 0) a.wpart[3 * SM_NB + blockIdx.x] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
 }
 
+// C = FR_C (96-byte eps rows): a block takes two steps (k, k + 1) of split s, so the cost
+// statistics' fold and the window's exponentials - the same for every step - are formed once per
+// two steps, and the grid is (H / 2) x GRAD_SPLIT = 256 workgroups, one per CU.  The eps are read
+// contiguously, eight rollouts (768 B) per wave load on lanes 0..47, lane l always holding
+// component pair l % 6 of rollout l / 6 of the octet: a load touches 6 cache lines, where one
+// rollout per lane touched 48 for 1 KB.  The loads go through a buffer descriptor per step over the
+// block's rows (32-bit offsets, the step's stride in the scalar offset; rows past the block read 0
+// from the range check).  The window's e_r go through LDS (rollout 8 o + l / 6 for octet o), and the
+// lanes' pair partials are added per component at the end.
+constexpr int WG_OCT = 17;              // octet loads per lane, step and window (4 waves x 8 rollouts)
+constexpr int WG_WIN = 32 * WG_OCT;     // rollouts per window (544: R = 4098 is 513 per split, one window)
+constexpr int WG_KPB = 2;               // steps per workgroup (C = FR_C)
+static_assert(WG_WIN <= 256 * GR, "a window's costs are loaded by the GR cost loads");
+
 template <int C, bool LARGE>
 __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
 {
     constexpr int CP = C;
+    constexpr bool OCT = C == FR_C;
+    constexpr int KPB = OCT ? WG_KPB : 1;
+    typedef double d2v __attribute__((ext_vector_type(2)));
     __shared__ double red[4 * CP];
     __shared__ double smn[WV], smx[WV], ssum[WV];
+    __shared__ double es[OCT ? 256 * GR : 1];            // e_r of the window (OCT)
+    __shared__ double ored[OCT ? KPB * 4 * 48 * 2 : 1];  // lane pair partials, [step][wave][lane][2] (OCT)
     const int t = threadIdx.x, rw = t >> 6, l = t & 63;
     const int64_t R = a.R;
-    const int k = blockIdx.x, s = blockIdx.y, ns = gridDim.y;
+    const int kb = blockIdx.x * KPB, s = blockIdx.y, ns = gridDim.y;
+    const bool k0 = blockIdx.x == 0;   // the block holding step 0
     const int64_t chunk = (a.count + ns - 1) / ns;
     const int64_t r0 = (int64_t)s * chunk, r1 = (r0 + chunk < a.count) ? r0 + chunk : a.count;
     // One memory trip, in this order: the cost statistics (unsharded), the costs (LARGE: e_r), then
     // the eps rows.  Vector memory completes in issue order, so the exponentials - which need only
-    // the costs and min / max - are formed while the eps loads are still in flight.  (Until r05 the
-    // statistics were loaded after the eps, and every block waited for all of its eps before its
-    // first exponential.)
+    // the costs and min / max - are formed while the eps loads are still in flight.
     const bool stats = !LARGE && a.stats != nullptr;
     unsigned long long skn = ~0ull, skx = 0;
     unsigned int scn = 0;
@@ -500,34 +518,53 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         skx = a.stats->kmax[16 * l];
         scn = a.stats->count[32 * l];
     }
-    double cpre[GR];    // the costs of rollouts r0 + t + 256 m (LARGE: e_r)
+    double cpre[GR];    // the costs of rollouts wb + t + 256 m of the window (LARGE: e_r)
+    double ne[OCT ? 1 : GR][OCT ? 1 : CP];   // C != FR_C: their eps
+    d2v ov[OCT ? KPB : 1][OCT ? WG_OCT : 1]; // OCT: the window's octet loads per step
+    const int pl = l % 6, rl = l / 6;        // OCT: this lane's pair and rollout within an octet
+    const bool al = l < 48;
+    // OCT: the steps' descriptors over rows [r0, r1) (built from launch-uniform values only)
+    __amdgpu_buffer_rsrc_t rs[OCT ? KPB : 1];
+    if constexpr (OCT) {
 #pragma unroll
-    for (int m = 0; m < GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        const int64_t gi = a.begin + (r < r1 ? r : 0);
-        if constexpr (LARGE) cpre[m] = a.wexp[gi];
-        else cpre[m] = a.cost[gi];
-    }
-    double ne[GR][CP];   // their eps (row 0 stands in past r1, unused)
-#pragma unroll
-    for (int m = 0; m < GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        const double *n = a.noise + ((int64_t)k * a.Rpad + (r < r1 ? r : 0)) * C;
-        if constexpr (CP % 2 == 0) {   // 16-byte loads (FrankaRidgeback: 96-byte rows)
-#pragma unroll
-            for (int c = 0; c < CP; c += 2) {
-                const double2 v = reinterpret_cast<const double2 *>(n)[c / 2];
-                ne[m][c] = v.x;
-                ne[m][c + 1] = v.y;
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < CP; c++) ne[m][c] = n[c];
+        for (int j = 0; j < KPB; j++) {
+            const int kk = min(kb + j, a.H - 1);
+            rs[j] = __builtin_amdgcn_make_buffer_rsrc((void *)(a.noise + ((int64_t)kk * a.Rpad + r0) * C), (short)0,
+                                                      (int)((r1 - r0) * C * 8), 0x00020000);
         }
     }
-    // unsharded, the normaliser slice of block (0, s) is its own rollout range [r0, r1): its e_r come
-    // from the gradient loop below, in the same per-thread order as the separate slice pass
-    const bool own_slice = !LARGE && k == 0 && a.begin == 0 && a.count == R;
+    auto load_window = [&](int64_t wb) {
+#pragma unroll
+        for (int m = 0; m < GR; m++) {
+            const int64_t r = wb + t + 256 * m;
+            const int64_t gi = a.begin + (r < r1 ? r : 0);
+            if constexpr (LARGE) cpre[m] = a.wexp[gi];
+            else cpre[m] = a.cost[gi];
+        }
+        if constexpr (OCT) {
+            const int noct = (int)((min(r1 - wb, (int64_t)WG_WIN) + 7) / 8);   // octets in the window
+            // lanes 48..63 and rows past r1 read 0 (past the descriptor's range)
+            const int voff = al ? (int)((wb - r0 + 8 * rw + rl) * (C * 8) + 16 * pl) : 0x7FFFFFF0;
+#pragma unroll
+            for (int j = 0; j < KPB; j++)
+#pragma unroll
+                for (int u = 0; u < WG_OCT; u++)
+                    if (rw + 4 * u < noct)   // wave-uniform
+                        ov[j][u] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs[j], voff, u * 32 * C * 8, 0));
+        } else {
+#pragma unroll
+            for (int m = 0; m < GR; m++) {
+                const int64_t r = wb + t + 256 * m;
+                const double *n = a.noise + ((int64_t)kb * a.Rpad + (r < r1 ? r : 0)) * C;
+#pragma unroll
+                for (int c = 0; c < CP; c++) ne[m][c] = n[c];
+            }
+        }
+    };
+    load_window(r0);
+    // unsharded, the normaliser slice of the step-0 block (0, s) is its own rollout range [r0, r1):
+    // its e_r come from the gradient loop below, in the same per-thread order as the slice pass
+    const bool own_slice = !LARGE && k0 && a.begin == 0 && a.count == R;
     double minimum, maximum, valid, total;
     if constexpr (LARGE) {
         if (rw == 0) {
@@ -542,11 +579,13 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         total = ssum[1];
     } else if (stats) {   // from the objective's atomics (exact: the same values as the pass)
         static_assert(CS_SLOTS == 64, "one slot per lane");
-        const unsigned long long kn = mppi_dev::wave_umin64_dpp(skn);
-        const unsigned long long kx = mppi_dev::wave_umax64_dpp(skx);
+        // the slots' keys decoded (order-preserving: the min / max of the values are the values of
+        // the min / max keys), empty slots as +inf / -inf, folded as doubles
+        const double vn = skn == ~0ull ? (double)INFINITY : mppi_dev::cost_from_key(skn);
+        const double vx = skx == 0ull ? -(double)INFINITY : mppi_dev::cost_from_key(skx);
         const unsigned int n = (unsigned int)mppi_dev::wave_sum_dpp((double)scn);
-        minimum = n ? mppi_dev::cost_from_key(kn) : (double)INFINITY;
-        maximum = n ? mppi_dev::cost_from_key(kx) : -(double)INFINITY;
+        minimum = n ? mppi_dev::wave_min_dpp(vn) : (double)INFINITY;
+        maximum = n ? mppi_dev::wave_max_dpp(vx) : -(double)INFINITY;
         valid = (double)n;
         total = 0.0;
     } else {
@@ -601,7 +640,7 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
     __syncthreads();
     total = 0.0;
     }
-    const bool lead = k == 0 && s == 0 && t == 0;
+    const bool lead = k0 && s == 0 && t == 0;
     Status *st = a.status;
     if (valid <= 1.0) {   // minmax_element over <= 1 element: it1 == it2 -> throw
         if (lead) { st->all_nan = 1; st->early = 1; st->minimum = minimum; st->maximum = maximum; }
@@ -613,11 +652,9 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         return;
     }
     auto expw = [&](double c) { return isnan(c) ? 0.0 : exp(-a.cost_scale * (c - minimum) / difference); };
-    // e_r of global rollout i: recomputed, or (LARGE) written by softmin_exp_kernel
-    auto wexp = [&](int64_t i) { if constexpr (LARGE) return a.wexp[i]; else return expw(a.cost[i]); };
     if constexpr (LARGE) {   // the normaliser is known: one partial carries it
-        if (k == 0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
-    } else if (k == 0 && !own_slice) {   // slice s of [0, R): e_r and its sum
+        if (k0 && t < GRAD_SPLIT) st->tsplit[t] = t == 0 ? total : 0.0;
+    } else if (k0 && !own_slice) {   // slice s of [0, R): e_r and its sum
         const int64_t wc = (R + ns - 1) / ns, w0 = (int64_t)s * wc, w1 = (w0 + wc < R) ? w0 + wc : R;
         double part = 0.0;
         for (int64_t i = w0 + t; i < w1; i += 256) {
@@ -632,54 +669,96 @@ __global__ __launch_bounds__(256) void weights_gradient_kernel(WGradArgs a)
         if (t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
     }
     if (lead) { st->all_nan = 0; st->early = 0; st->minimum = minimum; st->maximum = maximum; }
-    double acc[CP];
+    double acc[CP];      // C != FR_C: this thread's rollouts' sum
 #pragma unroll
     for (int c = 0; c < CP; c++) acc[c] = 0.0;
+    d2v oacc[OCT ? KPB : 1];   // OCT: this lane's pair, per step
+#pragma unroll
+    for (int j = 0; j < (OCT ? KPB : 1); j++) oacc[j] = d2v{0.0, 0.0};
     double part = 0.0;   // own_slice: this thread's share of the normaliser slice
-    double wr[GR];       // every exponential before the first eps is read (the loads still land)
+    for (int64_t wb = r0; wb < r1;) {
+        // the window's exponentials (their loads landed with the eps still in flight); OCT windows
+        // are WG_WIN rollouts, the GR cost loads may reach past one
+        const int64_t we = OCT ? min(r1, wb + WG_WIN) : r1;
+        double wr[GR];
 #pragma unroll
-    for (int m = 0; m < GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        if constexpr (LARGE) wr[m] = cpre[m];
-        else wr[m] = expw(cpre[m]);
-        wr[m] = r < r1 ? wr[m] : 0.0;
-        if (own_slice && r < r1) {
-            a.wexp[r] = wr[m];
-            part += wr[m];
+        for (int m = 0; m < GR; m++) {
+            const int64_t r = wb + t + 256 * m;
+            if constexpr (LARGE) wr[m] = cpre[m];
+            else wr[m] = expw(cpre[m]);
+            wr[m] = r < we ? wr[m] : 0.0;
+            if (own_slice && r < we) {
+                a.wexp[r] = wr[m];
+                part += wr[m];
+            }
         }
-    }
+        if constexpr (OCT) {
 #pragma unroll
-    for (int m = 0; m < GR; m++) {
-        const int64_t r = r0 + t + 256 * m;
-        if (r < r1) {
+            for (int m = 0; m < GR; m++) es[t + 256 * m] = wr[m];
+            __syncthreads();
+            const int noct = (int)((min(r1 - wb, (int64_t)WG_WIN) + 7) / 8);
 #pragma unroll
-            for (int c = 0; c < CP; c++) acc[c] += wr[m] * ne[m][c];
+            for (int u = 0; u < WG_OCT; u++) {
+                const int o = rw + 4 * u;
+                if (o < noct) {
+                    const double w = es[8 * o + rl];   // zero past r1 (wr above); lanes >= 48 loaded 0
+#pragma unroll
+                    for (int j = 0; j < KPB; j++) oacc[j] += w * ov[j][u];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < GR; m++) {
+                const int64_t r = wb + t + 256 * m;
+                if (r < r1) {
+#pragma unroll
+                    for (int c = 0; c < CP; c++) acc[c] += wr[m] * ne[m][c];
+                }
+            }
         }
-    }
-    for (int64_t r = r0 + t + 256 * GR; r < r1; r += 256) {
-        const double wr = wexp(a.begin + r);
-        if (own_slice) {
-            a.wexp[r] = wr;
-            part += wr;
-        }
-        const double *n = a.noise + ((int64_t)k * a.Rpad + r) * C;
-#pragma unroll
-        for (int c = 0; c < CP; c++) acc[c] += wr * n[c];
+        wb += OCT ? WG_WIN : 256 * GR;
+        if (wb >= r1) break;
+        if constexpr (OCT) __syncthreads();   // es is rewritten by the next window
+        load_window(wb);   // ranges past one window (R > 8 x 544): one more memory trip per window
     }
     if (own_slice) {   // as the slice pass: butterflies, then the four wave sums in order
         part = wave_sum(part);
         if (l == 0) ssum[rw] = part;
     }
-    // the block's 256 partials: butterflies within each wave, then the four wave sums in order
+    if constexpr (OCT) {
+        // component c = 2 p + i of step kb + j: the 32 lane partials of pair p (lanes p + 6 q of the
+        // four waves), in wave order
+        if (al)
 #pragma unroll
-    for (int c = 0; c < CP; c++) acc[c] = wave_sum(acc[c]);
-    if (l == 0)
+            for (int j = 0; j < KPB; j++) {
+                ored[((j * 4 + rw) * 48 + l) * 2] = oacc[j][0];
+                ored[((j * 4 + rw) * 48 + l) * 2 + 1] = oacc[j][1];
+            }
+        __syncthreads();
+        if (t < KPB * CP) {
+            const int j = t / CP, c = t % CP, p = c >> 1, i = c & 1;
+            double g = 0.0;
 #pragma unroll
-        for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
-    __syncthreads();
-    if (t < CP)
-        a.gsplit[((int64_t)s * a.H + k) * C + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
-    if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);
+            for (int w = 0; w < 4; w++) {
+                double gw = 0.0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) gw += ored[((j * 4 + w) * 48 + p + 6 * q) * 2 + i];
+                g += gw;
+            }
+            if (kb + j < a.H) a.gsplit[((int64_t)s * a.H + kb + j) * C + c] = g;
+        }
+    } else {
+        // the block's 256 partials: butterflies within each wave, then the four wave sums in order
+#pragma unroll
+        for (int c = 0; c < CP; c++) acc[c] = wave_sum(acc[c]);
+        if (l == 0)
+#pragma unroll
+            for (int c = 0; c < CP; c++) red[rw * CP + c] = acc[c];
+        __syncthreads();
+        if (t < CP)
+            a.gsplit[((int64_t)s * a.H + kb) * C + t] = (red[t] + red[CP + t]) + (red[2 * CP + t] + red[3 * CP + t]);
+    }
+    if (own_slice && t == 0) st->tsplit[s] = (ssum[0] + ssum[1]) + (ssum[2] + ssum[3]);   // (ordered by the barrier above)
 }
 
 __global__ void gradient_sum_kernel(const double *__restrict__ gsplit, int ns, int HC, const Status *__restrict__ status,
@@ -1177,7 +1256,8 @@ hipError_t launch_pm_rollout(const PmRolloutArgs &a, hipStream_t s)
 
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s)
 {
-    const dim3 grid((unsigned)a.H, GRAD_SPLIT);
+    // C = FR_C: WG_KPB steps per workgroup (weights_gradient_kernel)
+    const dim3 grid(a.C == FR_C ? (unsigned)((a.H + WG_KPB - 1) / WG_KPB) : (unsigned)a.H, GRAD_SPLIT);
     if (a.C != FR_C && a.C != 3) return hipErrorInvalidValue;
     if (a.R > SM_LARGE_R) {
         hipLaunchKernelGGL(softmin_minmax_kernel, dim3(SM_NB), dim3(256), 0, s, a);

@@ -22,6 +22,7 @@
 #                      AB_ENV_<V> (extra env for variant V, e.g. AB_ENV_tree0="MPPI_HANDOVER=0") apply
 #   pmstamps[:VARIANT] the fused point-mass kernel's phase stamps (MPPI_PM_STAMPS=1), in-tree or a variant
 #   wtrace:VARIANT     per-wave trace of VARIANT's COOP_TRACE build (tools/wave_trace_r03.py)
+#   kpmc:V1,V2,..      PMC of the kernels outside the rollout launch (weights / finish / rank), per library
 # Output: gpurun_out/$TAG/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -106,6 +107,26 @@ step_pmc() {   # [pm]
     python3 tools/pmc_traffic.py $D $out $prefix && cat $out
 }
 
+step_kpmc() {   # V1,V2,..: counters of the kernels outside the rollout launch, per library ("tree" = in-tree)
+    local vs
+    IFS=, read -ra vs <<< "$1"
+    for v in "${vs[@]}"; do
+        local lib=$PWD/gpurun_variants/$v/libmppi_amd.so D=$O/kpmc_$v
+        [ "$v" = tree ] && lib=$PWD/assistedmanipulation_amd/lib/libmppi_amd.so
+        mkdir -p $D
+        local B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline"
+        krun() {   # name counters...
+            local n=$1; shift
+            MPPI_AMD_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "weights|finish|rank_draw" \
+                -d $D -o $n --output-format csv -- $B > $D/$n.log 2>&1
+        }
+        krun sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU GRBM_GUI_ACTIVE && \
+        krun ta TA_BUSY_avr TA_TA_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum && \
+        krun fetch FETCH_SIZE && echo "kpmc $v ok" || return 1
+        for n in sq ta fetch; do python3 tools/pmc_summary.py $D/${n}_counter_collection.csv > $D/${n}_summary.txt; cat $D/${n}_summary.txt; done
+    done
+}
+
 step_sizes() {
     size() {   # name args...
         local n=$1; shift
@@ -165,6 +186,7 @@ for s in "$@"; do
         pmc) step_pmc ;;
         pmcpm) step_pmc pm ;;
         sizes) step_sizes ;;
+        kpmc) step_kpmc "$arg" ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;
         pmstamps) step_pmstamps "$arg" ;;
