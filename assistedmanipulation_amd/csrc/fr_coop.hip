@@ -327,7 +327,6 @@ __device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
     // s_nop 1: nt (a source of pivot 0's DPP FMAs) may be written right before the block
     asm("s_nop 1\n\t"
         /* pivot 0 */
-        "v_fmac_f64_dpp %1, %1, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %3, %18 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_mul_f64 %12, -%1, %19\n\t"
@@ -344,14 +343,13 @@ __device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
         "v_fmac_f64_dpp %3, %3, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %4, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b64_dpp %14, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %0, %0, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "v_rcp_f64 %15, %14\n\t"
         "v_fmac_f64_dpp %5, %5, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %15, %14\n\t"
         "v_fmac_f64_dpp %6, %6, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %7, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_mul_f64 %16, -%2, %15\n\t"
         "v_fma_f64 %17, -%14, %15, 1.0\n\t"
-        "v_fmac_f64_dpp %8, %8, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %9, %9, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %13, %16, %17, %16\n\t"
         "v_fmac_f64_dpp %10, %10, %12 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
