@@ -168,8 +168,6 @@ struct mppi_handle {
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [Rpad][H][FR_REC] and the filter() row's [H][FR_REC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
-    RelayXfer *d_relay = nullptr;   // the paired relay's hand-off (fr_coop.hip relay_stage), zeroed at create
-    int relay_token = 0;            // per rollout launch, nonzero (the hand-off's flags compare to it)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
     size_t inj_capacity = 0;   // doubles
@@ -975,7 +973,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
     CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_REC)));
-    CREATE_TRY(dalloc(h, &h->d_relay, (size_t)RELAY_GROUPS_MAX));
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
@@ -1647,10 +1644,6 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
         a.rec = h->d_rec;
-        // the paired relay's exchange and this launch's token (launch_fr_coop_update decides the pairing)
-        a.rx = h->d_relay;
-        if (++h->relay_token == 0) h->relay_token = 1;
-        a.rtoken = h->relay_token;
         // sharded: this rank's wait timeouts into cost slot R, which the all-reduce carries to every rank
         a.wait_sum = h->comm ? h->d_costs_local + h->R : (sharded(h) ? h->d_costs + h->R : nullptr);
         if (h->debug_updates > 0) {   // mppi_debug_inject: this update's launch carries the fault

@@ -1532,16 +1532,12 @@ __device__ __forceinline__ void wait_records(const FrRolloutArgs &a, int *flag)
     }
     if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
 }
-// The paired relay's wait across workgroups: until the token flag holds this launch's token.  The
-// producer stores its payload sc1 (agent-scope relaxed stores), waits for every one of them
-// (s_waitcnt 0), then stores the flag, one lane, sc1; this wave polls with sc1 loads and loads the
-// payload with sc1 loads after the match (MI355X_MICROARCH.md, inter-workgroup visibility: the
-// one-storing-wave form).  Bounded like the others; returns whether the token arrived.
-__device__ __forceinline__ int wait_token(const FrRolloutArgs &a, int *word)
+// the same bounded wait, returning the value it saw (0 if it gave up)
+__device__ __forceinline__ int wait_nonzero(const FrRolloutArgs &a, int *word)
 {
     for (int i = 0; i < WAIT_SPINS; i++) {
-        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.rtoken)
-            return 1;
+        const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v != 0) return v;
         __builtin_amdgcn_s_sleep(8);
     }
     if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
@@ -1612,45 +1608,16 @@ __device__ __forceinline__ int lds_read(int *w)
 {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
-// The relay group a workgroup holds rows of: q for workgroup q, and with the paired relay (a.rx)
-// for its partner q + RELAY_PAIR as well
-__device__ __forceinline__ int relay_group(const FrRolloutArgs &a)
-{
-    return (a.rx && (int)blockIdx.x >= RELAY_PAIR) ? (int)blockIdx.x - RELAY_PAIR : (int)blockIdx.x;
-}
 // first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4)
 __device__ __forceinline__ int64_t group_row0(const FrRolloutArgs &a, int g)
 {
-    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)relay_group(a) * ROWS_PER_WAVE;
+    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
 }
-// The chunks [c0, c1) of group g this workgroup evaluates: every chunk of a main wave's rows; of the
-// relay's rows, with the paired relay, the first half's in workgroup q and the second's in its
-// partner (the records stay in the workgroup that stored them: nothing but the sums crosses)
-__device__ __forceinline__ void group_chunks(const FrRolloutArgs &a, int g, int &c0, int &c1)
-{
-    const int nch = (a.H + CH - 1) / CH;
-    c0 = 0;
-    c1 = nch;
-    if (g == 4 && a.rx) {
-        const int split = (a.rsplit + 1) / CH;   // the first half's records are [0, rsplit] = chunks [0, split)
-        if ((int)blockIdx.x >= RELAY_PAIR) c0 = split;
-        else c1 = split;
-    }
-}
-__device__ __forceinline__ int relay_step(const FrRolloutArgs &a, int r, int H);
-// whether chunk c of group g can be read: its records are complete.  The relay's rows: once the
-// stages that store them have signalled the next (Lq[Q_STAGE], behind their s_waitcnt), so only the
-// chunks of the workgroup's last stage wait for the relay's flag.
+// whether chunk c of group g can be read: its records are complete
 __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
 {
+    if (g == 4) return lds_read(Lflag + LF_RELAY) != 0;
     const int last = min((c + 1) * CH, a.H) - 1;
-    if (g == 4) {
-        if (lds_read(Lflag + LF_RELAY) != 0) return true;
-        if (!a.handover) return false;
-        const int done = lds_read(Lq + Q_STAGE);   // stages of this workgroup done: records up to
-        const bool second = a.rx && (int)blockIdx.x >= RELAY_PAIR;   // relay_step(first stage + done) stored
-        return done > 0 && last <= relay_step(a, (second ? 4 : 0) + done, a.H);
-    }
     if (last < a.H - 1 && lds_read(Lq + Q_PROG + g) >= last + 3) return true;
     return lds_read(Lflag + g) != 0;
 }
@@ -1661,8 +1628,7 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
                                           int *Lq)
 {
     const int H = a.H;
-    int cb, ce;
-    group_chunks(a, g, cb, ce);   // the group's chunks in this workgroup
+    const int nch = (H + CH - 1) / CH;   // the group's chunks
     const int i = lane >> 4, k = c * CH + (lane & 15);
     const int64_t lr0 = group_row0(a, g), lr = lr0 + i;
     const bool rl = row_live(a, lr), live = rl && k < H;
@@ -1676,29 +1642,13 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     // the stores before the count: the wave that completes the group reads every chunk's costs
     const int n = __builtin_amdgcn_readfirstlane(
         __hip_atomic_fetch_add(Lq + Q_DONE + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (n + 1 != ce - cb) return;
-    const int kb = cb * CH, ke = min(ce * CH, H);
-    const bool first_half = g == 4 && a.rx && ke < H;    // paired relay, workgroup q: hand the sums on
-    const bool second_half = g == 4 && a.rx && kb > 0;   // its partner: continue from them
-    RelayXfer *x = second_half || first_half ? a.rx + relay_group(a) : nullptr;
-    double J = 0.0;
-    if (second_half) {   // the first half's sums (bounded wait; on a timeout the update fails)
-        const int tok = wait_token(a, &x->sums_tok);
-        J = (lane < ROWS_PER_WAVE && tok) ? __hip_atomic_load(x->sums + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    }
-    if (lane < ROWS_PER_WAVE) {
-        const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
-        for (int q = kb; q < ke; q++) J += cr[q];   // the reference's J += cost, in step order
-    }
-    if (first_half) {   // the partner adds the second half's step costs to these, in step order
-        if (lane < ROWS_PER_WAVE) __hip_atomic_store(x->sums + lane, J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        if (lane == 0) __hip_atomic_store(&x->sums_tok, a.rtoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
+    if (n + 1 != nch) return;
     if (lane < ROWS_PER_WAVE) {
         const int64_t r = lr0 + lane;
         if (row_live(a, r)) {
+            const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
+            double J = 0.0;
+            for (int q = 0; q < H; q++) J += cr[q];
             J = isnan(J) ? (double)NAN : J;
             if (a.fcost != nullptr && r == a.count) {
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
@@ -1717,14 +1667,13 @@ template <int CK, bool EN>
 __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int ng, int lane, const double *Lmodel,
                                          double *Lcs, int *Lflag, int *Lq)
 {
+    const int nch = (a.H + CH - 1) / CH;
 #pragma unroll 1
     for (int spin = 0; spin < WAIT_SPINS; spin++) {
         bool left = false, did = false;
 #pragma unroll 1
         for (int d = 0; d < ng && !did; d++) {
             const int g = first + d < ng ? first + d : first + d - ng;
-            int cb, nch;
-            group_chunks(a, g, cb, nch);   // (Lq[Q_NEXT + g] starts at cb)
             const int c0 = lds_read(Lq + Q_NEXT + g);
             if (c0 >= nch) continue;
             left = true;
@@ -1768,85 +1717,60 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// Relay stage r's steps [relay_step(r), relay_step(r + 1)): four quarters of the H - 1 loop steps,
-// or with the paired relay (a.rx) eight stages, 0..3 over [0, rsplit) and 4..7 over [rsplit, H - 1)
-__device__ __forceinline__ int relay_step(const FrRolloutArgs &a, int r, int H)
-{
-    if (!a.rx) return r >= 4 ? H - 1 : (r * (H - 1)) / 4;
-    if (r >= 8) return H - 1;
-    return r < 4 ? (r * a.rsplit) / 4 : a.rsplit + ((r - 4) * (H - 1 - a.rsplit)) / 4;
-}
+// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
+__device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
 
-// Relay stage s (wave 4 + s) of a workgroup with rows left over (a.handover): makes the next
-// update's draws for main wave s's rows (s > 0 in workgroup q; wave 0's are left to
-// rank_draw_kernel, as the engine expects of the first wave of these workgroups), waits for stage
-// s - 1 (Lq[Q_STAGE] == s), runs its part of the horizon at priority 3 and passes the state on; the
-// last stage raises the relay's records flag.  With the paired relay the workgroup q + RELAY_PAIR
-// (second) runs stages 4..7: its stage 4 takes the state stage 3 of workgroup q leaves in rx[q], and
-// each workgroup evaluates its own half of the relay rows' chunks (group_chunks).  Each SIMD of the
-// two workgroups then carries an eighth of the extra wave instead of a quarter; the relay's loop is
-// the same code, only the hand-off crosses.  (Round 4's attempt, RELAY2, changed the loop itself and
-// slowed every stage.)  Without a.handover wave 4 runs every step itself at the main waves'
-// priority.  Returns whether the stage ran (false: the previous stage never signalled, counted in
-// Status::wait_timeouts).
+// Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): makes the next
+// update's draws for main wave r's rows (r > 0; wave 0's are left to rank_draw_kernel, as the
+// engine expects of the first wave of these workgroups), waits for stage r - 1 (Lq[Q_STAGE] == r),
+// runs its quarter of the horizon at priority 3 and passes the state on; the last stage raises the
+// relay's records flag.  Without a.handover wave 4 runs every step itself at the main waves'
+// priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage ran (false: the
+// previous stage never signalled, counted in Status::wait_timeouts).
 template <int CK, bool EN>
-__device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, bool second, int lane, double *Lk, double *Lw,
+__device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
                                             const double *Lmodel, const double *Lx0, int *Lflag, int *Lq, double *Lst)
 {
     const int H = a.H;
-    const int q = relay_group(a);
-    const int64_t xlr = a.xbase + (int64_t)q * ROWS_PER_WAVE + (lane >> 4);
+    const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
     const int wblk = gridDim.x * 4 + blockIdx.x;
-    const int r = second ? 4 + s : s;   // the stage
     int kb = 0, ke = 0x7FFFFFFF;   // without a.handover: every step on this wave (one stage)
     if (a.handover) {
-        // the next update's draws for main wave s's rows first (workgroup q's wave 0 rows are left
-        // to rank_draw_kernel; the partner's are drawn here like any other workgroup's)
-        if ((s > 0 || second) && a.ahead_noise) group_draws(a, s, lane, Lflag);
-        if (s > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
+        // the next update's draws for main wave r's rows first (block 0's wave 0 rows are left to
+        // rank_draw_kernel)
+        if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
+        if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
             int st = 0;
-            for (int i = 0; i < (1 << 22) && st < s; i++) {
+            for (int i = 0; i < (1 << 22) && st < r; i++) {
                 st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (st < s) __builtin_amdgcn_s_sleep(2);
+                if (st < r) __builtin_amdgcn_s_sleep(2);
             }
-            if (st < s) {
+            if (st < r) {
                 if (lane == 0) note_wait_timeout(a);
                 return false;
             }
-        } else if (second) {   // stage 4: the lanes' state from workgroup q (sc1 loads), into Lst
-            if (!wait_token(a, &a.rx[q].state_tok)) return false;
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                Lst[3 * lane + c] = __hip_atomic_load(a.rx[q].state + 3 * lane + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __builtin_amdgcn_s_setprio(3);   // above the main waves (1) and the objective's (0)
-        kb = relay_step(a, r, H);
-        ke = relay_step(a, r + 1, H);
+        kb = relay_step(r, H);
+        ke = relay_step(r + 1, H);
     }
     // one call site: one copy of the step loop for both shapes
     coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke);
     if (a.handover) {
         __builtin_amdgcn_s_setprio(0);
-#ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0; the first half when paired)
+#ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
         if (a.trace && blockIdx.x == 0 && lane == 0 && r < 4) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (s < 3) {   // the state in Lst (and this stage's records) before the next stage starts
+        if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
             // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
             if (!((a.debug & 1) && r == 1))
-                __hip_atomic_store(Lq + Q_STAGE, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(Lq + Q_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             return true;
         }
-        if (a.rx && !second) {   // stage 3 of workgroup q: the state to the partner (sc1), then the token
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                __hip_atomic_store(a.rx[q].state + 3 * lane + c, Lst[3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_s_waitcnt(0);
-            if (lane == 0) __hip_atomic_store(&a.rx[q].state_tok, a.rtoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
-    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(a, 1, H) : -1;
-    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);   // this workgroup's relay records are stored
+    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(1, H) : -1;
+    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
     return true;
 }
 
@@ -1982,24 +1906,16 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
-    // workgroups with relay rows: q < nxb (stages 0..3), and with the paired relay q + RELAY_PAIR
-    // (stages 4..7, `second`)
-    const int nxb = (int)((a.xrows + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
-    const bool xr = (int)blockIdx.x < nxb;
-    const bool second = a.rx != nullptr && (int)blockIdx.x >= RELAY_PAIR && (int)blockIdx.x < RELAY_PAIR + nxb;
     const int64_t lr = wv < 4 ? (int64_t)(blockIdx.x * 4 + wv) * ROWS_PER_WAVE + rowi
-                              : a.xbase + (int64_t)relay_group(a) * ROWS_PER_WAVE + rowi;   // this lane's row (waves < 5)
-    const int rk = (wv < 4 || (wv == 4 && xr)) ? kept_rank(a, lr) : 0x7FFFFFFF;
+                              : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row (waves < 5)
+    const int rk = wv < 5 ? kept_rank(a, lr) : 0x7FFFFFFF;
     stage_body_table(a, Lmodel, 64 * XW);
     stage_x0(a, Lx0);
     if (threadIdx.x < LF_N) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < Q_N) Lq[threadIdx.x] = threadIdx.x < Q_NEXT ? -1 : 0;
-    const int ng = (xr || second) ? 5 : 4;   // row groups of the objective
-    if (threadIdx.x == Q_NEXT + 4) {   // the relay group's first chunk here (none: past every chunk)
-        int cb, ce;
-        group_chunks(a, 4, cb, ce);
-        Lq[Q_NEXT + 4] = (xr || second) ? cb : 0x7FFF;
-    }
+    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
+    const int ng = xr ? 5 : 4;   // row groups of the objective
+    if (!xr && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
     __syncthreads();
     // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
     const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
@@ -2028,8 +1944,8 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
     } else {
         const int s = wv - 4;   // this wave's SIMD
-        const bool relay = (xr || second) && (s == 0 || a.handover);
-        if (relay) relay_stage<CK, EN>(a, s, second, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
+        const bool relay = xr && (s == 0 || a.handover);
+        if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
         if (!cil) return;
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
@@ -2166,26 +2082,6 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
 }
 
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
-// The paired relay (relay_stage) for a launch of `groups` workgroups with xrows rows left over:
-// when the engine gave an exchange buffer, the stages hand over (a.handover), every relay group has
-// a partner workgroup in the grid, and the horizon splits at a chunk boundary with at least four
-// steps per stage on either side; else a.rx = null and the relay stays in one workgroup.
-static void pair_relay(FrRolloutArgs &a, int64_t groups, int64_t xrows)
-{
-    const int64_t nxb = (xrows + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
-    const int H = a.H, nch1 = (H + CH) / (2 * CH);   // the first half's chunks: about half the horizon
-    const int rsplit = nch1 * CH - 1;
-    const bool ok = a.rx != nullptr && a.handover && nxb > 0 && nxb <= RELAY_GROUPS_MAX && groups >= nxb + RELAY_PAIR &&
-                    nch1 >= 1 && rsplit >= 4 && H - 1 - rsplit >= 4;
-#ifdef AB_NO_PAIR   // (temporary A/B build)
-    const bool use = false && ok;
-#else
-    const bool use = ok;
-#endif
-    if (!use) a.rx = nullptr;
-    a.rsplit = use ? rsplit : 0;
-}
-
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry,
                                  CoopTail *tail, FrRolloutArgs *final2)
@@ -2206,13 +2102,11 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
         A.fcost = nullptr;   // the previous filter() rides with the rows left over
         A.xbase = n0;
         A.xrows = 0;
-        A.rx = nullptr;
         const int64_t gb = rest / WG_ROWS, xb = rest - gb * WG_ROWS;
         const bool frow = a0.fcost != nullptr;
         if (!frow) B.fcost = nullptr;
         B.xbase = gb * WG_ROWS;
         B.xrows = xb + (frow ? 1 : 0);
-        pair_relay(B, gb, B.xrows);
         *folded = frow;
         *costs_done = a.costs_in_launch != 0;
         *tail_drawn = a.ahead_noise != nullptr;
@@ -2237,7 +2131,6 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
         if (a.drawn_ahead) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
-        a.rx = nullptr;
         a.costs_in_launch = groups > 0 && !env.costs_in_launch_off ? 1 : 0;   // each wave its own rows'
         *costs_done = a.costs_in_launch != 0;
         if (final) *final = a;
@@ -2253,7 +2146,6 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
     *folded = frow;
     a.costs_in_launch = !env.costs_in_launch_off && a.H <= HC_MAX ? 1 : 0;   // Lcs holds HC_MAX steps
     a.handover = env.handover_off ? 0 : 1;
-    pair_relay(a, groups, xrows);
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
     if (xrows == 0 || !a.costs_in_launch || !a.drawn_ahead) a.ahead_noise = nullptr;

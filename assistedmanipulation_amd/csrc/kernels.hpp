@@ -114,17 +114,6 @@ struct FinishArgs {
     double *wait_local;
 };
 
-// The paired relay's hand-off per relay group (fr_coop.hip relay_stage): the lanes' (q, qd, E) at
-// step rsplit and the relay rows' step-cost sums over the first half, each published by a token
-// flag (the launch's rtoken) behind its sc1 stores
-struct RelayXfer {
-    int state_tok, sums_tok, pad[2];
-    double state[64 * 3];
-    double sums[4];
-};
-constexpr int RELAY_PAIR = 8;         // relay group q's partner workgroup: q + RELAY_PAIR
-constexpr int RELAY_GROUPS_MAX = 8;   // relay groups a launch may pair (rows left over <= 32)
-
 struct FrRolloutArgs {
     const DevModel *model;
     const DevCost *cost;
@@ -177,11 +166,6 @@ struct FrRolloutArgs {
     // MPPI_DEBUG_* fault injection (mppi_debug_inject; 0 in production): bit 0, relay stage 1 of
     // the workgroup with rows left over never signals stage 2 (tests the wait-timeout failure)
     int debug;
-    // the relay paired over two workgroups (fr_coop.hip relay_stage): relay group q runs stages 0..3
-    // over steps [0, rsplit) in workgroup q and stages 4..7 over [rsplit, H - 1) in workgroup
-    // q + RELAY_PAIR, the hand-off through rx[q] under this launch's token; rx null: one workgroup
-    RelayXfer *rx;
-    int rtoken, rsplit;
 };
 
 // What the objective reads at (step k, rollout): the state x_k the cost is evaluated at and the

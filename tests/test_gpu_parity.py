@@ -393,12 +393,11 @@ def test_draws_ahead_match_sampling_at_update(rollouts, objective, monkeypatch):
 @pytest.mark.parametrize("rollouts,objective", [(4096, "am"), (4096, "energy"), (4096, "track_point"), (1000, "am"),
                                                 (4097, "am")])
 def test_handover_equals_doubled_simd(rollouts, objective, monkeypatch):
-    """The relay (fr_coop.hip relay_stage): the fifth wave's rows travel through relay stages, each
-    resuming from the (q, qd, E) the previous stage left at the top of a step; since round 5 the
-    stages are paired over two workgroups (q and q + 8: stages 0..3 over steps [0, 31), 4..7 over
-    [31, 63), the state and the first half's cost sums handed over once).  Every output equals the
-    launch that keeps the rows on one doubled SIMD (MPPI_HANDOVER=0), bit for bit, over updates with
-    kept rollouts and shifts; 1000 rollouts have relay rows in three workgroups, 4097 two."""
+    """take_over (fr_coop.hip): the fifth wave's rows move, mid-horizon, to the first of waves 1..3
+    to end its own rows, off the SIMD the fifth wave shares with wave 0.  The moved rows resume from
+    the (q, qd, E) the fifth wave left at the top of a step, so every output equals the launch that
+    keeps them on the doubled SIMD (MPPI_HANDOVER=0), bit for bit, over updates with kept rollouts
+    and shifts; 1000 rollouts have fifth waves in three workgroups, 4097 four leftover rows."""
     conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=0.64, keep_best_rollouts=20, threads=8)
     times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
     make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
@@ -421,7 +420,7 @@ def test_handover_equals_doubled_simd(rollouts, objective, monkeypatch):
             rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
         out[ho] = rec + [(np.float64(t.get_optimal_total_cost()),) * 4]   # the folded filter() rows
     print("handover steps:", steps)
-    assert all(k == 31 // 4 for k in steps), steps   # the paired relay's first stage: [0, 7) (one workgroup: 15)
+    assert all(0 < k < 63 for k in steps), steps
     for j, (a, b) in enumerate(zip(out["0"], out["1"])):
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
