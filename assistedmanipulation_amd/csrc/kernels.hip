@@ -30,6 +30,7 @@
 #include "device_common.hpp"
 #include "engine_types.hpp"
 #include "kernels.hpp"
+#include "pm_model.hpp"
 #include "sample_device.hpp"
 
 using namespace mppi_eng;
@@ -320,23 +321,18 @@ __device__ __forceinline__ void pm_steps(const PmRolloutArgs &a, const DevPointM
 #pragma unroll
     for (int j = 0; j < PM_PF; j++) {
         if (k0 + j >= a.H || !alive) return;
-        double u[3];
+        double u[3], dv[3], cu;
+#pragma unroll
         for (int c = 0; c < 3; c++) u[c] = b.u[j][c] + b.e[j][c];
-        double cost = 0.0;
-        for (int i = 0; i < 3; i++) {
-            const double d = x[i] - P.target[i];
-            cost += P.q[i] * (d * d);
-        }
-        for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
-        const double sc = b.gm[j] * cost;
+        pm_control_step(P, u, a.dt, dv, cu);   // pm_model.hpp: the fused launch's operations
+        double Jn = J;
+        const double sc = pm_state_step(P, x, dv, cu, b.gm[j], a.dt, Jn);
         if (!a.optimal && isnan(sc)) {
             J = NAN;
             alive = false;
             return;
         }
-        J += sc;
-        for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
-        for (int i = 0; i < 3; i++) x[i] = x[i] + x[3 + i] * a.dt;
+        J = Jn;
     }
 }
 __global__ __launch_bounds__(256) void pm_rollout_kernel(PmRolloutArgs a)

@@ -41,6 +41,7 @@
 #include "device_common.hpp"
 #include "engine_types.hpp"
 #include "kernels.hpp"
+#include "pm_model.hpp"
 #include "sample_device.hpp"
 
 using namespace mppi_eng;
@@ -66,10 +67,12 @@ __device__ __forceinline__ uint64_t rank_key(double c)
     return isnan(c) ? ~0ull : mppi_dev::cost_order_key(c);
 }
 
-// the doubles of the eps rows [PR][H C + 1], which the finisher reuses for every block's partials
+// the doubles of the eps rows [PR][H C + 1] and the rollouts' control part [H][PR][4] behind them
+// (pm_rollout_pre), which the finisher reuses for every block's partials once the rollouts are done
 __host__ __device__ inline int64_t pm_region(int PR, int HC, int64_t nb)
 {
-    const int64_t e = (int64_t)PR * (HC + 1), p = nb * HC + nb;
+    const int H = HC / PC;
+    const int64_t e = (int64_t)PR * (HC + 1) + 4 * (int64_t)PR * H, p = nb * HC + nb;
     return e > p ? e : p;
 }
 
@@ -87,11 +90,13 @@ __device__ __forceinline__ void philox_eps(const PmFusedArgs &a, int64_t g, int 
     for (int c = 0; c < PC; c++) e[c] = a.tdv[c] * (double)z[c];
 }
 
-// pm_rollout_kernel's horizon (kernels.hip pm_steps), the same operations in the same order; eps
-// row k at eps[k * PC] (unused when optimal).  No branch per step: a NaN step cost leaves J NaN
-// to the end, which is the reference's NaN rollout cost (mppi.cpp:331-334); the states it
-// integrates past that point are never read.  (A step cost of +inf followed by -inf, which the
-// reference would sum to NaN and not stop on, is NaN here as well.)
+// pm_rollout_kernel's horizon (kernels.hip pm_steps): pm_model.hpp's control and state parts in the
+// same order, so the costs are bit-identical to the five-launch path; eps row k at eps[k * PC]
+// (unused when optimal).  No branch per step: a NaN step cost leaves J NaN to the end, which is the
+// reference's NaN rollout cost (mppi.cpp:331-334); the states it integrates past that point are
+// never read.  (A step cost of +inf followed by -inf, which the reference would sum to NaN and not
+// stop on, is NaN here as well.)  The update's rollouts take the control part from the block's
+// precomputed table (pm_rollout_pre); this form runs the folded filter() row.
 __device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double *x0, const double *Lus, const double *Lgm,
                                              const double *eps, bool optimal)
 {
@@ -102,26 +107,32 @@ __device__ __forceinline__ double pm_rollout(const PmFusedArgs &a, const double 
     double J = 0.0;
 #pragma unroll 4
     for (int k = 0; k < a.H; k++) {
-        double u[3];
+        double u[3], dv[3], cu;
 #pragma unroll
         for (int c = 0; c < 3; c++) u[c] = Lus[k * PC + c] + (optimal ? 0.0 : eps[k * PC + c]);
-        double cost = 0.0;
+        pm_control_step(P, u, a.dt, dv, cu);
+        pm_state_step(P, x, dv, cu, Lgm[k], a.dt, J);
+    }
+    return J;
+}
+
+// The rollout of lane l through the horizon, its control part read from Lpre [H][PR][4] (dv0, dv1,
+// dv2, cu per step, formed by the whole block in parallel): 18 fp64 operations per step on the chain
+template <int PR>
+__device__ __forceinline__ double pm_rollout_pre(const PmFusedArgs &a, const double *x0, const double *Lgm, const double *Lpre,
+                                                 int l)
+{
+    const DevPointMass &P = a.pm;
+    double x[6];
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const double d = x[i] - P.target[i];
-            cost += P.q[i] * (d * d);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; i++) cost += P.r[i] * (u[i] * u[i]);
-        const double sc = Lgm[k] * cost;
-        {
-#pragma clang fp contract(off)
-            J += sc;   // an add of the rounded product, as pm_rollout_kernel's (no fma)
-        }
-#pragma unroll
-        for (int i = 0; i < 3; i++) x[3 + i] = x[3 + i] + (u[i] * P.inv_mass) * a.dt;
-#pragma unroll
-        for (int i = 0; i < 3; i++) x[i] = x[i] + x[3 + i] * a.dt;
+    for (int i = 0; i < 6; i++) x[i] = x0[i];
+    double J = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < a.H; k++) {
+        const double2 p01 = *reinterpret_cast<const double2 *>(Lpre + (k * PR + l) * 4);
+        const double2 p23 = *reinterpret_cast<const double2 *>(Lpre + (k * PR + l) * 4 + 2);
+        const double dv[3] = {p01.x, p01.y, p23.x};
+        pm_state_step(P, x, dv, p23.y, Lgm[k], a.dt, J);
     }
     return J;
 }
@@ -165,6 +176,10 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     int *Lcnt = reinterpret_cast<int *>(Leps + pm_region(PR, HC, nb));
     // the previous update's U* [HC] and state [6] for the folded filter()
     double *LUf = reinterpret_cast<double *>(Lcnt + (QD - 1) * PR);
+    // the rollouts' control part per step, [H][PR][4] (pm_rollout_pre), behind the eps rows in the
+    // finisher's staging region (free until the rollouts are done; PR ES is even, so 16-byte aligned
+    // as Leps is)
+    double *Lpre = Leps + PR * ES;
     __shared__ int s_last;
     const int64_t r0 = (int64_t)b * PR;
     const SampleParams &P = a.sp;
@@ -266,13 +281,26 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     if (fold && t < 6) LUf[HC + t] = fx;
     __syncthreads();
     stamp(1);
+    // the control part of every (rollout, step) of the block, by all its threads (pm_model.hpp)
+    for (int it = t; it < PR * H; it += PT) {
+        const int k = it / PR, r = it - k * PR;
+        double u[3], dv[3], cu;
+#pragma unroll
+        for (int c = 0; c < 3; c++) u[c] = Lus[k * PC + c] + Leps[r * ES + k * PC + c];
+        pm_control_step(a.pm, u, a.dt, dv, cu);
+        double *o = Lpre + (k * PR + r) * 4;
+        *reinterpret_cast<double2 *>(o) = double2{dv[0], dv[1]};
+        *reinterpret_cast<double2 *>(o + 2) = double2{dv[2], cu};
+    }
+    __syncthreads();
     const int64_t gr = r0 + l;   // the rollout wave's lane l
     const bool mine = w == 0 && l < PR && gr < a.R;
     double J = NAN;
-    // rollouts (mppi.cpp:272-342): one lane per rollout through the horizon.  (Splitting the state
-    // chain from the step costs - the positions through LDS, the costs by all threads - measured
-    // slower: 28.7 against 27.6 us per update, profiles/r04/pm_split_ab/.)
-    if (mine) J = pm_rollout(a, a.x0v, Lus, Lgm, Leps + l * ES, false);
+    // rollouts (mppi.cpp:272-342): one lane per rollout through the horizon, the state part only.
+    // (Round 4 split the state chain from the step costs - the positions through LDS, the costs by
+    // all threads - and measured it slower: 28.7 against 27.6 us per update, profiles/r04/pm_split_ab/;
+    // the control part needs no state, so here it is formed before the chain instead.)
+    if (mine) J = pm_rollout_pre<PR>(a, a.x0v, Lgm, Lpre, l);
     stamp(11);
     if (w == 0) {
         if (mine) st_sc1(a.cost + gr, J);   // read by every block's rank (tail)

@@ -51,7 +51,8 @@ def test_fused_update_equals_five_launches(S, horison, monkeypatch):
         # rollout 1 = -U*, which the two paths round differently (the gradient's summation order)
         np.testing.assert_allclose(a[0][1], b[0][1], rtol=0, atol=1e-12, err_msg="update %d noise" % j)
         if j == 0:   # the same nominal (zeros): the same arithmetic on the same operands
-            np.testing.assert_array_equal(a[1], b[1], err_msg="update %d costs" % j)
+            np.testing.assert_array_equal(a[1], b[1], err_msg="update %d costs, rollouts %s differ" %
+                                          (j, np.flatnonzero(a[1] != b[1])[:8]))
         else:   # every rollout rides the shifted U*, which carries the gradient's rounding
             np.testing.assert_allclose(a[1], b[1], rtol=1e-13, atol=0, err_msg="update %d costs" % j)
         # exp(-s (c - min) / (max - min)) carries the costs' rounding, scaled by s (c - min) / (max - min)
