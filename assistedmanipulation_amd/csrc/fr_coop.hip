@@ -1688,7 +1688,18 @@ __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int
                 w++;
             }
             if (w == WAIT_SPINS && lane == 0) note_wait_timeout(a);
+#ifdef COST_TRACE   // block 0's chunks: start, end, wave (slots past the relay's)
+            const uint32_t tc0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
             cost_chunk<CK, EN>(a, g, c, lane, Lmodel, Lcs, Lq);
+#ifdef COST_TRACE
+            if (a.trace && blockIdx.x == 0 && lane == 0 && c < 4) {
+                uint32_t *tr = a.trace + 4 * (gridDim.x * 4 + 16 + 4 * g + c);
+                tr[0] = tc0;
+                tr[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                tr[2] = threadIdx.x >> 6;
+            }
+#endif
             did = true;
         }
         if (!left) return;

@@ -153,6 +153,32 @@ __device__ __forceinline__ double sum_in_order(const double *p, int n, int s)
     return acc;
 }
 
+// p[0] + p[ps] + ... and q[0] + q[qs] + ..., n terms each from 0.0 in index order: the two chains
+// interleaved, sixteen reads of each in flight at a time
+__device__ __forceinline__ void sum2_in_order(const double *p, int ps, const double *q, int qs, int n, double &a, double &b)
+{
+    a = 0.0;
+    b = 0.0;
+    int i = 0;
+    for (; i + 16 <= n; i += 16) {
+        double v[16], w[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            v[u] = p[(i + u) * ps];
+            w[u] = q[(i + u) * qs];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            a += v[u];
+            b += w[u];
+        }
+    }
+    for (; i < n; i++) {
+        a += p[i * ps];
+        b += q[i * qs];
+    }
+}
+
 }  // namespace
 
 // LDS (doubles): U*_shifted [H C], gamma [H], the block's costs [PR] and e_r [PR], the rank's keys
@@ -181,8 +207,56 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     // as Leps is)
     double *Lpre = Leps + PR * ES;
     __shared__ int s_last;
+    __shared__ double s_mb[8];   // the armed launch's state and shift (mailbox words 0..7)
+    __shared__ int s_go;
+    if (a.mbox) {   // armed (update_pm_fused): wait for the update's mailbox, or its cancel (bounded)
+        // Block 0 alone polls the host's mailbox (one reader on the host's line) and relays its
+        // words to the other blocks through device memory: the payload, then the flag, sc1.
+        if (w == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            int go = -1;
+            uint64_t v = 0;
+            if (b == 0) {
+                while (go < 0) {
+                    v = l < 10 ? __hip_atomic_load(a.mbox + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+                    uint64_t wd[10];
+#pragma unroll
+                    for (int i = 0; i < 10; i++)
+                        wd[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+                    if (wd[8] == a.mseq && wd[9] == pm_mbox_sum(wd, a.mseq)) go = 1;
+                    else if (wd[8] == (a.mseq | PM_MBOX_CANCEL) || __builtin_amdgcn_s_memrealtime() - t0 > PM_ARM_TIMEOUT_TICKS)
+                        go = 0;
+                    else __builtin_amdgcn_s_sleep(1);
+                }
+                if (go == 1 && l < 8) __hip_atomic_store(a.mrelay + l, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_waitcnt(0);
+                if (l == 0) __hip_atomic_store(a.mrelay + 8, go == 1 ? a.mseq : (a.mseq | PM_MBOX_CANCEL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                while (go < 0) {
+                    const uint64_t f = __hip_atomic_load(a.mrelay + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (f == a.mseq) go = 1;
+                    else if (f == (a.mseq | PM_MBOX_CANCEL) || __builtin_amdgcn_s_memrealtime() - t0 > PM_ARM_TIMEOUT_TICKS + 10000000ull)
+                        go = 0;
+                    else __builtin_amdgcn_s_sleep(1);
+                }
+                if (go == 1 && l < 8) v = __hip_atomic_load(a.mrelay + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (go == 1 && l < 8) s_mb[l] = __longlong_as_double((long long)v);
+            if (l == 0) s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;   // cancelled: nothing read or written
+    } else if (t < 8) {
+        s_mb[t] = a.x0v[t];   // (the state read through LDS either way: one address space)
+    }
+    const double *x0v = s_mb;
+    SampleParams P = a.sp;
+    if (a.mbox) {
+        P.shift_by = (int64_t)__double_as_longlong(s_mb[6]);
+        P.shifted = P.shift_by > 0 ? (P.shift_by < a.H ? a.H - P.shift_by : 0) : a.H;
+    }
     const int64_t r0 = (int64_t)b * PR;
-    const SampleParams &P = a.sp;
     const double *Uprev = a.U;   // U* as the previous update published it
     const unsigned target = a.epoch * (unsigned)nb;
     auto stamp = [&](int i) {   // diagnostics: one clock stamp per block and phase
@@ -270,7 +344,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     for (int i = t + PT; i < HC; i += PT) Lus[i] = us_at(i);
     if (t < H) Lgm[t] = gm_t;
     for (int k = t + PT; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
-    if (b == 0 && t < a.X) a.x0_out[t] = a.x0v[t];
+    if (b == 0 && t < a.X) a.x0_out[t] = x0v[t];
     // the previous update's filter() (mppi.cpp:450-479), which its launch left pending, runs in this
     // block's tail: its inputs are taken now, before this launch's finisher rewrites them - the U*
     // it published, its state (x0_opt) and whether it threw (then no filter)
@@ -300,7 +374,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     // (Round 4 split the state chain from the step costs - the positions through LDS, the costs by
     // all threads - and measured it slower: 28.7 against 27.6 us per update, profiles/r04/pm_split_ab/;
     // the control part needs no state, so here it is formed before the chain instead.)
-    if (mine) J = pm_rollout_pre<PR>(a, a.x0v, Lgm, Lpre, l);
+    if (mine) J = pm_rollout_pre<PR>(a, x0v, Lgm, Lpre, l);
     stamp(11);
     if (w == 0) {
         if (mine) st_sc1(a.cost + gr, J);   // read by every block's rank (tail)
@@ -405,12 +479,15 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     if (s_last) {
         Status *st = a.status;
         const bool upd = !early && !wt, ok = !all_nan && !wt;
-        const double total = upd ? sum_in_order(Lst + G, nb, 1) : 0.0;
+        // the normaliser (every thread, for its outputs and the status words) beside the first
+        // output's gradient sum: two independent chains, each in block order
+        double total = 0.0, g0 = 0.0;
+        if (upd) sum2_in_order(Lst + G, 1, Lst + min(t, HC - 1), HC, nb, total, g0);
         for (int o = t; o < HC; o += PT) {   // finish (mppi.cpp:421-447) and publish (178-182)
             const int c = o % PC;
             double u = Lus[o];
             if (upd) {
-                const double gs = sum_in_order(Lst + o, nb, HC) / total;   // sum_r e_r eps_r / sum_r e_r
+                const double gs = (o == t ? g0 : sum_in_order(Lst + o, nb, HC)) / total;   // sum_r e_r eps_r / sum_r e_r
                 a.gradient[o] = gs;
                 u += gs * a.gradient_step;
                 if (a.control_bound) u = smax(smin(u, a.cmax[c]), a.cmin[c]);
@@ -421,7 +498,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             if (ok) a.U[o] = v;
             pub(a.out + o, v);
         }
-        if (t < a.X) a.x0_opt[t] = a.x0v[t];
+        if (t < a.X) a.x0_opt[t] = x0v[t];
         if (t == 0) {
             st->all_nan = all_nan;
             st->early = early;

@@ -23,3 +23,10 @@ print("fifth wave rows: start %.1f end %.1f" % (us(fx[0]), us(fx[1])))
 print("launch end (last wave end) %.1f us" % max(us(we).max(), us(fx[1])))
 if len(sys.argv) > 3 and sys.argv[3] == "relay":   # relay builds: block 0's stage ends in the next slot
     print("relay stage ends:", ["%.1f" % us(x) for x in rec[nmain + 1]])
+if len(sys.argv) > 3 and ns >= 1024 + 16 + 20:   # COST_TRACE builds: block 0's chunks (start, end, wave), group-major
+    for g in range(5):
+        row = []
+        for c in range(4):
+            s0, s1, wv, _ = rec[nmain + 16 + 4 * g + c]
+            row.append("%.1f-%.1f w%d" % (us(s0), us(s1), wv) if s0 else "-")
+        print("block 0 group %d chunks:" % g, "  ".join(row))
