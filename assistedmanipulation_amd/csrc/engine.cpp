@@ -43,7 +43,6 @@ EnvSwitches env_switches_read()
     e.handover_off = is("MPPI_HANDOVER", '0');
     e.split_off = is("MPPI_SPLIT", '0');
     e.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
-    e.pm_arm_off = is("MPPI_PM_ARM", '0');
     return e;
 }
 }  // namespace mppi_eng
@@ -219,15 +218,6 @@ struct mppi_handle {
     uint64_t *d_pm_stamps = nullptr;   // MPPI_PM_STAMPS=1: the launch's phase stamps per block
     std::vector<double> pm_stamp_sum; // their per-phase sums (us after the block's entry), printed at destroy
     int64_t pm_stamp_n = 0;
-    // the armed launch (pm_arm): the next update's pm_update_kernel queued behind this one, waiting
-    // at entry for the mapped mailbox [PM_MBOX_WORDS]
-    uint64_t *h_mbox = nullptr, *h_mbox_dev = nullptr;
-    uint64_t *d_mrelay = nullptr;  // [16] the launch's device relay of the mailbox (block 0 to the others)
-    bool pm_armed = false;
-    PmFusedArgs pm_armed_args{};   // its arguments (x0v and the shift unused: they come by the mailbox)
-    std::chrono::steady_clock::time_point pm_armed_at;
-    uint64_t mbox_seq = 0;         // the last mailbox sequence armed
-    int64_t pm_armed_used = 0, pm_armed_cancelled = 0;   // diagnostics (mppi_update_info)
     // per-update phase state
     bool phase_open = false;
     std::chrono::steady_clock::time_point t_start;
@@ -243,19 +233,6 @@ mppi_status fail(mppi_handle *h, mppi_status st, const std::string &msg)
     if (h) h->err = msg;
     else g_last_error = msg;
     return st;
-}
-
-// The armed point-mass launch (update_pm_fused) is released by its cancel: its blocks return at
-// entry, so whatever is queued behind it runs at once.  Every entry point that queues work on the
-// engine's streams, waits for them or reads device memory calls this first; only the update that
-// takes the armed launch, and calls that touch host state alone, do not.
-void pm_disarm(mppi_handle *h)
-{
-    if (!h || !h->pm_armed) return;
-    volatile uint64_t *m = h->h_mbox;
-    m[8] = h->mbox_seq | PM_MBOX_CANCEL;
-    h->pm_armed = false;
-    h->pm_armed_cancelled++;
 }
 
 #define HIP_TRY(expr)                                                                                          \
@@ -1016,11 +993,6 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipHostGetDevicePointer((void **)&h->h_out_dev, h->h_out, 0));
     std::memset(h->h_out, 0, (HC + 8) * sizeof(double));   // the publish flag starts below every sequence
     CREATE_TRY(hipHostMalloc((void **)&h->h_opt, 8 * sizeof(double), hipHostMallocDefault));
-    CREATE_TRY(hipHostMalloc((void **)&h->h_mbox, PM_MBOX_WORDS * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
-    CREATE_TRY(hipHostGetDevicePointer((void **)&h->h_mbox_dev, h->h_mbox, 0));
-    std::memset(h->h_mbox, 0, PM_MBOX_WORDS * sizeof(uint64_t));
-    CREATE_TRY(dalloc(h, &h->d_mrelay, 16));
-    CREATE_TRY(hipMemset(h->d_mrelay, 0, 16 * sizeof(uint64_t)));
     h->h_opt[0] = 0.0;
     CREATE_TRY(hipMemcpy(h->d_T, h->T.data(), h->T.size() * sizeof(double), hipMemcpyHostToDevice));
     CREATE_TRY(hipMemcpy(h->d_cmin, h->cmin.data(), (size_t)Cd * sizeof(double), hipMemcpyHostToDevice));
@@ -1110,7 +1082,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     // zero-fills above run on the null stream, which the non-blocking streams do not wait for.
     CREATE_TRY(hipDeviceSynchronize());
     CREATE_TRY(launch_rank(h->d_costs, h->S, h->d_rank, h->d_rank_keys, h->stream));
-    if (!h->trace_path.empty()) CREATE_TRY(dalloc(h, &h->d_trace, (size_t)(4 * ((h->R + 1) / 4 + 40))));   // + the relay waves' slots
+    if (!h->trace_path.empty()) CREATE_TRY(dalloc(h, &h->d_trace, (size_t)(4 * ((h->R + 1) / 4 + 40))));   // + the relay waves' and block 0's chunks' slots (COOP_TRACE)
 #undef CREATE_TRY
     *out = h;
     return MPPI_OK;
@@ -1132,7 +1104,6 @@ void mppi_destroy(mppi_handle *h)
                      h->ht_sum[0] / (double)std::max<int64_t>(1, h->ht_n[0]), h->ht_sum[1] / (double)std::max<int64_t>(1, h->ht_n[1]),
                      h->ht_sum[2] / (double)h->ht_n[2], (long long)h->ht_n[2]);
     (void)hipSetDevice(h->device);
-    pm_disarm(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->stream_opt) (void)hipStreamSynchronize(h->stream_opt);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -1141,7 +1112,6 @@ void mppi_destroy(mppi_handle *h)
     for (void *p : h->allocations) (void)hipFree(p);
     if (h->h_out) (void)hipHostFree(h->h_out);
     if (h->h_opt) (void)hipHostFree(h->h_opt);
-    if (h->h_mbox) (void)hipHostFree(h->h_mbox);
     if (h->ev_pub) (void)hipEventDestroy(h->ev_pub);
     if (h->ev_opt_done) (void)hipEventDestroy(h->ev_opt_done);
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
@@ -1163,7 +1133,6 @@ static inline bool sharded(const mppi_handle *h) { return h->world > 1 || h->com
 
 mppi_status mppi_set_shard(mppi_handle *h, int world, int rank)
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     if (h->updated_once) return fail(h, MPPI_ERR_INVALID, "shard must be set before the first update");
     int64_t b, e;
@@ -1187,7 +1156,6 @@ mppi_status mppi_comm_unique_id(char out[128])
 
 mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char unique_id[128])
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     mppi_status st = mppi_set_shard(h, world, rank);
     if (st != MPPI_OK) return st;
@@ -1201,7 +1169,6 @@ mppi_status mppi_comm_init(mppi_handle *h, int world, int rank, const char uniqu
 
 mppi_status mppi_comm_info(mppi_handle *h, int *nranks, int *rank, int *device, char *pci_bus_id, int len)
 {
-    pm_disarm(h);
     if (!h || !nranks || !rank) return MPPI_ERR_INVALID;
     if (h->comm) {   // what the communicator itself says, not what the caller asked for
         NCCL_TRY(ncclCommCount(h->comm, nranks));
@@ -1217,7 +1184,6 @@ mppi_status mppi_comm_info(mppi_handle *h, int *nranks, int *rank, int *device, 
 
 mppi_status mppi_set_noise_source(mppi_handle *h, int source, uint64_t seed)
 {
-    pm_disarm(h);
     if (!h || (source != MPPI_NOISE_DEVICE_PHILOX && source != MPPI_NOISE_HOST_INJECTED)) return MPPI_ERR_INVALID;
     h->noise_source = source;
     h->seed = seed;
@@ -1226,7 +1192,6 @@ mppi_status mppi_set_noise_source(mppi_handle *h, int source, uint64_t seed)
 
 mppi_status mppi_inject_noise(mppi_handle *h, const double *eps, int64_t columns)
 {
-    pm_disarm(h);
     if (!h || (!eps && columns) || columns < 0) return MPPI_ERR_INVALID;
     h->inj_pending.insert(h->inj_pending.end(), eps, eps + columns * h->C);
     return MPPI_OK;
@@ -1234,7 +1199,6 @@ mppi_status mppi_inject_noise(mppi_handle *h, const double *eps, int64_t columns
 
 mppi_status mppi_noise_draws(mppi_handle *h, double time, int64_t *columns)
 {
-    pm_disarm(h);
     if (!h || !columns) return MPPI_ERR_INVALID;
     *columns = draws_for(h, (int64_t)((time - h->last_shift_time) / h->dt));
     return MPPI_OK;
@@ -1242,7 +1206,6 @@ mppi_status mppi_noise_draws(mppi_handle *h, double time, int64_t *columns)
 
 mppi_status mppi_set_index_semantics(mppi_handle *h, int semantics)
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     if (semantics == MPPI_INDEX_COMPAT_UINT8) {
         if (h->R > 255) return fail(h, MPPI_ERR_UNSUPPORTED, "compat uint8 index semantics require rollouts + 2 <= 255 (the reference hangs beyond)");
@@ -1257,7 +1220,6 @@ mppi_status mppi_set_index_semantics(mppi_handle *h, int semantics)
 
 mppi_status mppi_set_forecast(mppi_handle *h, const double *wrench_Hx6)
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     if (wrench_Hx6) h->forecast.assign(wrench_Hx6, wrench_Hx6 + 6 * h->H);
     else h->forecast.clear();
@@ -1327,7 +1289,6 @@ void average_refresh(mppi_handle::DeviceForecast &f, double time)
 
 mppi_status mppi_forecast_attach(mppi_handle *h, const mppi_forecast_config *c)
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1393,7 +1354,6 @@ mppi_status mppi_forecast_attach(mppi_handle *h, const mppi_forecast_config *c)
 
 mppi_status mppi_forecast_observe(mppi_handle *h, const double *m, double time)
 {
-    pm_disarm(h);
     if (!h || !m || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
     mppi_handle::DeviceForecast &f = h->fc;
     if (f.type == FC_LOCF) {   // forecast.hpp:96-100
@@ -1422,7 +1382,6 @@ mppi_status mppi_forecast_observe(mppi_handle *h, const double *m, double time)
 
 mppi_status mppi_forecast_observe_time(mppi_handle *h, double time)
 {
-    pm_disarm(h);
     if (!h || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
     mppi_handle::DeviceForecast &f = h->fc;
     if (f.type == FC_AVERAGE) {
@@ -1437,7 +1396,6 @@ mppi_status mppi_forecast_observe_time(mppi_handle *h, double time)
 
 mppi_status mppi_forecast_get(mppi_handle *h, double time, double *out)
 {
-    pm_disarm(h);
     if (!h || !out || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(launch_forecast_eval(forecast_args(h), time, h->d_fc_out, h->stream));
@@ -1448,7 +1406,6 @@ mppi_status mppi_forecast_get(mppi_handle *h, double time, double *out)
 
 mppi_status mppi_forecast_table(mppi_handle *h, double t0, double dt, int64_t steps, double *out)
 {
-    pm_disarm(h);
     if (!h || !out || steps < 0 || h->fc.type == FC_NONE) return MPPI_ERR_INVALID;
     if (steps == 0) return MPPI_OK;
     HIP_TRY(hipSetDevice(h->device));
@@ -1464,7 +1421,6 @@ mppi_status mppi_forecast_table(mppi_handle *h, double t0, double dt, int64_t st
 
 mppi_status mppi_step_constants(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     std::vector<StepConst> st((size_t)h->H);
@@ -1478,9 +1434,9 @@ mppi_status mppi_step_constants(mppi_handle *h, double *out)
     return MPPI_OK;
 }
 
-void *mppi_device_costs(mppi_handle *h) { pm_disarm(h); return h ? (void *)h->d_costs : nullptr; }
-void *mppi_device_gradient(mppi_handle *h) { pm_disarm(h); return h ? (void *)h->d_gpart : nullptr; }
-void *mppi_stream(mppi_handle *h) { pm_disarm(h); return h ? (void *)h->stream : nullptr; }
+void *mppi_device_costs(mppi_handle *h) { return h ? (void *)h->d_costs : nullptr; }
+void *mppi_device_gradient(mppi_handle *h) { return h ? (void *)h->d_gpart : nullptr; }
+void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 
 // ---- update ---------------------------------------------------------------------------------
 
@@ -1580,7 +1536,6 @@ static FinishArgs finish_args(mppi_handle *h);
 
 mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
 {
-    pm_disarm(h);
     if (!h || !state) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
@@ -1831,7 +1786,6 @@ static WGradArgs wgrad_args(const mppi_handle *h)
 
 mppi_status mppi_update_phase2(mppi_handle *h)
 {
-    pm_disarm(h);
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     WGradArgs w{};
@@ -1983,7 +1937,6 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
 
 mppi_status mppi_update_phase3(mppi_handle *h)
 {
-    pm_disarm(h);
     if (!h || !h->phase_open) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     double seq = 0.0;
@@ -2136,7 +2089,6 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
 
 mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates)
 {
-    pm_disarm(h);
     if (!h || fault < 0 || fault > MPPI_DEBUG_RELAY_NO_SIGNAL || updates < 0) return MPPI_ERR_INVALID;
     h->debug_flags = fault;
     h->debug_updates = updates;
@@ -2145,7 +2097,6 @@ mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates)
 
 mppi_status mppi_debug_folded_cost(mppi_handle *h, double *cost)
 {
-    pm_disarm(h);
     if (!h || !cost) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -2155,7 +2106,6 @@ mppi_status mppi_debug_folded_cost(mppi_handle *h, double *cost)
 
 mppi_status mppi_set_graph(mppi_handle *h, int enable)
 {
-    pm_disarm(h);
     if (!h || enable < 0 || enable > 1) return MPPI_ERR_INVALID;
     h->graph_mode = enable;
     return MPPI_OK;
@@ -2163,7 +2113,6 @@ mppi_status mppi_set_graph(mppi_handle *h, int enable)
 
 mppi_status mppi_graph_updates(mppi_handle *h, int64_t *count)
 {
-    pm_disarm(h);
     if (!h || !count) return MPPI_ERR_INVALID;
     *count = h->graph_updates;
     return MPPI_OK;
@@ -2178,21 +2127,27 @@ static bool pm_fused_eligible(const mppi_handle *h)
            h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->host_trace && !h->d_trace;
 }
 
-// pm_update_kernel's arguments for update `upd` as the host state stands before the update's own
-// bookkeeping: the eps buffers as its swap leaves them, its publish sequence and epoch.  The state
-// and the shift are left 0 (the caller's; an armed launch reads them from the mailbox).  No side
-// effects.
-static PmFusedArgs pm_args(const mppi_handle *h, int64_t upd, bool ahead_valid, bool fold)
+static mppi_status update_pm_fused(mppi_handle *h, const double *state, double time)
 {
-    PmFusedArgs a;
-    std::memset(&a, 0, sizeof a);   // (padding included: pm_args_same compares bytes)
+    HIP_TRY(hipSetDevice(h->device));
+    h->t_start = std::chrono::steady_clock::now();
+    h->rollout_time = time;
+    h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);   // sample(): shift by truncation (mppi.cpp:194-201)
+    if (h->shift_by > 0) {
+        h->last_shift_time = time;
+        h->shifted = std::max<int64_t>(0, h->H - h->shift_by);
+    }
+    PmFusedArgs a{};
     a.pm = h->pm_host;
     a.steps = h->d_steps;
+    a.sp.shift_by = h->shift_by;
+    a.sp.shifted = h->shift_by > 0 ? h->shifted : h->H;
     a.sp.keep = keep_count(h);
-    a.sp.update_index = upd;
+    a.sp.update_index = h->update_count;
     a.sp.seed = h->seed;
     a.sp.tdiag = 1;
     for (int c = 0; c < 3; c++) a.tdv[c] = h->T[(size_t)(c * h->C + c)];
+    std::memcpy(a.x0v, state, (size_t)h->X * sizeof(double));
     a.x0_out = h->d_x0;
     a.X = (int)h->X;
     a.H = (int)h->H;
@@ -2201,11 +2156,13 @@ static PmFusedArgs pm_args(const mppi_handle *h, int64_t upd, bool ahead_valid, 
     a.dt = h->dt;
     a.rank = h->d_rank;
     // this update's draws were made ahead by the previous launch's tail when nothing they depend on changed
-    a.ahead = ahead_valid && h->ahead.update_index == upd && h->ahead.seed == h->seed && h->ahead.begin == h->begin &&
-              h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
-    a.prev = h->d_noise;           // the update swaps the buffers: this update's eps into the other one
-    a.noise = h->d_noise_prev;
-    a.ahead_noise = h->d_noise;    // free once the kept columns are copied (grid barrier)
+    a.ahead = h->ahead_valid && h->ahead.update_index == h->update_count && h->ahead.seed == h->seed &&
+              h->ahead.begin == h->begin && h->ahead.count == h->count && h->ahead.H == h->H && h->ahead.C == h->C;
+    h->ahead_valid = false;
+    std::swap(h->d_noise, h->d_noise_prev);   // this update's eps into the other buffer
+    a.prev = h->d_noise_prev;
+    a.noise = h->d_noise;
+    a.ahead_noise = h->d_noise_prev;          // free once the kept columns are copied (grid barrier)
     a.cost = h->d_costs;
     a.wexp = h->d_wexp;
     a.stats = h->d_cstats;
@@ -2225,96 +2182,28 @@ static PmFusedArgs pm_args(const mppi_handle *h, int64_t upd, bool ahead_valid, 
     a.Us = h->d_Us;
     a.gradient = h->d_grad;
     a.out = h->h_out_dev;
-    a.seq = (double)(h->publish_seq + 1);
+    a.seq = (double)(++h->publish_seq);
     a.opt_cost = h->d_opt;
     a.x0_opt = h->d_x0_opt;
     a.stamps = h->d_pm_stamps;
     // the previous update's pending filter() rides in this launch (block 0's second wave, beside
     // its rollouts); this update's stays pending for the next launch, or for a read (wait_optimal)
-    a.fold_filter = fold ? 1 : 0;
+    a.fold_filter = h->opt_state == mppi_handle::OPT_PENDING ? 1 : 0;
     a.fx0 = h->d_x0_opt;
-    return a;
-}
-
-// Whether two argument blocks agree on everything but the state, the shift and the mailbox
-static bool pm_args_same(const PmFusedArgs &x, const PmFusedArgs &y)
-{
-    PmFusedArgs u, v;
-    std::memcpy(&u, &x, sizeof u);
-    std::memcpy(&v, &y, sizeof v);
-    for (PmFusedArgs *p : {&u, &v}) {
-        std::memset(p->x0v, 0, sizeof p->x0v);
-        p->sp.shift_by = 0;
-        p->sp.shifted = 0;
-        p->mbox = nullptr;
-        p->mseq = 0;
-        p->mrelay = nullptr;
-    }
-    return std::memcmp(&u, &v, sizeof u) == 0;
-}
-
-// The armed launch: with nothing else on the update's path, the next update's launch is queued behind
-// this one as soon as this one is, with the mailbox (PmFusedArgs::mbox), while the host waits for the
-// publish anyway.  The next update then writes its state and shift into the mailbox instead of
-// launching: the launch call (≈4 µs of host time) and the dispatch of a launch onto an idle queue
-// leave the update's path.  The next update takes the armed launch only if its arguments are the ones
-// armed (pm_args_same: nothing the update depends on changed, this update succeeded) and it is fresh
-// (well inside the launch's own one-second bound); else it cancels it (pm_disarm) and launches.
-static bool pm_arm_ok(const mppi_handle *h)
-{
-    return !h->env.pm_arm_off && h->timing == 0 && !h->d_pm_stamps && !h->host_trace;
-}
-
-static mppi_status update_pm_fused(mppi_handle *h, const double *state, double time)
-{
-    HIP_TRY(hipSetDevice(h->device));
-    h->t_start = std::chrono::steady_clock::now();
-    h->rollout_time = time;
-    h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);   // sample(): shift by truncation (mppi.cpp:194-201)
-    if (h->shift_by > 0) {
-        h->last_shift_time = time;
-        h->shifted = std::max<int64_t>(0, h->H - h->shift_by);
-    }
-    PmFusedArgs a = pm_args(h, h->update_count, h->ahead_valid, h->opt_state == mppi_handle::OPT_PENDING);
-    a.sp.shift_by = h->shift_by;
-    a.sp.shifted = h->shift_by > 0 ? h->shifted : h->H;
-    std::memcpy(a.x0v, state, (size_t)h->X * sizeof(double));
-    bool armed = false;
-    if (h->pm_armed) {
-        const double age = std::chrono::duration<double>(h->t_start - h->pm_armed_at).count();
-        armed = age < 0.25 && h->timing == 0 && pm_args_same(a, h->pm_armed_args);
-        if (!armed) pm_disarm(h);
-    }
-    h->ahead_valid = false;
-    std::swap(h->d_noise, h->d_noise_prev);   // this update's eps into the other buffer
     // a filter() of the five-launch path still running on the side stream reads d_U / d_x0_opt
     if (h->opt_state == mppi_handle::OPT_LAUNCHED) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_opt_done, 0));
-    if (armed) {   // the mailbox: state and shift, their sum, then the sequence (x86 stores stay in order)
-        volatile uint64_t *m = h->h_mbox;
-        uint64_t w[8] = {};
-        std::memcpy(w, state, (size_t)h->X * sizeof(double));
-        w[6] = (uint64_t)h->shift_by;
-        for (int i = 0; i < 8; i++) m[i] = w[i];
-        m[9] = pm_mbox_sum(w, h->mbox_seq);
-        std::atomic_thread_fence(std::memory_order_release);
-        m[8] = h->mbox_seq;
-        h->pm_armed = false;
-        h->pm_armed_used++;
-    } else {
-        hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
-        if (h->timing == 1) {   // the launch's event pair into the ring (mppi_rollout_kernel_times)
-            ev_r0 = h->ev_ring[2 * h->ring_head];
-            ev_r1 = h->ev_ring[2 * h->ring_head + 1];
-            h->ring_head = (h->ring_head + 1) % mppi_handle::EV_RING;
-            h->ring_count = std::min(h->ring_count + 1, (int)mppi_handle::EV_RING);
-            h->ring_unread = true;
-            HIP_TRY(hipEventRecord(ev_r0, h->stream));
-        }
-        HIP_TRY(launch_pm_update(a, h->stream));
-        if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
+    hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
+    if (h->timing == 1) {   // the launch's event pair into the ring (mppi_rollout_kernel_times)
+        ev_r0 = h->ev_ring[2 * h->ring_head];
+        ev_r1 = h->ev_ring[2 * h->ring_head + 1];
+        h->ring_head = (h->ring_head + 1) % mppi_handle::EV_RING;
+        h->ring_count = std::min(h->ring_count + 1, (int)mppi_handle::EV_RING);
+        h->ring_unread = true;
+        HIP_TRY(hipEventRecord(ev_r0, h->stream));
     }
+    HIP_TRY(launch_pm_update(a, h->stream));
     h->pm_epoch = a.epoch;
-    h->publish_seq++;
+    if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
     // filter() of this update is left pending (as phase 3 leaves the cooperative launch's); the next
     // update's draws are in d_noise_prev
     h->opt_steps = h->d_steps;
@@ -2329,20 +2218,8 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
     h->info[MPPI_INFO_ROWS] = h->count;
     h->info[MPPI_INFO_HANDOVER] = -1;
     h->info[MPPI_INFO_FUSED_UPDATE] = 1;
-    h->info[MPPI_INFO_ARMED] = armed ? 1 : 0;
     h->updated_once = true;
     h->phase_open = true;
-    if (pm_arm_ok(h)) {   // the next update's launch, armed behind this one (as if this one succeeds)
-        PmFusedArgs n = pm_args(h, h->update_count + 1, true, true);
-        n.mbox = h->h_mbox_dev;
-        n.mseq = ++h->mbox_seq;
-        n.mrelay = h->d_mrelay;
-        if (launch_pm_update(n, h->stream) == hipSuccess) {
-            h->pm_armed = true;
-            h->pm_armed_args = n;
-            h->pm_armed_at = std::chrono::steady_clock::now();
-        }
-    }
     mppi_status st = phase3_wait(h, a.seq);
     if (h->d_pm_stamps && st == MPPI_OK) {   // diagnostics: each phase's end after the block's entry
         std::vector<uint64_t> sv((size_t)h->pm_nblocks * PM_STAMPS);
@@ -2365,8 +2242,7 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
 mppi_status mppi_update(mppi_handle *h, const double *state, double time)
 {
     if (h && state && pm_fused_eligible(h)) return update_pm_fused(h, state, time);
-    if (h) h->info[MPPI_INFO_FUSED_UPDATE] = h->info[MPPI_INFO_ARMED] = 0;
-    pm_disarm(h);   // (an update that left the fused path: a setting changed)
+    if (h) h->info[MPPI_INFO_FUSED_UPDATE] = 0;
     if (h && state && graph_eligible(h)) return update_graph(h, state, time);
     if (h && sharded(h) && !h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
     mppi_status st = mppi_update_phase1(h, state, time);
@@ -2401,7 +2277,6 @@ mppi_status mppi_get(mppi_handle *h, double time, double *control)
 
 mppi_status mppi_costs(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipMemcpy(out, h->d_costs, (size_t)h->R * sizeof(double), hipMemcpyDeviceToHost));
@@ -2410,7 +2285,6 @@ mppi_status mppi_costs(mppi_handle *h, double *out)
 
 mppi_status mppi_weights(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     // the device keeps e_r and the normaliser (weights_gradient_kernel, finish): w_r = e_r / total,
@@ -2425,7 +2299,6 @@ mppi_status mppi_weights(mppi_handle *h, double *out)
 
 mppi_status mppi_gradient(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipMemcpy(out, h->d_grad, (size_t)(h->H * h->C) * sizeof(double), hipMemcpyDeviceToHost));
@@ -2434,7 +2307,6 @@ mppi_status mppi_gradient(mppi_handle *h, double *out)
 
 mppi_status mppi_optimal_control(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     std::lock_guard<std::mutex> lock(h->mtx);
     std::memcpy(out, h->U_host.data(), h->U_host.size() * sizeof(double));
@@ -2461,7 +2333,6 @@ static mppi_status wait_optimal(mppi_handle *h)
 
 mppi_status mppi_synchronize(mppi_handle *h)
 {
-    pm_disarm(h);
     if (!h) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -2470,7 +2341,6 @@ mppi_status mppi_synchronize(mppi_handle *h)
 
 mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
 {
-    pm_disarm(h);
     if (!h || !cost) return MPPI_ERR_INVALID;
     mppi_status st = wait_optimal(h);
     if (st != MPPI_OK) return st;
@@ -2481,7 +2351,6 @@ mppi_status mppi_optimal_cost(mppi_handle *h, double *cost)
 
 mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
 {
-    pm_disarm(h);
     if (!h || !terms7) return MPPI_ERR_INVALID;
     if (h->dyn_kind != MPPI_DYNAMICS_FRANKARIDGEBACK || h->cost_kind != MPPI_COST_ASSISTED_MANIPULATION)
         return fail(h, MPPI_ERR_UNSUPPORTED, "per-term totals: AssistedManipulation on the cooperative kernel only");
@@ -2501,7 +2370,6 @@ mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
 
 mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout)
 {
-    pm_disarm(h);
     if (!h || !rollout) return MPPI_ERR_INVALID;
     std::vector<double> c((size_t)h->R);
     mppi_status st = mppi_costs(h, c.data());
@@ -2524,7 +2392,6 @@ mppi_status mppi_update_duration(mppi_handle *h, double *seconds)
 
 mppi_status mppi_noise(mppi_handle *h, double *out)
 {
-    pm_disarm(h);
     if (!h || !out) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     const int64_t HC = h->H * h->C;
@@ -2549,8 +2416,6 @@ mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
         h->info[MPPI_INFO_HANDOVER] = w;
     }
     h->info[MPPI_INFO_WAIT_TIMEOUTS_TOTAL] = h->wait_timeouts_total;
-    h->info[MPPI_INFO_ARMED_USED] = h->pm_armed_used;
-    h->info[MPPI_INFO_ARMED_CANCELLED] = h->pm_armed_cancelled;
     std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;
 }
@@ -2567,7 +2432,6 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *R, int64_t *H, int64_t *C, int64_
 
 mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64_t *start_idx)
 {
-    pm_disarm(h);
     if (!h || !uu || !tt || !start_idx) return MPPI_ERR_INVALID;
     if (h->sg_window <= 0) return fail(h, MPPI_ERR_INVALID, "smoothing disabled");
     HIP_TRY(hipSetDevice(h->device));
@@ -2580,7 +2444,6 @@ mppi_status mppi_smoothing_windows(mppi_handle *h, double *uu, double *tt, int64
 
 mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
 {
-    pm_disarm(h);
     if (!h || !ms5) return MPPI_ERR_INVALID;
     mppi_status st = wait_optimal(h);
     if (st != MPPI_OK) return st;
@@ -2590,7 +2453,6 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5)
 
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5)
 {
-    pm_disarm(h);
     return mppi_kernel_times_detail(h, ms5, 5);
 }
 
@@ -2609,7 +2471,6 @@ mppi_status mppi_set_timing(mppi_handle *h, int level)
 
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
 {
-    pm_disarm(h);
     if (!h || !ms || n < 0 || n > 7) return MPPI_ERR_INVALID;
     if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
@@ -2625,7 +2486,6 @@ mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
 
 mppi_status mppi_rollout_kernel_times(mppi_handle *h, float *ms, int capacity, int *count)
 {
-    pm_disarm(h);
     if (!h || !count || capacity < 0 || (capacity > 0 && !ms)) return MPPI_ERR_INVALID;
     HIP_TRY(hipSetDevice(h->device));
     const int n = std::min(h->ring_count, capacity);

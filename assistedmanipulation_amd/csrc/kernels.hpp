@@ -331,7 +331,7 @@ bool fr_coop_costs_in_launch(const EnvSwitches &env);   // the objective runs in
 // before creating a handle): a handle's launch paths never change under it, and no getenv runs on
 // the update path (~80 ns each)
 struct EnvSwitches {
-    bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off, pm_arm_off;
+    bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off;
 };
 EnvSwitches env_switches_read();
 // Whether a pending filter() folds into the update launch of `count` rows with the objective in
@@ -424,30 +424,7 @@ struct PmFusedArgs {
     int fold_filter;            // the previous update's filter() is pending: run it in this launch
     const double *fx0;          // its state (x0_opt as the previous launch left it)
     uint64_t *stamps;           // diagnostics (MPPI_PM_STAMPS=1): [nblocks][PM_STAMPS] s_memrealtime, or null
-    // the armed launch (engine.cpp pm_arm): the mapped host mailbox whose sequence mseq releases the
-    // launch with the update's state and shift (x0v, sp.shift_by / sp.shifted unused), and whose
-    // cancel (mseq | PM_MBOX_CANCEL) ends it at entry; null for a launch queued by its own update
-    const uint64_t *mbox;
-    uint64_t mseq;
-    uint64_t *mrelay;           // [9] device memory: block 0's copy of the mailbox words 0..7, then its flag
 };
-// The armed launch's mailbox, PM_MBOX_WORDS 64-bit words in mapped host memory: the state (words
-// 0..5, doubles), the shift (6, int64), 0 (7), the sequence (8) and pm_mbox_sum over words 0..8 (9).
-// The host writes the sequence last; the launch takes the words only when the sum matches the words
-// it read, so a read that returned some of the host's old words with the new sequence is retried.
-constexpr int PM_MBOX_WORDS = 16;
-constexpr uint64_t PM_MBOX_CANCEL = 1ull << 63;
-constexpr uint64_t PM_ARM_TIMEOUT_TICKS = 100000000ull;   // s_memrealtime (100 MHz): 1 s, then the launch ends
-__host__ __device__ inline uint64_t pm_mbox_sum(const uint64_t *w, uint64_t seq)
-{
-    uint64_t h = 0xcbf29ce484222325ull ^ seq;
-    for (int i = 0; i < 8; i++) {
-        h ^= w[i];
-        h *= 0x100000001b3ull;
-    }
-    h ^= seq;
-    return h * 0x100000001b3ull;
-}
 // entry, sampled, rolled out (costs folded into the statistics), barrier passed, partials stored,
 // ticket taken, staged, (finisher:) stored, published, ranked, end, costs computed
 constexpr int PM_STAMPS = 12;

@@ -207,56 +207,8 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     // as Leps is)
     double *Lpre = Leps + PR * ES;
     __shared__ int s_last;
-    __shared__ double s_mb[8];   // the armed launch's state and shift (mailbox words 0..7)
-    __shared__ int s_go;
-    if (a.mbox) {   // armed (update_pm_fused): wait for the update's mailbox, or its cancel (bounded)
-        // Block 0 alone polls the host's mailbox (one reader on the host's line) and relays its
-        // words to the other blocks through device memory: the payload, then the flag, sc1.
-        if (w == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            int go = -1;
-            uint64_t v = 0;
-            if (b == 0) {
-                while (go < 0) {
-                    v = l < 10 ? __hip_atomic_load(a.mbox + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
-                    uint64_t wd[10];
-#pragma unroll
-                    for (int i = 0; i < 10; i++)
-                        wd[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-                    if (wd[8] == a.mseq && wd[9] == pm_mbox_sum(wd, a.mseq)) go = 1;
-                    else if (wd[8] == (a.mseq | PM_MBOX_CANCEL) || __builtin_amdgcn_s_memrealtime() - t0 > PM_ARM_TIMEOUT_TICKS)
-                        go = 0;
-                    else __builtin_amdgcn_s_sleep(1);
-                }
-                if (go == 1 && l < 8) __hip_atomic_store(a.mrelay + l, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_s_waitcnt(0);
-                if (l == 0) __hip_atomic_store(a.mrelay + 8, go == 1 ? a.mseq : (a.mseq | PM_MBOX_CANCEL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                while (go < 0) {
-                    const uint64_t f = __hip_atomic_load(a.mrelay + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (f == a.mseq) go = 1;
-                    else if (f == (a.mseq | PM_MBOX_CANCEL) || __builtin_amdgcn_s_memrealtime() - t0 > PM_ARM_TIMEOUT_TICKS + 10000000ull)
-                        go = 0;
-                    else __builtin_amdgcn_s_sleep(1);
-                }
-                if (go == 1 && l < 8) v = __hip_atomic_load(a.mrelay + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (go == 1 && l < 8) s_mb[l] = __longlong_as_double((long long)v);
-            if (l == 0) s_go = go;
-        }
-        __syncthreads();
-        if (!s_go) return;   // cancelled: nothing read or written
-    } else if (t < 8) {
-        s_mb[t] = a.x0v[t];   // (the state read through LDS either way: one address space)
-    }
-    const double *x0v = s_mb;
-    SampleParams P = a.sp;
-    if (a.mbox) {
-        P.shift_by = (int64_t)__double_as_longlong(s_mb[6]);
-        P.shifted = P.shift_by > 0 ? (P.shift_by < a.H ? a.H - P.shift_by : 0) : a.H;
-    }
     const int64_t r0 = (int64_t)b * PR;
+    const SampleParams &P = a.sp;
     const double *Uprev = a.U;   // U* as the previous update published it
     const unsigned target = a.epoch * (unsigned)nb;
     auto stamp = [&](int i) {   // diagnostics: one clock stamp per block and phase
@@ -344,7 +296,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     for (int i = t + PT; i < HC; i += PT) Lus[i] = us_at(i);
     if (t < H) Lgm[t] = gm_t;
     for (int k = t + PT; k < H; k += PT) Lgm[k] = a.steps[k].gamma_k;
-    if (b == 0 && t < a.X) a.x0_out[t] = x0v[t];
+    if (b == 0 && t < a.X) a.x0_out[t] = a.x0v[t];
     // the previous update's filter() (mppi.cpp:450-479), which its launch left pending, runs in this
     // block's tail: its inputs are taken now, before this launch's finisher rewrites them - the U*
     // it published, its state (x0_opt) and whether it threw (then no filter)
@@ -374,7 +326,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     // (Round 4 split the state chain from the step costs - the positions through LDS, the costs by
     // all threads - and measured it slower: 28.7 against 27.6 us per update, profiles/r04/pm_split_ab/;
     // the control part needs no state, so here it is formed before the chain instead.)
-    if (mine) J = pm_rollout_pre<PR>(a, x0v, Lgm, Lpre, l);
+    if (mine) J = pm_rollout_pre<PR>(a, a.x0v, Lgm, Lpre, l);
     stamp(11);
     if (w == 0) {
         if (mine) st_sc1(a.cost + gr, J);   // read by every block's rank (tail)
@@ -498,7 +450,7 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             if (ok) a.U[o] = v;
             pub(a.out + o, v);
         }
-        if (t < a.X) a.x0_opt[t] = x0v[t];
+        if (t < a.X) a.x0_opt[t] = a.x0v[t];
         if (t == 0) {
             st->all_nan = all_nan;
             st->early = early;

@@ -433,14 +433,9 @@ class Trajectory:
         the doubled SIMD or -1, the in-launch waits that gave up in the last update - which then
         failed - and summed since create)."""
         out = np.zeros(abi.MPPI_UPDATE_INFO_N, dtype=np.int64)
-        p = out.ctypes.data_as(C.POINTER(C.c_int64))
-        st = self._L.mppi_update_info(self._h, p, out.size)
-        if st != 0:   # a library from before the armed-launch slots (A/B runs under MPPI_AMD_LIB)
-            out = out[:10]
-            st = self._L.mppi_update_info(self._h, p, out.size)
-        self._check(st)
+        self._check(self._L.mppi_update_info(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), out.size))
         keys = ("cooperative", "folded_filter", "objective_in_launch", "tail_draws", "sampling", "rows", "handover",
-                "wait_timeouts", "wait_timeouts_total", "fused_update", "armed", "armed_used", "armed_cancelled")
+                "wait_timeouts", "wait_timeouts_total", "fused_update")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def debug_inject(self, fault, updates=1):

@@ -398,12 +398,7 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
 #define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass,
                                              pm_update_kernel) */
-#define MPPI_INFO_ARMED 10                /* 1: that launch was the armed one, queued by the
-                                             previous update and released by the mailbox */
-#define MPPI_INFO_ARMED_USED 11           /* armed launches taken since create */
-#define MPPI_INFO_ARMED_CANCELLED 12      /* armed launches cancelled since create (another
-                                             call came first, or the arguments changed) */
-#define MPPI_UPDATE_INFO_N 13
+#define MPPI_UPDATE_INFO_N 10
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
 /* Fault injection for the failure-detection tests (no reference counterpart; never set in

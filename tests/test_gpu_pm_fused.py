@@ -119,60 +119,3 @@ def test_folded_filter_cost_against_oracle():
         prev_opt = orc.optimal_cost()
         prev_costs, prev_noise = costs, noise
         x = x + 0.01
-
-
-def test_armed_launch_equals_plain_launches(monkeypatch):
-    """The armed launch (engine.cpp update_pm_fused: the next update's launch queued behind this one,
-    released by the mapped mailbox with the state and the shift) against plain launches
-    (MPPI_PM_ARM=0): U* bit for bit over updates that take the armed launch, and over calls in
-    between that cancel it (reads of device results, a setting change), with the armed launches
-    counted in mppi_update_info."""
-    times = [0.05 * j for j in range(12)] + [0.62, 0.64, 0.70, 0.75, 0.75, 0.80]
-    reads = {4, 9, 15}   # device reads after these updates: the armed launch is cancelled
-    out = {}
-    for arm in ("1", "0"):
-        monkeypatch.setenv("MPPI_PM_ARM", arm)
-        conf, t = _pm(1024, 0.32)
-        x = np.zeros(6)
-        rec = []
-        for j, tm in enumerate(times):
-            t.update(x, tm)
-            info = t.update_info()
-            assert info["fused_update"] == 1 and info["wait_timeouts"] == 0, info
-            if arm == "0":
-                assert info["armed"] == 0 and info["armed_used"] == 0, info
-            elif j > 0 and (j - 1) not in reads:
-                assert info["armed"] == 1, (j, info)   # nothing came between the two updates
-            rec.append(t.get(tm).copy())   # host-side read: leaves the armed launch in place
-            if j in reads:
-                rec.append(t.costs().copy())
-                rec.append(t.noise().copy())
-            x = x + 0.01
-        info = t.update_info()
-        if arm == "1":
-            assert info["armed_used"] == len(times) - 1 - len(reads), info
-            assert info["armed_cancelled"] == len(reads), info
-        rec.append(t.get_optimal_rollout().copy())
-        t.synchronize()
-        out[arm] = rec
-    assert len(out["1"]) == len(out["0"])
-    for i, (a, b) in enumerate(zip(out["1"], out["0"])):
-        np.testing.assert_array_equal(a, b, err_msg="record %d" % i)
-
-
-def test_armed_launch_expires_unused():
-    """An armed launch that no update takes ends by itself within its bound (one second), and the
-    next update then launches plainly."""
-    import time as _time
-    conf, t = _pm(1024, 0.32)
-    x = np.zeros(6)
-    t.update(x, 0.0)
-    t.update(x, 0.05)
-    assert t.update_info()["armed"] == 1
-    _time.sleep(1.5)   # past the host's freshness bound (0.25 s) and the launch's own (1 s)
-    t.update(x, 0.10)
-    info = t.update_info()
-    assert info["armed"] == 0 and info["armed_cancelled"] == 1 and info["wait_timeouts"] == 0, info
-    t.update(x, 0.15)
-    assert t.update_info()["armed"] == 1
-    assert np.all(np.isfinite(t.costs()))
