@@ -23,7 +23,7 @@ def _pm(S, horison, K=20):
     return conf, t
 
 
-@pytest.mark.parametrize("S,horison", [(1024, 0.32), (1000, 0.32), (2046, 0.64), (62, 0.16)])
+@pytest.mark.parametrize("S,horison", [(1024, 0.32), (1000, 0.32), (2046, 0.64), (62, 0.16), (4094, 0.08)])
 def test_fused_update_equals_five_launches(S, horison, monkeypatch):
     """Noise bit for bit (draws made ahead by the previous launch's tail, kept columns shifted in),
     costs bit for bit (the same per-rollout arithmetic), weights / gradient / U* and the filter()

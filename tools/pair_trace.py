@@ -1,6 +1,6 @@
 import numpy as np, sys
 raw = np.fromfile(sys.argv[1], dtype=np.uint32)
-ns = 1048
+ns = 1064
 rec = raw.reshape(-1, ns, 4).astype(np.int64)
 for u in (-1, -2, -3):
     r = rec[u]
@@ -9,7 +9,7 @@ for u in (-1, -2, -3):
     us = lambda x: (np.asarray(x) - t0) / 100.0
     print("update", u)
     print("  block 0 stage ends", np.round(us(r[1025]), 1), " block 8 stage ends", np.round(us(r[1033]), 1))
-    print("  token at stage 4 %.1f, first-half sums %.1f, second-half J %.1f" % (us(r[1040][2]), us(r[1040][1]), us(r[1040][0])))
+    print("  token at stage 4 %.1f, first-half sums %.1f, second-half J %.1f" % (us(r[1063][2]), us(r[1063][1]), us(r[1063][0])))
     for b in (0, 8):
         print("  block %d main loop ends" % b, np.round(us(le[4*b:4*b+4]), 1), "wave ends", np.round(us(we[4*b:4*b+4]), 1))
     bw = us(we).reshape(256, 4).max(1)
