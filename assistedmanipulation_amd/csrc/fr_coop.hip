@@ -1596,19 +1596,9 @@ __device__ __forceinline__ bool row_live(const FrRolloutArgs &a, int64_t lr)
 // line a chunk reads is written after it.  The relay's rows are taken after their last stage.
 constexpr int CH = 16;          // steps per chunk
 constexpr int HC_MAX = 128;     // the horizon bound of the objective in this launch (Lcs)
-// A group's last chunk is the launch's tail: it is read only after the group's loop, and one
-// record's objective on one lane is a chain of about 1500 dependent-latency-bound instructions (7-11
-// us, block 0's chunk stamps).  For the AssistedManipulation objective that chunk is split into
-// NPART tasks that other waves take at once - the joint terms, the workspace (and energy) terms, the
-// kinematic terms - each for the chunk's 64 records, two doubles a record into LDS (Lpart); the wave
-// that completes the last part adds them up in get_cost's order (am_combine).
-constexpr int NPART = 3;
-// (not with the energy tank: its larger per-row LDS leaves no room for Lpart)
-template <int CK, bool EN>
-constexpr bool split_last() { return CK == mppi_cost::CK_ASSISTED_MANIPULATION && !EN; }
 // LDS words (Lq): the main waves' steps, the groups' next chunk to take and chunks completed, the
-// relay's stage, the parts of each group's last chunk completed
-enum { Q_PROG = 0, Q_NEXT = 4, Q_DONE = 9, Q_STAGE = 14, Q_PART = 15, Q_N = 20 };
+// relay's stage
+enum { Q_PROG = 0, Q_NEXT = 4, Q_DONE = 9, Q_STAGE = 14, Q_N = 16 };
 // LDS flags (Lflag): main wave g's records are stored (g), the relay's rows are done (LF_RELAY),
 // main wave g's kept columns are copied (LF_KEPT + g: its rows' previous eps is read, so their next
 // draws may overwrite it)
@@ -1632,47 +1622,10 @@ __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c
     return lds_read(Lflag + g) != 0;
 }
 
-// Part `part` of the AssistedManipulation objective at the lane's record rk (step constants sc):
-// 0 the joint-limit and velocity terms, 1 the workspace and energy terms, 2 the trajectory and
-// manipulability terms (mppi_cost::am_*: assisted_manipulation_cost's pieces)
-template <bool EN>
-__device__ __forceinline__ void am_part(const DevCost &Cs, int part, const StepConst &sc, const double *rk, const double *Lj,
-                                       double &x, double &y)
-{
-    const double2 *r2 = reinterpret_cast<const double2 *>(rk);
-    if (part == 0) {
-        double r[2 * FR_NB];
-#pragma unroll
-        for (int i = 0; i < FR_NB; i++) {
-            const double2 v = r2[REC_QQD / 2 + i];
-            r[2 * i] = v.x;
-            r[2 * i + 1] = v.y;
-        }
-        mppi_cost::am_joint_terms<MB>(r, Lj, x, y);
-    } else if (part == 1) {
-        double t[REC_VL - REC_EE];
-#pragma unroll
-        for (int i = 0; i < (REC_VL - REC_EE) / 2; i++) {
-            const double2 v = r2[REC_EE / 2 + i];
-            t[2 * i] = v.x;
-            t[2 * i + 1] = v.y;
-        }
-        x = mppi_cost::am_workspace_term(Cs, rk[REC_QQD + 4], t, t + (REC_AM - REC_EE));
-        y = EN ? mppi_cost::am_energy_term(Cs, t[REC_E - REC_EE]) : 0.0;
-    } else {
-        double vl[3], jj[6];
-        mppi_cost::kin_sums(r2, vl, jj);
-        x = mppi_cost::trajectory_term(Cs, sc, vl);
-        y = mppi_cost::manipulability_term(Cs, jj);
-    }
-}
-
-// The step costs of chunk c of group g into Lcs (part >= 0: that part of the group's last chunk
-// into Lpart, and the wave that completes its parts combines them); the pass that completes the
-// group sums its rows
+// The step costs of chunk c of group g into Lcs; the pass that completes the group sums its rows
 template <int CK, bool EN>
-__device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c, int part, int lane, const double *Lmodel,
-                                          double *Lcs, double *Lpart, int *Lq)
+__device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c, int lane, const double *Lmodel, double *Lcs,
+                                          int *Lq)
 {
     const int H = a.H;
     const int nch = (H + CH - 1) / CH;   // the group's chunks
@@ -1684,21 +1637,7 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     const double *rec = frow ? a.frec : a.rec + lrv * H * FR_REC;
     const StepConst *stp = frow ? a.fsteps : a.steps;
     const int kk = live ? k : 0;
-    double cs;
-    if (split_last<CK, EN>() && part >= 0) {
-        double *lp = Lpart + (g * 64 + lane) * (2 * NPART);
-        double x, y;
-        am_part<EN>(*a.cost, part, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO, x, y);
-        lp[2 * part] = x;
-        lp[2 * part + 1] = y;
-        // the stores before the count: the wave that completes the parts reads them all
-        const int m = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(Lq + Q_PART + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (m + 1 != NPART) return;
-        cs = stp[kk].gamma_k * mppi_cost::am_combine<EN>(*a.cost, lp[0], lp[1], lp[2], lp[3], lp[4], lp[5]);
-    } else {
-        cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO);
-    }
+    const double cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO);
     if (live) Lcs[(g * ROWS_PER_WAVE + i) * HC_MAX + k] = cs;
     // the stores before the count: the wave that completes the group reads every chunk's costs
     const int n = __builtin_amdgcn_readfirstlane(
@@ -1726,25 +1665,23 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
 // waits for its records); returns once every chunk is taken.  Bounded.
 template <int CK, bool EN>
 __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int ng, int lane, const double *Lmodel,
-                                         double *Lcs, double *Lpart, int *Lflag, int *Lq)
+                                         double *Lcs, int *Lflag, int *Lq)
 {
-    // a group's tasks: its chunks, the last one as NPART parts (split_last)
-    const int nch = (a.H + CH - 1) / CH, ntask = split_last<CK, EN>() ? nch + NPART - 1 : nch;
+    const int nch = (a.H + CH - 1) / CH;
 #pragma unroll 1
     for (int spin = 0; spin < WAIT_SPINS; spin++) {
         bool left = false, did = false;
 #pragma unroll 1
         for (int d = 0; d < ng && !did; d++) {
             const int g = first + d < ng ? first + d : first + d - ng;
-            const int t0 = lds_read(Lq + Q_NEXT + g);
-            if (t0 >= ntask) continue;
+            const int c0 = lds_read(Lq + Q_NEXT + g);
+            if (c0 >= nch) continue;
             left = true;
-            if (!chunk_ready(a, g, min(t0, nch - 1), Lflag, Lq)) continue;
+            if (!chunk_ready(a, g, c0, Lflag, Lq)) continue;
             // every lane executes the add (lane 0 adds 1): no lane-dependent branch around it
-            const int tk = __builtin_amdgcn_readfirstlane(
+            const int c = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_fetch_add(Lq + Q_NEXT + g, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (tk >= ntask) continue;
-            const int c = min(tk, nch - 1), part = (split_last<CK, EN>() && tk >= nch - 1) ? tk - (nch - 1) : -1;
+            if (c >= nch) continue;
             int w = 0;
             while (!chunk_ready(a, g, c, Lflag, Lq) && w < WAIT_SPINS) {
                 __builtin_amdgcn_s_sleep(4);
@@ -1754,9 +1691,9 @@ __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int
 #ifdef COST_TRACE   // block 0's chunks: start, end, wave (slots past the relay's)
             const uint32_t tc0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-            cost_chunk<CK, EN>(a, g, c, part, lane, Lmodel, Lcs, Lpart, Lq);
+            cost_chunk<CK, EN>(a, g, c, lane, Lmodel, Lcs, Lq);
 #ifdef COST_TRACE
-            if (a.trace && blockIdx.x == 0 && lane == 0 && c < 4 && part <= 0) {
+            if (a.trace && blockIdx.x == 0 && lane == 0 && c < 4) {
                 uint32_t *tr = a.trace + 4 * (gridDim.x * 4 + 16 + 4 * g + c);
                 tr[0] = tc0;
                 tr[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -1977,7 +1914,6 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ int Lq[Q_N];          // the main waves' steps, chunk counters, the relay's stage
     __shared__ double Lst[64 * 3];   // the relay's (q, qd, E) per lane between stages
     __shared__ double Lcs[5 * ROWS_PER_WAVE * HC_MAX];   // step costs of the groups' rows
-    __shared__ double Lpart[split_last<CK, EN>() ? 5 * 64 * 2 * NPART : 1];   // the last chunks' parts (cost_chunk)
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
@@ -2012,7 +1948,7 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         __builtin_amdgcn_s_setprio(0);
         if (cil) {
             signal_records(Lflag + wv);
-            cost_work<CK, EN>(a, wv, ng, lane, Lmodel, Lcs, Lpart, Lflag, Lq);
+            cost_work<CK, EN>(a, wv, ng, lane, Lmodel, Lcs, Lflag, Lq);
         }
 #ifdef COST_TRACE   // COOP_TRACE builds: slot 3 = the wave's end (after its objective work)
         if (a.trace && lane == 0) a.trace[4 * wblk + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -2025,7 +1961,7 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
         if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
-        cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lpart, Lflag, Lq);
+        cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
 }
 

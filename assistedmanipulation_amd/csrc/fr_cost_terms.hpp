@@ -127,15 +127,10 @@ __device__ __forceinline__ void derive_record(const double *rk, double *r)
     r[FR_NREC - 1] = 0.0;
 }
 
-// The pieces of AssistedManipulation::get_cost.  assisted_manipulation_cost evaluates them in one
-// pass; the rollout launch's objective may evaluate them on separate waves for a group's last chunk
-// (fr_coop.hip, cost parts) and combine them with am_combine - the same operations on the same
-// operands in the same order, so the same bits.
-// The joint-limit and velocity terms of the (q, qd) pairs r[REC_QQD + 2j], [2j + 1]: joints 0..5
-// and 6..11 summed apart from 0.0, in joint order, then added (the association of the lane sums
-// they replaced)
-template <int JS>
-__device__ __forceinline__ void am_joint_terms(const double *r, const double *Lj, double &joint, double &vel)
+// AssistedManipulation::get_cost at the record's state with its kinematics
+template <bool EN, int JS>
+__device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
+                                                             const double *Lj, const double2 *src)
 {
     double j0 = 0.0, j1 = 0.0, v0 = 0.0, v1 = 0.0;
     int off = 0;
@@ -152,64 +147,7 @@ __device__ __forceinline__ void am_joint_terms(const double *r, const double *Lj
         if (j < 6) { j0 += lj; v0 += lv; }
         else { j1 += lj; v1 += lv; }
     }
-    joint = j0 + j1;
-    vel = v0 + v1;
-}
-// workspace_cost (assisted_manipulation.cpp:160-209) at base yaw q_2 = yaw, EE position ee and
-// arm-mount position am
-__device__ __forceinline__ double am_workspace_term(const DevCost &Cs, double yaw, const double *ee, const double *am)
-{
-    double s, c;
-    fsincos(yaw, &s, &c, sincos_constants());   // base yaw q_2
-    double wc = 0.0;
-    const double r22 = (1.0 - c) + c;
-    const double fw0 = c, fw1 = s, fw2 = 0.0;
-    const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
-    const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
-    const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
-    const double rb2 = am[2] + off2;
-    const double t0 = ee[0] - (am[0] + off0), t1 = ee[1] - (am[1] + off1), t2 = ee[2] - rb2;
-    const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
-    wc += left_barrier(Cs.ws_infront, proj);
-    wc += right_barrier(Cs.ws_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
-    const double n1 = sqrt(t0 * t0 + t1 * t1);
-    const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
-    const double ya = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
-    const double ay = fabs(ya);
-    const double yc = (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
-    wc += isnan(ya) ? 0.0 : yc;
-    wc += left_barrier(Cs.ws_above, ee[2] - rb2);
-    return wc;
-}
-// energy_cost (:211-222) at tank level E
-__device__ __forceinline__ double am_energy_term(const DevCost &Cs, double E)
-{
-    return left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);
-}
-// get_cost's sum of the enabled terms, in its order (the trajectory and manipulability terms as
-// trajectory_term / manipulability_term give them)
-template <bool EN>
-__device__ __forceinline__ double am_combine(const DevCost &Cs, double joint, double vel, double wc, double en, double traj,
-                                            double manip)
-{
-    double cost = 0.0;
-    cost += Cs.en_joint ? joint : 0.0;
-    cost += Cs.en_self ? Cs.self_collision : 0.0;
-    cost += Cs.en_work ? wc : 0.0;
-    if constexpr (EN) cost += en;
-    cost += Cs.en_vel ? vel : 0.0;
-    cost += Cs.en_traj ? traj : 0.0;
-    cost += Cs.en_manip ? manip : 0.0;
-    return cost;
-}
-
-// AssistedManipulation::get_cost at the record's state with its kinematics
-template <bool EN, int JS>
-__device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
-                                                             const double *Lj, const double2 *src)
-{
-    double joint, vel;
-    am_joint_terms<JS>(r, Lj, joint, vel);
+    const double joint = j0 + j1, vel = v0 + v1;
     // the rest of the record (r holds the (q, qd) pairs only) is loaded through a pointer that
     // waits for the joint sums: the remaining terms start after them instead of interleaving with
     // them and holding their values live (two waves per SIMD instead of four)
@@ -226,9 +164,41 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
     double vl[3], jj[6];   // from the stored record's motion subspaces (kin_sums)
     kin_sums(tp, vl, jj);
     r = rest - REC_EE;   // r[REC_EE .. REC_VL) from here on
-    const double wc = am_workspace_term(Cs, yaw, r + REC_EE, r + REC_AM);
-    const double en = EN ? am_energy_term(Cs, r[REC_E]) : 0.0;
-    return am_combine<EN>(Cs, joint, vel, wc, en, trajectory_term(Cs, sc, vl), manipulability_term(Cs, jj));
+    double s, c;
+    fsincos(yaw, &s, &c, sincos_constants());   // base yaw q_2
+    const double *ee = r + REC_EE, *am = r + REC_AM;
+    double wc = 0.0;
+    {
+        const double r22 = (1.0 - c) + c;
+        const double fw0 = c, fw1 = s, fw2 = 0.0;
+        const double off0 = (0.1 * c + (-s) * 0.0) + 0.0 * 0.15;
+        const double off1 = (0.1 * s + c * 0.0) + 0.0 * 0.15;
+        const double off2 = (0.0 * 0.1 + 0.0 * 0.0) + r22 * 0.15;
+        const double rb2 = am[2] + off2;
+        const double t0 = ee[0] - (am[0] + off0), t1 = ee[1] - (am[1] + off1), t2 = ee[2] - rb2;
+        const double proj = ((t0 * fw0 + t1 * fw1) + t2 * fw2) / ((fw0 * fw0 + fw1 * fw1) + fw2 * fw2);
+        wc += left_barrier(Cs.ws_infront, proj);
+        wc += right_barrier(Cs.ws_reach, sqrt((t0 * t0 + t1 * t1) + t2 * t2));
+        const double n1 = sqrt(t0 * t0 + t1 * t1);
+        const double n2 = sqrt(fw0 * fw0 + fw1 * fw1);
+        const double yaw = acos((t0 * fw0 + t1 * fw1) / n1 / n2);
+        const double ay = fabs(yaw);
+        const double yc = (Cs.yaw_c + Cs.yaw_l * fabs(ay)) + Cs.yaw_q * ay * ay;
+        wc += isnan(yaw) ? 0.0 : yc;
+        wc += left_barrier(Cs.ws_above, ee[2] - rb2);
+    }
+    double cost = 0.0;
+    cost += Cs.en_joint ? joint : 0.0;
+    cost += Cs.en_self ? Cs.self_collision : 0.0;
+    cost += Cs.en_work ? wc : 0.0;
+    if constexpr (EN) {   // energy_cost (:211-222)
+        const double E = r[REC_E];
+        cost += left_barrier(Cs.en_below, E) + right_barrier(Cs.en_above, E);
+    }
+    cost += Cs.en_vel ? vel : 0.0;
+    cost += Cs.en_traj ? trajectory_term(Cs, sc, vl) : 0.0;
+    cost += Cs.en_manip ? manipulability_term(Cs, jj) : 0.0;
+    return cost;
 }
 
 // The seven terms of AssistedManipulation::get_cost at one step record (the whole record in r), as
