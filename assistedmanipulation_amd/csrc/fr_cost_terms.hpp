@@ -152,9 +152,12 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
     // waits for the joint sums: the remaining terms start after them instead of interleaving with
     // them and holding their values live (two waves per SIMD instead of four)
     static_assert(REC_EE == 2 * FR_NB && REC_VL - REC_EE == 8, "record tail");
+    // (the dependency rides on an index, not on the pointer: an opaque pointer loses its address
+    // space, and its loads became flat_load, which wait for the LDS counter as well)
     double rest[REC_VL - REC_EE], yaw = r[REC_QQD + 4];
-    const double2 *tp = src;
-    asm volatile("" : "+v"(tp), "+v"(yaw) : "v"(joint), "v"(vel));
+    int dep = 0;
+    asm volatile("" : "+v"(dep), "+v"(yaw) : "v"(joint), "v"(vel));
+    const double2 *tp = src + dep;
 #pragma unroll
     for (int i = 0; i < (REC_VL - REC_EE) / 2; i++) {
         const double2 v = tp[REC_EE / 2 + i];
