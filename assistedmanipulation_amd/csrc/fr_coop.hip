@@ -1788,7 +1788,11 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int l
 // The update's state into LDS: from the launch's arguments with the draws made ahead, else from x0
 __device__ __forceinline__ void stage_x0(const FrRolloutArgs &a, double *Lx0)
 {
-    if ((int)threadIdx.x < MAX_X) Lx0[threadIdx.x] = a.drawn_ahead ? a.samp.x0v[threadIdx.x] : a.x0[threadIdx.x < FR_X ? threadIdx.x : 0];
+    if ((int)threadIdx.x < MAX_X) {   // (values selected, not pointers: a select of the argument block and a
+                                      // global pointer is a generic pointer, whose load waits on LDS too)
+        const double va = a.samp.x0v[threadIdx.x], vx = a.x0[threadIdx.x < FR_X ? threadIdx.x : 0];
+        Lx0[threadIdx.x] = a.drawn_ahead ? va : vx;
+    }
 }
 
 // Draws ahead (a.drawn_ahead): the eps tensor already holds this update's draws, made by
@@ -1813,21 +1817,25 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
         const int kend = sa.sp.shift_by > 0 ? (int)sa.sp.shifted : sa.H;
         const int64_t sh = sa.sp.shift_by > 0 ? sa.sp.shift_by : 0;
         constexpr int UN = 8;
+        typedef double d2v __attribute__((ext_vector_type(2)));   // (HIP's double2 kept v on the stack)
         for (int k0 = ph; k0 < kend; k0 += 4 * UN) {
-            double2 v[UN][2];
+            d2v v[UN][2];
 #pragma unroll
             for (int u = 0; u < UN; u++) {
                 const int k = k0 + 4 * u < kend ? k0 + 4 * u : ph;
-                const double2 *src = reinterpret_cast<const double2 *>(sa.prev + (((int64_t)k + sh) * sa.Rpad + lr) * FR_C + 4 * blk);
+                const d2v *src = reinterpret_cast<const d2v *>(sa.prev + (((int64_t)k + sh) * sa.Rpad + lr) * FR_C + 4 * blk);
                 v[u][0] = src[0];
                 v[u][1] = src[1];
             }
+            // past kend the loads read step ph's source and the stores rewrite step ph with it (the
+            // value its first store wrote): no branch per store, so v stays in registers (a
+            // conditional store sequence put it on the stack)
 #pragma unroll
             for (int u = 0; u < UN; u++) {
-                if (k0 + 4 * u >= kend) break;
-                double *dst = sa.noise + ((int64_t)(k0 + 4 * u) * sa.Rpad + lr) * FR_C + 4 * blk;
-                reinterpret_cast<double2 *>(dst)[0] = v[u][0];
-                reinterpret_cast<double2 *>(dst)[1] = v[u][1];
+                const int k = k0 + 4 * u < kend ? k0 + 4 * u : ph;
+                double *dst = sa.noise + ((int64_t)k * sa.Rpad + lr) * FR_C + 4 * blk;
+                reinterpret_cast<d2v *>(dst)[0] = v[u][0];
+                reinterpret_cast<d2v *>(dst)[1] = v[u][1];
             }
         }
     }

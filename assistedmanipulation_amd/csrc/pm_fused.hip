@@ -280,12 +280,15 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
             } else {
                 philox_eps(a, g, k, P.update_index, e);
             }
-            double *o = a.noise + ((int64_t)k * a.Rpad + g) * PC;
+            // (a global-space pointer: merged across the branches above, a generic one became
+            // flat stores, which the LDS waits that follow wait for as well)
+            __attribute__((address_space(1))) double *o =
+                (__attribute__((address_space(1))) double *)(a.noise + ((int64_t)k * a.Rpad + g) * PC);
 #pragma unroll
-            for (int c = 0; c < PC; c++) {
-                le[c] = e[c];
-                if (store) o[c] = e[c];
-            }
+            for (int c = 0; c < PC; c++) le[c] = e[c];
+            if (store)
+#pragma unroll
+                for (int c = 0; c < PC; c++) o[c] = e[c];
         }
     };
     if (H <= QD * IB)   // the common case straight-line: no loop header for the waits to merge at
