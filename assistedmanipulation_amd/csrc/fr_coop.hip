@@ -1335,7 +1335,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     const bool opt_row = a.optimal || frow;   // no noise (mppi.cpp:450-479)
     // U*_shifted row k is Up row min(k + ush, H - 1): with the draws made ahead (a.drawn_ahead) the
     // shift reads U* itself (mppi.cpp:197-207); the state staged in LDS (stage_x0)
-    const double *x0p = FROW && frow ? a.fx0 : Lx0;
     const double *Up = FROW && frow ? a.fU : a.Ushift;
     const int ush = FROW && frow ? 0 : a.ush;
     double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_REC;   // [rollout][step][FR_REC]
@@ -1403,9 +1402,19 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         qd = Lst[3 * lane + 1];
         E = Lst[3 * lane + 2];
     } else {
-        q = jl ? x0p[jb] : 0.0;
-        qd = jl ? x0p[FR_NB + jb] : 0.0;
-        E = EN ? x0p[FR_X - 1] : 0.0;   // EnergyTank::set_energy(state.available_energy)
+        // the folded filter() row's state from global memory, the update's from LDS: values
+        // selected, not pointers (a select of the two is a generic pointer, whose loads leave the
+        // step loop's header waiting for every store in flight, vmcnt(0))
+        double fq = 0.0, fqd = 0.0, fE = 0.0;
+        if (FROW && frow) {
+            fq = a.fx0[jb];
+            fqd = a.fx0[FR_NB + jb];
+            fE = EN ? a.fx0[FR_X - 1] : 0.0;
+        }
+        const double lq = Lx0[jb], lqd = Lx0[FR_NB + jb], lE = EN ? Lx0[FR_X - 1] : 0.0;
+        q = jl ? (FROW && frow ? fq : lq) : 0.0;
+        qd = jl ? (FROW && frow ? fqd : lqd) : 0.0;
+        E = EN ? (FROW && frow ? fE : lE) : 0.0;   // EnergyTank::set_energy(state.available_energy)
     }
     const double *grav = a.model->gravity;
     double sq, cq;
@@ -1437,6 +1446,10 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
     double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
     if (kb == 0) store_record<EN>(recp(0), j, L, q, qd, kin, E);
+    // a relay stage enters its loop with nothing in flight (its first step needs step kb's loads
+    // anyway): where the entry edge held an unknown count, the loop header waited for every store
+    // in flight on every step, the back edge's record stores included
+    if constexpr (HO == 3) __builtin_amdgcn_s_waitcnt(0);
     for (int k = kb; k < kend; k++) {
         if constexpr (PROG) __hip_atomic_store(Lprog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const double eps_l = eps_n, ub_l = ub_n;
