@@ -2,6 +2,7 @@
 driven three ways - through Trajectory.update, through the raw ctypes entry point, and as bench.py
 drives it (timing level 1 every 4th update) - printing ms/update; the engine prints its host
 stamps when each handle closes."""
+import os
 import sys
 import time
 
@@ -18,14 +19,16 @@ def make():
     return t
 
 
-def run(mode, n=200):
+def run(mode, n=int(os.environ.get("PROBE_N", "200"))):
+    # PROBE_WARM: untimed updates first (the GPU's warm-up takes ~120 updates, tools/ramp_probe.py)
+    warm = int(os.environ.get("PROBE_WARM", "10"))
     t = make()
     x = am.huddled_state()
-    for j in range(10):
+    for j in range(warm):
         t.update(x, 0.05 * j)
     f, h, ptr = t._L.mppi_update, t._h, t._state_ptr
     t._state_buf[:] = x
-    j = 10
+    j = warm
     t0 = time.perf_counter()
     for i in range(n):
         if mode == "wrapper":
