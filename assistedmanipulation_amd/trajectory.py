@@ -309,6 +309,25 @@ class Trajectory:
         self._update_last = float(time)
         self._update_count += 1
 
+    def c_update_entry(self, state):
+        """The C-ABI update entry for a caller that drives its own loop, as a C++ caller of
+        include/mppi_amd.hpp does: returns (fn, handle, state pointer), with `state` copied into
+        the handle's state buffer once; fn(handle, pointer, time) is mppi_update (mppi.cpp:154-187)
+        and returns an mppi_status (abi.MPPI_OK = 0).  Change the state by writing the buffer
+        (self.state_buffer) in place.  Skips only the Python bookkeeping of update(): the
+        rolled-out-state copy and the update count."""
+        buf = self._state_buf
+        if np.size(state) != self.X:
+            raise ValueError("state must have %d entries, got %d" % (self.X, np.size(state)))
+        np.copyto(buf, np.reshape(np.asarray(state, dtype=np.float64), -1))
+        self._rolled_out_state = buf
+        return self._L.mppi_update, self._h, self._state_ptr
+
+    @property
+    def state_buffer(self):
+        """The state buffer c_update_entry's pointer points at."""
+        return self._state_buf
+
     def set_graph(self, enable):
         """The hipGraph path of update() (mppi_set_graph): the steady-state update as one graph launch."""
         self._check(self._L.mppi_set_graph(self._h, int(bool(enable))))

