@@ -580,12 +580,18 @@ bool pm_fused_fits(int64_t R, int H) { return pm_fused_rows(R, H) != 0; }
 
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s)
 {
-    if (!pm_fused_fits(a.R, a.H)) return hipErrorInvalidValue;
-    const int PR = pm_fused_rows(a.R, a.H);
-    const unsigned nb = (unsigned)((a.R + PR - 1) / PR);
-    if (nb != a.nblocks) return hipErrorInvalidValue;   // the barrier and ticket targets assume it
+    // the handle's block count passed pm_fused_rows' residency check at create; each launch only
+    // re-derives the rows per block from it (the occupancy queries behind pm_fused_rows, three per
+    // launch, cost about a microsecond of every update's host path)
+    int PR = 0;
+    for (int p = 16; p <= 64 && !PR; p *= 2)
+        if ((a.R + p - 1) / p == (int64_t)a.nblocks) PR = p;
+    if (!PR || a.R < 4 || a.H < 1 || a.R > PM_FUSED_MAX_R || a.nblocks > PM_FUSED_MAX_BLOCKS)
+        return hipErrorInvalidValue;   // the barrier and ticket targets assume the handle's count
+    const unsigned nb = a.nblocks;
     if (a.tpart != a.gpart + (size_t)nb * a.H * PC) return hipErrorInvalidValue;   // the finisher's staging
-    const size_t lds = pm_fused_lds_bytes(a.R, a.H);
+    const size_t lds = lds_bytes(PR, a.R, a.H);
+    if (lds > 150 * 1024) return hipErrorInvalidValue;
     if (PR == 16)
         hipLaunchKernelGGL(pm_update_kernel<16>, dim3(nb), dim3(PT), lds, s, a);
     else if (PR == 32)
