@@ -2124,13 +2124,17 @@ static bool pm_fused_eligible(const mppi_handle *h)
 {
     if (h->env.pm_fused_off) return false;
     return h->dyn_kind == MPPI_DYNAMICS_POINT_MASS && h->d_pm_sync && h->noise_source == MPPI_NOISE_DEVICE_PHILOX &&
-           h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->host_trace && !h->d_trace;
+           h->tdiag && !sharded(h) && h->sg_window == 0 && h->timing <= 1 && !h->d_trace;
 }
 
 static mppi_status update_pm_fused(mppi_handle *h, const double *state, double time)
 {
     HIP_TRY(hipSetDevice(h->device));
     h->t_start = std::chrono::steady_clock::now();
+    if (h->host_trace && h->ht_n[0] > h->ht_n[1]) {   // (MPPI_HOST_TRACE, as mppi_update_phase1)
+        h->ht_sum[1] += std::chrono::duration<double, std::micro>(h->t_start - h->ht_ret).count();
+        h->ht_n[1]++;
+    }
     h->rollout_time = time;
     h->shift_by = (int64_t)((time - h->last_shift_time) / h->dt);   // sample(): shift by truncation (mppi.cpp:194-201)
     if (h->shift_by > 0) {
@@ -2202,6 +2206,10 @@ static mppi_status update_pm_fused(mppi_handle *h, const double *state, double t
         HIP_TRY(hipEventRecord(ev_r0, h->stream));
     }
     HIP_TRY(launch_pm_update(a, h->stream));
+    if (h->host_trace) {
+        h->ht_sum[2] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h->t_start).count();
+        h->ht_n[2]++;
+    }
     h->pm_epoch = a.epoch;
     if (ev_r1) HIP_TRY(hipEventRecord(ev_r1, h->stream));
     // filter() of this update is left pending (as phase 3 leaves the cooperative launch's); the next
