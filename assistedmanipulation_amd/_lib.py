@@ -64,6 +64,8 @@ PROTOTYPES = {
     "mppi_argmin": (C.c_int, [_h, _i64p]),
     "mppi_optimal_terms": (C.c_int, [_h, _dp]),
     "mppi_update_duration": (C.c_int, [_h, _dp]),
+    "mppi_update_last": (C.c_int, [_h, _dp]),
+    "mppi_device_costs_count": (C.c_int64, [_h]),
     "mppi_noise": (C.c_int, [_h, _dp]),
     "mppi_dims": (C.c_int, [_h, _i64p, _i64p, _i64p, _i64p]),
     "mppi_update_info": (C.c_int, [_h, _i64p, C.c_int]),

@@ -38,8 +38,9 @@ MPPI_NOISE_DEVICE_PHILOX = 0
 MPPI_NOISE_HOST_INJECTED = 1
 MPPI_INDEX_WIDE = 0
 MPPI_INDEX_COMPAT_UINT8 = 1
-MPPI_UPDATE_INFO_N = 10   # mppi_update_info slots (MPPI_INFO_*)
+MPPI_UPDATE_INFO_N = 13   # mppi_update_info slots (MPPI_INFO_*)
 MPPI_DEBUG_RELAY_NO_SIGNAL = 1   # mppi_debug_inject: relay stage 1 never signals stage 2
+MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL = 2   # mppi_debug_inject: the next graph captures fail to instantiate
 # EndEffectorState layout (MPPI_EE_*) and DynamicsForecast rows (MPPI_DF_*)
 MPPI_EE_POSITION, MPPI_EE_QUATERNION, MPPI_EE_ROTATION = 0, 3, 7
 MPPI_EE_LINEAR_VELOCITY, MPPI_EE_ANGULAR_VELOCITY = 16, 19

@@ -68,12 +68,14 @@ struct mppi_handle {
     hipEvent_t ev_pub = nullptr, ev_opt_done = nullptr, ev_opt_end = nullptr;
     hipEvent_t ev_dyn = nullptr;   // after the rollout (dynamics) kernel, before the cost kernel
     hipEvent_t ev_wg = nullptr;    // timing level 2: after weights_gradient_kernel (kernel_ms[6])
+    hipEvent_t ev_ar = nullptr;    // timing level 2, RCCL-sharded: after the cost all-reduce (kernel_ms[7])
     // filter() (the optimal rollout) of the last update: pending (not launched yet: it rides in the
     // next update's remainder launch, or runs alone when something needs it first), launched
     enum { OPT_NONE, OPT_PENDING, OPT_LAUNCHED, OPT_FOLDED } opt_state = OPT_NONE;
     const StepConst *opt_steps = nullptr;   // the step constants its update used
-    // sample, rollout (dynamics + cost kernels), reduce, optimal rollout, update, dynamics kernel
-    float kernel_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    // sample, rollout (dynamics + cost kernels), reduce, optimal rollout, update, dynamics kernel,
+    // the weight reduce alone, the cost all-reduce (RCCL-sharded)
+    float kernel_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // HIP-event timing on the update path (mppi_set_timing): 0 none, 1 the rollout kernel alone
     // ([5]), 2 every phase.  Each event record costs the stream a few microseconds between kernels.
     int timing = 0;
@@ -205,6 +207,9 @@ struct mppi_handle {
     };
     std::vector<GraphNode> gnodes;   // the kernel nodes whose arguments each update rewrites
     int64_t graph_updates = 0;          // updates that ran as the graph (diagnostics)
+    int64_t graph_failures = 0;         // captures that failed (the update then ran eagerly)
+    std::string graph_error;            // why the last one failed
+    int debug_graph_fail = 0;           // mppi_debug_inject(MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL, n)
     // in-launch waits that gave up (fr_coop.hip note_wait_timeout), summed over the updates
     int64_t wait_timeouts_total = 0;
     // mppi_debug_inject: fault bits for the next debug_updates rollout launches (tests only)
@@ -933,10 +938,11 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
 
     CREATE_TRY(hipSetDevice(device));
     {
-        int ncu = 0;
+        int ncu = 0, lds = 0;
         CREATE_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-        fr_coop_set_cu_count((unsigned)ncu);
-        pm_fused_set_device(device);
+        CREATE_TRY(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+        h->env.cus = (unsigned)ncu;   // this handle's device (no process-global: ADVICE r05)
+        h->env.lds_max = lds;
     }
     // the update stream at the greatest priority (its queue's dispatches go first): measured
     // 0.7-1.4 us per update faster over seven interleaved pairs at 4096x64
@@ -956,6 +962,7 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_opt_end, hipEventDisableSystemFence));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_dyn, hipEventDisableSystemFence));
     CREATE_TRY(hipEventCreateWithFlags(&h->ev_wg, hipEventDisableSystemFence));
+    CREATE_TRY(hipEventCreateWithFlags(&h->ev_ar, hipEventDisableSystemFence));
     const size_t HC = (size_t)(h->H * h->C);
     CREATE_TRY(dalloc(h, &h->d_x0, (size_t)Xd));
     CREATE_TRY(dalloc(h, &h->d_x0_opt, (size_t)Xd));
@@ -1043,8 +1050,8 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
         CREATE_TRY(dalloc(h, &h->d_pm, 1));
         CREATE_TRY(hipMemcpy(h->d_pm, &p, sizeof(p), hipMemcpyHostToDevice));
         h->pm_host = p;
-        if (h->C == 3 && h->X == 6 && pm_fused_fits(h->R, (int)h->H)) {   // the one-launch update's scratch
-            const int rows = pm_fused_rows(h->R, (int)h->H);
+        const int rows = pm_fused_rows(h->R, (int)h->H, h->env.cus, h->env.lds_max);
+        if (h->C == 3 && h->X == 6 && rows) {   // the one-launch update's scratch
             h->pm_nblocks = (unsigned)((h->R + rows - 1) / rows);
             CREATE_TRY(dalloc(h, &h->d_pm_sync, 2));
             CREATE_TRY(dalloc(h, &h->d_pm_part, (size_t)h->pm_nblocks * (HC + 1)));
@@ -1117,6 +1124,7 @@ void mppi_destroy(mppi_handle *h)
     if (h->ev_opt_end) (void)hipEventDestroy(h->ev_opt_end);
     if (h->ev_dyn) (void)hipEventDestroy(h->ev_dyn);
     if (h->ev_wg) (void)hipEventDestroy(h->ev_wg);
+    if (h->ev_ar) (void)hipEventDestroy(h->ev_ar);
     if (h->stream_opt) (void)hipStreamDestroy(h->stream_opt);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1435,6 +1443,7 @@ mppi_status mppi_step_constants(mppi_handle *h, double *out)
 }
 
 void *mppi_device_costs(mppi_handle *h) { return h ? (void *)h->d_costs : nullptr; }
+int64_t mppi_device_costs_count(mppi_handle *h) { return h ? h->R + 1 : 0; }
 void *mppi_device_gradient(mppi_handle *h) { return h ? (void *)h->d_gpart : nullptr; }
 void *mppi_stream(mppi_handle *h) { return h ? (void *)h->stream : nullptr; }
 
@@ -1899,7 +1908,11 @@ static mppi_status phase3_wait(mppi_handle *h, double seq)
     }
     if (h->timing >= 2) {
         (void)hipEventElapsedTime(&h->kernel_ms[5], h->ev[1], h->ev_dyn);
-        (void)hipEventElapsedTime(&h->kernel_ms[6], h->ev[2], h->ev_wg);   // the weight reduce alone
+        // the weight reduce alone: behind the cost all-reduce when the engine runs it (ev_ar)
+        const bool ar = h->comm != nullptr;
+        (void)hipEventElapsedTime(&h->kernel_ms[6], ar ? h->ev_ar : h->ev[2], h->ev_wg);
+        h->kernel_ms[7] = 0.0f;
+        if (ar) (void)hipEventElapsedTime(&h->kernel_ms[7], h->ev[2], h->ev_ar);
     }
     const bool all_nan = h->h_out[HC + 1] != 0.0;
     const bool sg_error = h->h_out[HC + 3] != 0.0;
@@ -2030,10 +2043,69 @@ static mppi_status allreduce_gradient(mppi_handle *h)
     return MPPI_OK;
 }
 
+// The host-side state one update's phases advance (phase 1: the shift, the swapped eps buffers, the
+// draws-ahead signature, the folded filter(); phase 3: the publish sequence, the pending filter(),
+// the next draws' signature).  A capture that fails after recording an update restores it and runs
+// the same update eagerly.
+struct UpdateSnapshot {
+    double last_shift_time, rollout_time;
+    int64_t shift_by, shifted;
+    double *noise, *noise_prev;
+    mppi_handle::AheadSig ahead;
+    bool ahead_valid;
+    int opt_state;
+    const StepConst *opt_steps;
+    StepConst *steps;
+    uint64_t publish_seq;
+};
+static UpdateSnapshot snapshot_update(const mppi_handle *h)
+{
+    return {h->last_shift_time, h->rollout_time, h->shift_by, h->shifted, h->d_noise, h->d_noise_prev,
+            h->ahead, h->ahead_valid, (int)h->opt_state, h->opt_steps, h->d_steps, h->publish_seq};
+}
+static void restore_update(mppi_handle *h, const UpdateSnapshot &u)
+{
+    h->last_shift_time = u.last_shift_time;
+    h->rollout_time = u.rollout_time;
+    h->shift_by = u.shift_by;
+    h->shifted = u.shifted;
+    h->d_noise = u.noise;
+    h->d_noise_prev = u.noise_prev;
+    h->ahead = u.ahead;
+    h->ahead_valid = u.ahead_valid;
+    h->opt_state = (decltype(h->opt_state))u.opt_state;
+    h->opt_steps = u.opt_steps;
+    h->d_steps = u.steps;
+    h->publish_seq = u.publish_seq;
+    h->phase_open = false;
+}
+
+static mppi_status update_eager(mppi_handle *h, const double *state, double time);
+
+// Capture failed after this update's launches were recorded (nothing of it ran): drop the graph for
+// good and run the same update eagerly from the restored host state.  Sharded over RCCL this keeps
+// the collectives matched - the peer ranks replay (or run eagerly) this update's two all-reduces,
+// and this rank issues the same two in the same order - instead of leaving them blocked in the first.
+static mppi_status graph_capture_failed(mppi_handle *h, const UpdateSnapshot &u, hipGraph_t g, const double *state, double time,
+                                        const std::string &why)
+{
+    if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+    if (g) (void)hipGraphDestroy(g);
+    h->graph_exec = nullptr;
+    h->graph = nullptr;
+    h->gnodes.clear();
+    h->graph_mode = 0;   // never again: the eager path from here on
+    h->graph_failures++;
+    h->graph_error = why;
+    restore_update(h, u);
+    return update_eager(h, state, time);
+}
+
 static mppi_status update_graph(mppi_handle *h, const double *state, double time)
 {
     const bool capture = h->graph_exec == nullptr;
     const bool coll = h->comm != nullptr;
+    const UpdateSnapshot snap = snapshot_update(h);
     if (capture) HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     else h->graph_dry = true;
     mppi_status st = mppi_update_phase1(h, state, time);
@@ -2046,18 +2118,39 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
     if (capture) {
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(h->stream, &g);
-        if (st != MPPI_OK || e != hipSuccess) {
+        if (st != MPPI_OK) {   // a phase failed before its launches: as the eager path would
             if (g) (void)hipGraphDestroy(g);
-            h->graph_mode = 0;   // never again: the eager path from here on
-            if (st != MPPI_OK) return st;
-            HIP_TRY(e);
-        }
-        h->graph = g;
-        HIP_TRY(hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0));
-        st = graph_nodes(h);
-        if (st != MPPI_OK) {
             h->graph_mode = 0;
             return st;
+        }
+        if (e != hipSuccess)
+            return graph_capture_failed(h, snap, g, state, time, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        hipError_t ie = hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0);
+        if (ie == hipSuccess && h->debug_graph_fail > 0) {   // mppi_debug_inject(MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL)
+            h->debug_graph_fail--;
+            ie = hipErrorOutOfMemory;
+        }
+        if (ie != hipSuccess) {
+            if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+            h->graph_exec = nullptr;
+            return graph_capture_failed(h, snap, g, state, time, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        }
+        h->graph = g;
+        st = graph_nodes(h);
+        if (st != MPPI_OK) {
+            // the instantiated graph holds this update as captured (its collectives included): run it
+            // once, then drop it - the next updates are eager, with the same collectives in order
+            h->graph_error = h->err;
+            h->graph_failures++;
+            const hipError_t le = hipGraphLaunch(h->graph_exec, h->stream);
+            (void)hipGraphExecDestroy(h->graph_exec);
+            (void)hipGraphDestroy(h->graph);
+            h->graph_exec = nullptr;
+            h->graph = nullptr;
+            h->gnodes.clear();
+            h->graph_mode = 0;
+            HIP_TRY(le);
+            return phase3_wait(h, seq);
         }
     } else {
         if (st != MPPI_OK) return st;
@@ -2089,7 +2182,11 @@ static mppi_status update_graph(mppi_handle *h, const double *state, double time
 
 mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates)
 {
-    if (!h || fault < 0 || fault > MPPI_DEBUG_RELAY_NO_SIGNAL || updates < 0) return MPPI_ERR_INVALID;
+    if (!h || fault < 0 || fault > MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL || updates < 0) return MPPI_ERR_INVALID;
+    if (fault == MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL) {   // a host-side fault: no launch carries it
+        h->debug_graph_fail = updates;
+        return MPPI_OK;
+    }
     h->debug_flags = fault;
     h->debug_updates = updates;
     return MPPI_OK;
@@ -2252,10 +2349,16 @@ mppi_status mppi_update(mppi_handle *h, const double *state, double time)
     if (h && state && pm_fused_eligible(h)) return update_pm_fused(h, state, time);
     if (h) h->info[MPPI_INFO_FUSED_UPDATE] = 0;
     if (h && state && graph_eligible(h)) return update_graph(h, state, time);
+    return update_eager(h, state, time);
+}
+
+static mppi_status update_eager(mppi_handle *h, const double *state, double time)
+{
     if (h && sharded(h) && !h->comm) return fail(h, MPPI_ERR_COMM, "sharded handle without communicator: use the phase-split API");
     mppi_status st = mppi_update_phase1(h, state, time);
     if (st != MPPI_OK) return st;
     if (sharded(h) && (st = allreduce_costs(h)) != MPPI_OK) return st;
+    if (h->comm && h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_ar, h->stream));
     st = mppi_update_phase2(h);
     if (st != MPPI_OK) return st;
     if (sharded(h) && (st = allreduce_gradient(h)) != MPPI_OK) return st;
@@ -2391,6 +2494,13 @@ mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout)
     return MPPI_OK;
 }
 
+mppi_status mppi_update_last(mppi_handle *h, double *time)
+{
+    if (!h || !time) return MPPI_ERR_INVALID;
+    *time = h->update_last;
+    return MPPI_OK;
+}
+
 mppi_status mppi_update_duration(mppi_handle *h, double *seconds)
 {
     if (!h || !seconds) return MPPI_ERR_INVALID;
@@ -2424,6 +2534,9 @@ mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n)
         h->info[MPPI_INFO_HANDOVER] = w;
     }
     h->info[MPPI_INFO_WAIT_TIMEOUTS_TOTAL] = h->wait_timeouts_total;
+    h->info[MPPI_INFO_GRAPH_UPDATES] = h->graph_updates;
+    h->info[MPPI_INFO_GRAPH_FAILURES] = h->graph_failures;
+    h->info[MPPI_INFO_UPDATE_COUNT] = (int64_t)h->update_count;
     std::memcpy(info, h->info, (size_t)n * sizeof(int64_t));
     return MPPI_OK;
 }
@@ -2479,7 +2592,7 @@ mppi_status mppi_set_timing(mppi_handle *h, int level)
 
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n)
 {
-    if (!h || !ms || n < 0 || n > 7) return MPPI_ERR_INVALID;
+    if (!h || !ms || n < 0 || n > 8) return MPPI_ERR_INVALID;
     if (h->opt_state == mppi_handle::OPT_LAUNCHED && hipEventQuery(h->ev_opt_end) == hipSuccess)
         (void)hipEventElapsedTime(&h->kernel_ms[3], h->ev[4], h->ev_opt_end);
     if (h->ring_unread) {   // level 1: the newest recorded pair

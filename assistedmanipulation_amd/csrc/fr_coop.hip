@@ -1988,9 +1988,9 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 namespace mppi_eng {
 
-static unsigned g_cu_count = 256;   // set by fr_coop_set_cu_count (hipDeviceProp multiProcessorCount)
-
-void fr_coop_set_cu_count(unsigned n) { g_cu_count = n ? n : 256; }
+// The device's CU count is the handle's (EnvSwitches::cus, hipDeviceAttributeMultiprocessorCount
+// at create): one round of workgroups is one per CU
+static int64_t cu_count(const EnvSwitches &env) { return env.cus ? (int64_t)env.cus : 256; }
 
 // Dynamic LDS that lifts a multi-wave workgroup above half of the CU's 160 KiB, so that the
 // dispatcher places one workgroup per CU (one wave per SIMD) whatever the kernel's static LDS
@@ -2057,10 +2057,10 @@ bool fr_coop_costs_in_launch(const EnvSwitches &env) { return !env.costs_in_laun
 bool fr_coop_update_split(int64_t count, const EnvSwitches &env)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
-    const int64_t round = (int64_t)g_cu_count * WG_ROWS;
+    const int64_t round = cu_count(env) * WG_ROWS;
     if (count <= 2 * round || env.split_off) return false;
     const int64_t rest = count - round, gb = rest / WG_ROWS, xb = rest - gb * WG_ROWS + 1;   // + a folded filter() row
-    return gb > 0 && gb <= (int64_t)g_cu_count && xb <= gb * ROWS_PER_WAVE;
+    return gb > 0 && gb <= cu_count(env) && xb <= gb * ROWS_PER_WAVE;
 }
 
 // Whether launch_fr_coop_update runs rounds of four-wave groups (the launches that can sample
@@ -2069,7 +2069,7 @@ bool fr_coop_update_fusable(int64_t count, const EnvSwitches &env)
 {
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, xrows = count - groups * WG_ROWS + 1;   // + a folded filter() row
-    return (groups > 0 && groups <= (int64_t)g_cu_count && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count, env);
+    return (groups > 0 && groups <= cu_count(env) && xrows <= groups * ROWS_PER_WAVE) || fr_coop_update_split(count, env);
 }
 
 bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env)
@@ -2078,7 +2078,7 @@ bool fr_coop_update_folds(int64_t count, int H, const EnvSwitches &env)
     if (fr_coop_update_split(count, env)) return true;
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     const int64_t groups = count / WG_ROWS, extra = count - groups * WG_ROWS;
-    return extra > 0 && groups > 0 && groups <= (int64_t)g_cu_count && extra + 1 <= groups * ROWS_PER_WAVE;
+    return extra > 0 && groups > 0 && groups <= cu_count(env) && extra + 1 <= groups * ROWS_PER_WAVE;
 }
 
 bool fr_coop_is_update_kernel(const void *f)
@@ -2125,7 +2125,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
     constexpr int64_t WG_ROWS = 4 * ROWS_PER_WAVE;
     *folded = false;
     if (fr_coop_update_split(a0.count, env)) {   // two launches: one round of full groups, then the rest
-        const int64_t n0 = (int64_t)g_cu_count * WG_ROWS, rest = a0.count - n0;
+        const int64_t n0 = cu_count(env) * WG_ROWS, rest = a0.count - n0;
         FrRolloutArgs a = a0;
         a.costs_in_launch = !env.costs_in_launch_off && a.H <= HC_MAX ? 1 : 0;
         a.handover = env.handover_off ? 0 : 1;
@@ -2148,7 +2148,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
         if (tail) *tail = CoopTail{n0, n0 + B.xbase, (int)((B.xrows + 3) / 4), 2};
         if (dry) return hipSuccess;
         if (e0) (void)hipEventRecord(e0, s);
-        launch_x_any(A, (unsigned)g_cu_count, s);
+        launch_x_any(A, (unsigned)cu_count(env), s);
         launch_x_any(B, (unsigned)gb, s);
         if (e1) (void)hipEventRecord(e1, s);
         return hipGetLastError();
@@ -2159,7 +2159,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
     const bool frow = a0.fcost != nullptr && extra > 0;
     const int64_t xrows = extra + (frow ? 1 : 0);
     FrRolloutArgs a = a0;
-    if (groups == 0 || groups > (int64_t)g_cu_count || xrows > groups * ROWS_PER_WAVE) {
+    if (groups == 0 || groups > cu_count(env) || xrows > groups * ROWS_PER_WAVE) {
         if (a.drawn_ahead) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;

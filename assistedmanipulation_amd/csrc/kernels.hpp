@@ -302,7 +302,6 @@ static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
-void fr_coop_set_cu_count(unsigned n);   // the device's CU count (the split leaves one CU to the remainder)
 // The update's rollouts (fr_coop_x_kernel): one workgroup per CU of four one-SIMD waves of rollouts
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
@@ -332,6 +331,11 @@ bool fr_coop_costs_in_launch(const EnvSwitches &env);   // the objective runs in
 // the update path (~80 ns each)
 struct EnvSwitches {
     bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off;
+    // the handle's device: its CU count (the rollout launches' rounds of workgroups) and LDS per
+    // block (the fused point mass's residency check), set at create for that device - per handle, so
+    // that handles created on different devices from several threads never read each other's
+    unsigned cus;
+    int lds_max;
 };
 EnvSwitches env_switches_read();
 // Whether a pending filter() folds into the update launch of `count` rows with the objective in
@@ -385,10 +389,9 @@ constexpr int PM_FUSED_MAX_BLOCKS = 256;          // one per CU: the grid barrie
 // rollouts per block: the fewest of 16, 32, 64 whose grid (at most 256 blocks) and LDS (the
 // finisher stages every block's partials) fit, so that the rank and the draws spread over the most
 // CUs; 0 when none does
-// (every block must be resident at once for the in-launch grid barrier: pm_fused_set_device gives
-// the device's CUs and LDS, and a shape that does not fit takes the five launches)
-int pm_fused_rows(int64_t R, int H);
-void pm_fused_set_device(int device);
+// (every block must be resident at once for the in-launch grid barrier: the handle's device's CUs
+// and LDS per block (EnvSwitches::cus, lds_max), and a shape that does not fit takes the five launches)
+int pm_fused_rows(int64_t R, int H, unsigned cus, int lds_max);
 struct PmFusedArgs {
     DevPointMass pm;
     const StepConst *steps;     // [H] gamma_k
@@ -428,8 +431,6 @@ struct PmFusedArgs {
 // entry, sampled, rolled out (costs folded into the statistics), barrier passed, partials stored,
 // ticket taken, staged, (finisher:) stored, published, ranked, end, costs computed
 constexpr int PM_STAMPS = 12;
-bool pm_fused_fits(int64_t R, int H);
-size_t pm_fused_lds_bytes(int64_t R, int H);
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);
 // AssistedManipulation's seven per-term totals of one rollout from its [H][FR_REC] records
 hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s);

@@ -534,49 +534,28 @@ static size_t lds_bytes(int PR, int64_t R, int H)
 }
 
 // The in-launch grid barrier needs every block resident at once: the most blocks of each variant
-// the device holds together (occupancy per CU at the variant's LDS, times the CUs), set at create
-// (pm_fused_set_device); until then the grid's bound alone
-static int g_pm_cus = 0, g_pm_lds_max = 0;
-
-static int resident_blocks(int PR, size_t lds)
+// the device holds together (occupancy per CU at the variant's LDS, times the handle's CUs)
+static int resident_blocks(int PR, size_t lds, unsigned cus, int lds_max)
 {
-    if (g_pm_cus <= 0) return PM_FUSED_MAX_BLOCKS;
-    if (lds > (size_t)g_pm_lds_max) return 0;
+    if (cus == 0 || lds > (size_t)lds_max) return 0;
     int per_cu = 0;
     hipError_t e = hipErrorInvalidValue;
     if (PR == 16) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<16>, PT, lds);
     else if (PR == 32) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<32>, PT, lds);
     else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pm_update_kernel<64>, PT, lds);
-    return e == hipSuccess ? per_cu * g_pm_cus : 0;
+    return e == hipSuccess ? per_cu * (int)cus : 0;
 }
 
-void pm_fused_set_device(int device)
-{
-    int cus = 0, lds = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
-    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 0;
-    g_pm_cus = cus;
-    g_pm_lds_max = lds;
-}
-
-int pm_fused_rows(int64_t R, int H)
+int pm_fused_rows(int64_t R, int H, unsigned cus, int lds_max)
 {
     if (R < 4 || H < 1 || R > PM_FUSED_MAX_R) return 0;
     for (int PR = 16; PR <= 64; PR *= 2) {
         const int64_t nb = (R + PR - 1) / PR;
         const size_t lds = lds_bytes(PR, R, H);
-        if (nb <= PM_FUSED_MAX_BLOCKS && lds <= 150 * 1024 && nb <= resident_blocks(PR, lds)) return PR;
+        if (nb <= PM_FUSED_MAX_BLOCKS && lds <= 150 * 1024 && nb <= resident_blocks(PR, lds, cus, lds_max)) return PR;
     }
     return 0;
 }
-
-size_t pm_fused_lds_bytes(int64_t R, int H)
-{
-    const int PR = pm_fused_rows(R, H);
-    return PR ? lds_bytes(PR, R, H) : 0;
-}
-
-bool pm_fused_fits(int64_t R, int H) { return pm_fused_rows(R, H) != 0; }
 
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s)
 {

@@ -170,6 +170,15 @@ def comm_unique_id():
     return buf.raw
 
 
+class CUpdateEntry(tuple):
+    """(fn, handle, state pointer) of Trajectory.c_update_entry, holding the Trajectory alive."""
+
+    def __new__(cls, items, trajectory):
+        t = super().__new__(cls, items)
+        t.trajectory = trajectory
+        return t
+
+
 class Trajectory:
     """mppi::Trajectory (mppi.hpp:267-658) on one MI355X device."""
 
@@ -186,8 +195,6 @@ class Trajectory:
         self._rolled_out_state[:] = 0.0   # m_rollout_state.setZero() (mppi.cpp:121)
         self._state_buf = np.zeros(self.X, dtype=np.float64)
         self._state_ptr = _p(self._state_buf)
-        self._update_last = 0.0
-        self._update_count = 0
 
     @staticmethod
     def create(configuration: Configuration, dynamics: Dynamics, cost: Cost, device=0):
@@ -306,22 +313,23 @@ class Trajectory:
         if st != abi.MPPI_OK:
             self._check(st)
         self._rolled_out_state = buf   # copied when queried (get_rolled_out_state)
-        self._update_last = float(time)
-        self._update_count += 1
 
     def c_update_entry(self, state):
         """The C-ABI update entry for a caller that drives its own loop, as a C++ caller of
         include/mppi_amd.hpp does: returns (fn, handle, state pointer), with `state` copied into
         the handle's state buffer once; fn(handle, pointer, time) is mppi_update (mppi.cpp:154-187)
         and returns an mppi_status (abi.MPPI_OK = 0).  Change the state by writing the buffer
-        (self.state_buffer) in place.  Skips only the Python bookkeeping of update(): the
-        rolled-out-state copy and the update count."""
+        (self.state_buffer) in place.  The update count and time live in the engine
+        (get_update_count / get_update_last read them), so updates made through it count.
+        Lifetime: the handle and the pointer are this Trajectory's; the returned entry holds a
+        reference to it (entry.trajectory), so keep the entry - or the Trajectory - alive while
+        calling fn (after close() or garbage collection the handle is freed)."""
         buf = self._state_buf
         if np.size(state) != self.X:
             raise ValueError("state must have %d entries, got %d" % (self.X, np.size(state)))
         np.copyto(buf, np.reshape(np.asarray(state, dtype=np.float64), -1))
         self._rolled_out_state = buf
-        return self._L.mppi_update, self._h, self._state_ptr
+        return CUpdateEntry((self._L.mppi_update, self._h, self._state_ptr), self)
 
     @property
     def state_buffer(self):
@@ -354,8 +362,6 @@ class Trajectory:
 
     def update_phase3(self, time):
         self._check(self._L.mppi_update_phase3(self._h))
-        self._update_last = float(time)
-        self._update_count += 1
 
     def device_costs_ptr(self):
         return self._L.mppi_device_costs(self._h)
@@ -390,10 +396,18 @@ class Trajectory:
         return d.value
 
     def get_update_last(self):
-        return self._update_last
+        """Trajectory::get_update_last: the engine's own (every update entry counts)."""
+        d = C.c_double()
+        self._check(self._L.mppi_update_last(self._h, C.byref(d)))
+        return d.value
 
     def get_update_count(self):
-        return self._update_count
+        """Trajectory::get_update_count: the engine's count of successful updates."""
+        return self.update_info()["update_count"]
+
+    def device_costs_count(self):
+        """Doubles of device_costs_ptr() a phase-split caller all-reduces (R + 1)."""
+        return int(self._L.mppi_device_costs_count(self._h))
 
     def get_rollout_count(self):
         return self.R
@@ -454,7 +468,8 @@ class Trajectory:
         out = np.zeros(abi.MPPI_UPDATE_INFO_N, dtype=np.int64)
         self._check(self._L.mppi_update_info(self._h, out.ctypes.data_as(C.POINTER(C.c_int64)), out.size))
         keys = ("cooperative", "folded_filter", "objective_in_launch", "tail_draws", "sampling", "rows", "handover",
-                "wait_timeouts", "wait_timeouts_total", "fused_update")
+                "wait_timeouts", "wait_timeouts_total", "fused_update", "graph_updates", "graph_failures",
+                "update_count")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def debug_inject(self, fault, updates=1):
@@ -496,11 +511,12 @@ class Trajectory:
         """[sample, rollout, weight-reduce, optimal rollout, whole update] in ms (HIP events).
         wait=False does not wait for the overlapped optimal rollout ([3] may be an earlier one's).
         detail=True appends [5], the rollout (dynamics) kernel alone ([1] also spans the cost kernel),
-        and [6], the weights + gradient launch alone ([2] also spans the finish kernel; timing level
-        2); it implies wait=False."""
+        [6], the weights + gradient launch alone ([2] also spans the finish kernel; timing level
+        2), and [7], the cost all-reduce ahead of it (RCCL-sharded; 0 otherwise); it implies
+        wait=False."""
         if detail:
-            out = (C.c_float * 7)()
-            self._check(self._L.mppi_kernel_times_detail(self._h, out, 7))
+            out = (C.c_float * 8)()
+            self._check(self._L.mppi_kernel_times_detail(self._h, out, 8))
             return list(out)
         out = (C.c_float * 5)()
         fn = self._L.mppi_kernel_times if wait else self._L.mppi_kernel_times_nowait

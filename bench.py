@@ -57,6 +57,7 @@ BYTES_SURVEY_PM = 2 * 3 * 8.0     # 48 B (point mass, C = 3)
 BYTES_EPS_FR = 96.0
 BYTES_REC = 768.0   # the stored step record (kernels.hpp FR_REC; 336 B until r05)
 EV_EVERY = 8   # timed updates per rollout-kernel event sample
+EV_GRAPH = 16  # --graph 1: eager updates after the timed loop whose rollout launches are timed
 PMC_JSON = os.path.join(HERE, "profiles", "r05", "final", "pmc_rollout.json")
 PMC_WG_JSON = os.path.join(HERE, "profiles", "r05", "final", "pmc_weights.json")   # weights_gradient_kernel's traffic
 PMC_PM_JSON = os.path.join(HERE, "profiles", "r05", "final", "pmc_pm.json")      # pm_update_kernel's traffic
@@ -92,6 +93,10 @@ def parse():
     p.add_argument("--cpu-warmup", type=int, default=5, help="untimed CPU warm-up updates, BASELINE.md §2")
     p.add_argument("--graph", type=int, default=-1,
                    help="1: the hipGraph update path (mppi_set_graph), 0: eager launches, -1: the engine's default")
+    p.add_argument("--comm1", type=int, default=0,
+                   help="1 (N = 1 only): run the sharded update through a one-rank RCCL communicator "
+                        "(mppi_comm_init(1, 0)): the cost and gradient all-reduces, and with --graph 1 the "
+                        "captured graph with RCCL's nodes, timed on one GPU")
     a = p.parse_args()
     pm = a.workload == "point_mass"
     if a.samples_per_gpu is None:
@@ -141,7 +146,7 @@ def time_oracle(libpath, conf, dyn, cost, updates, warmup, compat_uint8=0, forec
     return float(np.median(durs)), float(np.percentile(durs, 90)), orc.H
 
 
-def cpu_baseline(args, pm):
+def cpu_baseline(args, pm, world=1):
     """The oracle (fp64 restatement of the reference's CPU mppi.cpp path, Pinocchio-order
     arithmetic, contiguous-block thread partition of mppi.cpp:272-307) on this host, g++ -O3
     -march=native: the bench's workload at the process's CPU share (WIDE indices: R > 255 hangs
@@ -153,7 +158,12 @@ def cpu_baseline(args, pm):
     except Exception:
         libpath = O.LIB_PATH
     threads = args.cpu_threads or cpu_share()
-    S, H = args.samples_per_gpu, args.horizon_steps
+    S, H = args.samples_per_gpu * world, args.horizon_steps   # the whole job's workload
+    # bounded: the configured updates at configs[2]'s size, scaled down for larger workloads (about
+    # 10-30 s of CPU work at 16 threads), at least 3 timed and 1 warm-up
+    scale = (4096.0 * 64) / (S * H)
+    updates = args.cpu_updates if scale >= 1 else max(3, int(args.cpu_updates * scale))
+    warm = args.cpu_warmup if scale >= 1 else max(1, int(args.cpu_warmup * scale))
     if pm:
         conf = am.point_mass_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=KEEP_BEST)
         conf.threads = threads
@@ -162,17 +172,17 @@ def cpu_baseline(args, pm):
         conf = am.frankaridgeback_configuration(rollouts=S, horison=H * 0.01, keep_best_rollouts=KEEP_BEST,
                                                 threads=threads)
         dyn, cost = am.FrankaRidgebackDynamics(), am.AssistedManipulation()
-    med, p90, Ho = time_oracle(libpath, conf, dyn, cost, args.cpu_updates, args.cpu_warmup, forecast=not pm)
+    med, p90, Ho = time_oracle(libpath, conf, dyn, cost, updates, warm, forecast=not pm)
     nproc = os.cpu_count() or 0
     out = {"value": S * Ho / med, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
-           "median_s_per_update": med, "p90_s_per_update": p90, "warmup_updates": args.cpu_warmup,
-           "timed_updates": args.cpu_updates, "process_cpu_share": cpu_share(), "host_nproc": nproc,
+           "median_s_per_update": med, "p90_s_per_update": p90, "warmup_updates": warm,
+           "timed_updates": updates, "process_cpu_share": cpu_share(), "host_nproc": nproc,
            "cpu_model": cpu_model(),
            "sample": "%d warm-up + %d timed updates of the %dx%d %s workload (BASELINE.md §2), "
                      "oracle/mppi_oracle.cpp fp64, g++ -O3 -march=native, %d threads: the process's CPU share "
                      "(affinity mask capped by OMP_NUM_THREADS), not the host's nproc %d, which the GPU box "
                      "shares between its GPUs; host %s" % (
-                         args.cpu_warmup, args.cpu_updates, S, Ho, "point-mass" if pm else "FrankaRidgeback",
+                         warm, updates, S, Ho, "point-mass" if pm else "FrankaRidgeback",
                          threads, nproc, cpu_model())}
     if not pm:   # configs[0]: the reference's own plumbing case, single thread, uint8 indices
         c0 = am.frankaridgeback_configuration(rollouts=128, horison=0.32, keep_best_rollouts=KEEP_BEST, threads=1)
@@ -182,7 +192,24 @@ def cpu_baseline(args, pm):
                            "median_s_per_update": m0, "p90_s_per_update": q0,
                            "warmup_updates": args.cpu_warmup, "timed_updates": args.cpu_updates,
                            "workload": "128 x 32 FrankaRidgeback, single thread, uint8 index semantics (BASELINE configs[0])"}
+    if world > 1:
+        out["sample"] += "; the whole %d-rank job's workload, on rank 0 after the timed loop" % world
     return out
+
+
+def workload_label(pm, S_total, H, smoothing, world, graph):
+    """The BASELINE.json config a run's shape is (the prefix of config.workload), or "" for another
+    shape.  configs[2] is 4096 x 64 per GPU (weak at N > 1), configs[3] 32768 x 64 in all,
+    configs[4] 65536 x 128 with the Savitzky-Golay filter (window 10) and the captured graph."""
+    if pm:
+        return "BASELINE configs[1]: " if (S_total == 1024 and H == 32) else ""
+    if S_total == 32768 and H == 64 and not smoothing:
+        return "BASELINE configs[3]: "
+    if S_total == 65536 and H == 128 and smoothing == 10:
+        return "BASELINE configs[4]%s: " % ("" if graph == 1 else " (eager launches, not the hipGraph)")
+    if S_total == 4096 * world and H == 64 and not smoothing:
+        return "BASELINE configs[2]: " if world == 1 else "BASELINE configs[2]'s 4096 x 64 per GPU (weak): "
+    return ""
 
 
 def launch_ranks(n):
@@ -280,37 +307,46 @@ def run(args, world, rank, local_rank, dist):
     import assistedmanipulation_amd as am_  # the engine's ROCm runtime loads here, in the rank process
     from assistedmanipulation_amd import abi as abi_
     am, abi = am_, abi_
+    create, unique_id = am.Trajectory.create, am.comm_unique_id
+    if os.environ.get("MPPI_BENCH_STUB_ENGINE") == "1":   # CPU schema test: a stand-in engine (tests/bench_stub.py)
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import bench_stub
+        create, unique_id = bench_stub.creator(world, rank), bench_stub.comm_unique_id
     pm = args.workload == "point_mass"
     S_total = args.samples_per_gpu * world
     horison = args.horizon_steps * 0.01
     sg = am.Smoothing(args.smoothing, 1) if (args.smoothing > 0 and not pm) else None
     if pm:
         conf = am.point_mass_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST)
-        traj = am.Trajectory.create(conf, am.PointMassDynamics(), am.QuadraticCost(), device=local_rank)
+        traj = create(conf, am.PointMassDynamics(), am.QuadraticCost(), device=local_rank)
         default_workload = args.samples_per_gpu == 1024 and args.horizon_steps == 32
-        cfg_index = 1
         x = np.zeros(6)
     else:
         conf = am.frankaridgeback_configuration(rollouts=S_total, horison=horison, keep_best_rollouts=KEEP_BEST,
                                                 smoothing=sg)
-        traj = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
+        traj = create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation(), device=local_rank)
+        # the shape the recorded PMC traffic was collected on (4096 x 64 per GPU, no filter)
         default_workload = args.samples_per_gpu == SAMPLES_PER_GPU and args.horizon_steps == 64 and sg is None
-        cfg_index = 2 if world == 1 else 3
         x = am.huddled_state()
     if traj is None:
         raise SystemExit("engine create failed")
+    comm1 = world == 1 and args.comm1 == 1
     if world > 1:
-        uid = [am.comm_unique_id() if rank == 0 else None]
+        uid = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         traj.comm_init(world, rank, uid[0])
         infos = [None] * world
         dist.all_gather_object(infos, traj.comm_info())
     else:
+        if comm1:   # the sharded path on one GPU: a one-rank RCCL communicator
+            traj.comm_init(1, 0, unique_id())
         try:
             infos = [traj.comm_info()]
         except AttributeError:   # an older library under an A/B run (MPPI_AMD_LIB) lacks mppi_comm_info
             infos = [{"nranks": 0, "rank": -1, "device": local_rank, "pci_bus_id": "unknown"}]
     rccl = rccl_check(infos, world)   # (every rank checks: a bad run stops before the timed loop)
+    if comm1 and infos[0]["nranks"] != 1:
+        sys.exit("bench.py: --comm1 but the engine reports %d communicator ranks" % infos[0]["nranks"])
     traj.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
     if args.graph >= 0:
         traj.set_graph(args.graph)
@@ -318,9 +354,16 @@ def run(args, world, rank, local_rank, dist):
         traj.set_forecast(am.constant_forecast(traj.H))
     traj.set_timing(1)   # creates the engine's timing-event ring outside the timed region
     traj.set_timing(0)
+    # HIP events around the rollout kernel on every EV_EVERY-th update of the timed region (each
+    # event record delays the next kernel on the stream by ~4.5 us; the kernel's duration does not
+    # vary, so a sample of the launches gives its average).  The engine keeps the event pairs and
+    # they are read after the timed region (mppi_rollout_kernel_times).  The graph path replays only
+    # updates without timing events, so with --graph 1 the timed loop records none and the rollout
+    # launch is timed over EV_GRAPH further (eager) updates after it.
+    sample_events = args.graph != 1
     j = 0
     for i in range(args.warmup):   # the timed loop's pattern (first event records happen here)
-        sampled = i % EV_EVERY == 0
+        sampled = sample_events and i % EV_EVERY == 0
         if sampled:
             traj.set_timing(1)
         traj.update(x, 0.05 * j)
@@ -329,20 +372,17 @@ def run(args, world, rank, local_rank, dist):
         j += 1
     if dist:
         dist.barrier()
-    # HIP events around the rollout kernel on every EV_EVERY-th update of the timed region (each
-    # event record delays the next kernel on the stream by ~4.5 us; the kernel's duration does not
-    # vary, so a sample of the launches gives its average).  The engine keeps the event pairs and
-    # they are read after the timed region (mppi_rollout_kernel_times).
     traj.rollout_kernel_times()    # clear the record
     g0 = traj.graph_updates()
     # the timed loop calls the C-ABI entry mppi_update itself (what a C++ caller of mppi_amd.hpp
     # calls), the constant state in the handle's buffer once, instead of Trajectory.update's
     # per-call copy and bookkeeping (≈0.7-1.3 us per update, tools/host_loop_probe.py)
-    upd, hnd, sptr = traj.c_update_entry(x)
+    entry = traj.c_update_entry(x)   # (holds traj alive)
+    upd, hnd, sptr = entry
     ok = abi.MPPI_OK
     t0 = time.perf_counter()
     for i in range(args.steps):
-        sampled = i % EV_EVERY == 0
+        sampled = sample_events and i % EV_EVERY == 0
         if sampled:
             traj.set_timing(1)
         st = upd(hnd, sptr, 0.05 * j)   # returns once U* is published; filter() overlaps the next update
@@ -353,13 +393,22 @@ def run(args, world, rank, local_rank, dist):
         j += 1
     traj.synchronize()             # the last update's filter() finishes inside the timed region
     elapsed = time.perf_counter() - t0
-    dyn_times = traj.rollout_kernel_times()   # the rollout kernel's HIP-event times, sampled updates
+    graph_timed = traj.graph_updates() - g0   # updates of the timed loop that ran as the hipGraph
     info = traj.update_info()      # what the engine's rollout launch did (its own choice, not re-derived)
-    info["graph_updates_timed"] = traj.graph_updates() - g0   # updates of the timed loop that ran as the hipGraph
+    info["graph_updates_timed"] = graph_timed
+    ev_source = "HIP events on every %d-th timed update" % EV_EVERY
+    if not sample_events:   # the graph path: the rollout launch timed over further eager updates
+        traj.set_timing(1)
+        for _ in range(EV_GRAPH):
+            traj.update(x, 0.05 * j)
+            j += 1
+        traj.set_timing(0)
+        ev_source = "HIP events over %d eager updates after the timed (graph) loop" % EV_GRAPH
+    dyn_times = traj.rollout_kernel_times()   # the rollout kernel's HIP-event times, sampled updates
     dyn_ms = sum(dyn_times) / max(len(dyn_times), 1)
     # the per-phase breakdown from a few further updates with every event recorded (untimed)
     traj.set_timing(2)
-    kt = np.zeros(7)
+    kt = np.zeros(8)
     nb = 5
     for _ in range(nb):
         traj.update(x, 0.05 * j)
@@ -407,10 +456,13 @@ def run(args, world, rank, local_rank, dist):
         flops_unit = FLOPS_PER_ROLLOUT_STEP if in_launch else FLOPS_DYN_PER_ROLLOUT_STEP
         rows_units = info["rows"] * traj.H   # rollout rows of the launch (+ a folded filter() row)
         achieved_tflops = flops_unit * rows_units / (dyn_ms * 1e-3) / 1e12
-        traffic = None
-        if os.path.exists(PMC_JSON) and world == 1 and default_workload:
+        traffic, traffic_note = None, None
+        if os.path.exists(PMC_JSON) and default_workload and not comm1:
             with open(PMC_JSON) as f:
                 traffic = json.load(f)["traffic_bytes"]
+            if world > 1:   # rank 0's launch holds its 4096-4097 rollouts + the folded filter() row
+                traffic_note = ("recorded for the N = 1 launch of 4099 rows; rank 0's launch here has %d rows"
+                                % info["rows"])
         # the launch's HBM bytes by design: eps read, step records written and (objective in the
         # launch) read back, the next update's eps written in the tail (tail draws)
         launch_bytes = ((BYTES_EPS_FR + BYTES_REC * (2 if in_launch else 1)) * rows_units
@@ -423,7 +475,10 @@ def run(args, world, rank, local_rank, dist):
                     "traffic_source": recorded_label(PMC_JSON),
                     "flops_per_rollout_step": flops_unit,
                     "launch_bytes_by_design": launch_bytes,
-                    "launch_GBs_by_design": launch_bytes / (dyn_ms * 1e-3) / 1e9}
+                    "launch_GBs_by_design": launch_bytes / (dyn_ms * 1e-3) / 1e9,
+                    "launch_time_source": ev_source}
+        if traffic_note:
+            roofline["traffic_note"] = traffic_note
         survey_bytes = BYTES_SURVEY_FR
     # SURVEY §8(d)'s algorithmic bytes per update (eps written once + read once by the reduce, fp64)
     # over the whole update's time: the HBM view of the metric; what the design moves beyond it (the
@@ -437,16 +492,20 @@ def run(args, world, rank, local_rank, dist):
                                                "step_record_round_trip": 2 * BYTES_REC if info["objective_in_launch"] else BYTES_REC}
     # the weight reduce (weights_gradient_kernel): the HBM-bound kernel of the path - it reads the
     # [H][R][C] eps tensor once (96 B per rollout-step, fp64) and the costs; HIP events around it
-    # alone in the untimed breakdown updates (kt[6]), PMC traffic from the profile set
+    # alone in the untimed breakdown updates (kt[6]: behind the cost all-reduce when the engine's
+    # RCCL communicator runs one, whose own time is kt[7]), PMC traffic from the profile set
     wg_ms = kt[6]
-    if wg_ms > 0 and world == 1:   # sharded, [6] also spans the cost all-reduce ahead of the launch
+    if wg_ms > 0:
         wg_bytes = (BYTES_EPS_FR if not pm else 24.0) * units + 8.0 * traj.R   # the local eps, all R costs
         wg = {"kernel": "weights_gradient_kernel", "bound": "hbm",
               "ms": wg_ms, "bytes_per_launch": wg_bytes,
               "achieved_GBs": wg_bytes / (wg_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS}
         wg["frac"] = wg["achieved_GBs"] / HBM_PEAK_GBS
         wg["traffic"] = None
-        if os.path.exists(PMC_WG_JSON) and world == 1 and default_workload and not pm:
+        if world > 1 or comm1:
+            wg["cost_allreduce_ms"] = kt[7]
+            wg["note"] = "rank %d's shard; timed after the cost all-reduce (cost_allreduce_ms, RCCL), not including it" % rank
+        if os.path.exists(PMC_WG_JSON) and world == 1 and not comm1 and default_workload and not pm:
             with open(PMC_WG_JSON) as f:
                 rec = json.load(f)
             if wg["kernel"].split()[0] in rec["kernel"]:   # recorded for the kernel this run used
@@ -457,15 +516,17 @@ def run(args, world, rank, local_rank, dist):
         if dist:
             dist.destroy_process_group()
         return
+    label = workload_label(pm, S_total, traj.H, args.smoothing if sg else 0, world, args.graph)
     if pm:
-        workload = "%s%d samples x %d horizon, point-mass analytic dynamics + quadratic cost" % (
-            "BASELINE configs[1]: " if default_workload else "", S_total, traj.H)
+        workload = "%s%d samples x %d horizon, point-mass analytic dynamics + quadratic cost" % (label, S_total, traj.H)
         metric = "MPPI rollouts/sec (samples x horizon steps/s), %dx%d point mass" % (S_total, traj.H)
         data = "synthetic (x0 = 0, target (1,1,1), Philox noise)"
     else:
-        workload = "%s%d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, full AssistedManipulation cost stack%s%s" % (
-            ("BASELINE configs[%d]: " % cfg_index) if default_workload else "", S_total, traj.H,
-            ", Savitzky-Golay window %d order 1" % args.smoothing if sg else "", ", sample-sharded over RCCL" if world > 1 else "")
+        workload = "%s%d samples x %d horizon, FrankaRidgeback Pinocchio dynamics, full AssistedManipulation cost stack%s%s%s" % (
+            label, S_total, traj.H,
+            ", Savitzky-Golay window %d order 1" % args.smoothing if sg else "",
+            ", sample-sharded over RCCL" if world > 1 else (", through a one-rank RCCL communicator" if comm1 else ""),
+            ", hipGraph-captured update" if args.graph == 1 else "")
         metric = "MPPI rollouts/sec (samples x horizon steps/s), %dx%d FrankaRidgeback" % (S_total, traj.H)
         data = "synthetic (HUDDLED state, constant forecast wrench (20,0,0) N, Philox noise)"
     line = {
@@ -482,17 +543,17 @@ def run(args, world, rank, local_rank, dist):
         "dtype": "f64",
         "data": data,
         "config": {"workload": workload, "samples": S_total, "horizon": traj.H, "keep_best": KEEP_BEST,
-                   "parallelism": "samples-dp%d" % world},
+                   "parallelism": "samples-dp%d" % world, "graph": args.graph, "comm1": int(comm1)},
         "engine": info,
         "kernel_ms": {"rollout_launch": dyn_ms, "rollout_launch_samples": len(dyn_times), "breakdown_untimed": {
                       "sample": kt[0], "rollout": kt[1], "reduce": kt[2], "weights_gradient": kt[6],
-                      "optimal_rollout": kt[3], "update": kt[4]}},
+                      "cost_allreduce": kt[7], "optimal_rollout": kt[3], "update": kt[4]}},
         "roofline": roofline,
         "hbm": hbm,
         "rccl": rccl,
     }
-    if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(args, pm)
+    if not args.no_cpu_baseline:   # rank 0, after the timed loop: the whole job's workload
+        line["cpu_baseline"] = cpu_baseline(args, pm, world)
         # not vs_baseline (no published number): the GPU / CPU-port ratio, same workload
         line["speedup_vs_cpu_baseline"] = value / line["cpu_baseline"]["value"]
     print(json.dumps(line))

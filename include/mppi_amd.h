@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPPI_AMD_ABI_VERSION 4
+#define MPPI_AMD_ABI_VERSION 5   /* 5: mppi_device_costs_count, MPPI_INFO_GRAPH_*, MPPI_INFO_UPDATE_COUNT */
 
 #define MPPI_MAX_BODIES 16
 #define MPPI_MAX_CONTROL 16
@@ -345,6 +345,10 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
 mppi_status mppi_update_phase2(mppi_handle *h);
 mppi_status mppi_update_phase3(mppi_handle *h);
 void *mppi_device_costs(mppi_handle *h);     /* R + 1 doubles (the costs, then the wait-timeout count) */
+/* The number of doubles of mppi_device_costs the caller all-reduces: R + 1 since ABI version 4 (R
+ * before; a caller that reduces only R loses the cross-rank wait-timeout failure).  Integrators
+ * check mppi_abi_version() >= 5 and size the all-reduce from this. */
+int64_t mppi_device_costs_count(mppi_handle *h);
 void *mppi_device_gradient(mppi_handle *h);  /* C*H doubles */
 void *mppi_stream(mppi_handle *h);           /* hipStream_t */
 
@@ -378,6 +382,9 @@ mppi_status mppi_argmin(mppi_handle *h, int64_t *rollout);
 #define MPPI_TERM_MANIPULABILITY 6   /* get_manipulability_cost()   (.hpp:256-258) */
 mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7);
 mppi_status mppi_update_duration(mppi_handle *h, double *seconds);
+/* Trajectory::get_update_last (mppi.hpp:381-384): the time of the last successful update, whichever
+ * entry made it (mppi_update, the phase-split calls); the count is MPPI_INFO_UPDATE_COUNT. */
+mppi_status mppi_update_last(mppi_handle *h, double *time);
 mppi_status mppi_noise(mppi_handle *h, double *noise_R_C_H);
 mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
                       int64_t *control_C, int64_t *state_X);
@@ -398,7 +405,12 @@ mppi_status mppi_dims(mppi_handle *h, int64_t *rollouts_R, int64_t *steps_H,
 #define MPPI_INFO_WAIT_TIMEOUTS_TOTAL 8   /* the same, summed over every update since create */
 #define MPPI_INFO_FUSED_UPDATE 9          /* 1: the whole update ran as one launch (point mass,
                                              pm_update_kernel) */
-#define MPPI_UPDATE_INFO_N 10
+#define MPPI_INFO_GRAPH_UPDATES 10        /* updates since create that ran as the captured hipGraph */
+#define MPPI_INFO_GRAPH_FAILURES 11       /* graph captures that failed (that update then ran eagerly,
+                                             its collectives matched; the handle stays eager) */
+#define MPPI_INFO_UPDATE_COUNT 12         /* successful updates since create (Trajectory::update
+                                             calls that published, whichever entry made them) */
+#define MPPI_UPDATE_INFO_N 13
 mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
 
 /* Fault injection for the failure-detection tests (no reference counterpart; never set in
@@ -406,6 +418,10 @@ mppi_status mppi_update_info(mppi_handle *h, int64_t *info, int n);
  * MPPI_DEBUG_RELAY_NO_SIGNAL: relay stage 1 of the workgroup with rows left over never signals
  * stage 2, so the bounded in-launch waits give up and the update must fail (MPPI_ERR_DEVICE). */
 #define MPPI_DEBUG_RELAY_NO_SIGNAL 1
+/* MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL: the next `updates` hipGraph captures report an instantiation
+ * failure after recording the update (host side; no launch carries it): the update must still run,
+ * eagerly, with its collectives, and the handle stays on the eager path. */
+#define MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL 2
 mppi_status mppi_debug_inject(mppi_handle *h, int fault, int updates);
 /* The optimal-rollout cost the device holds now, as the last launch left it, without running or
  * waiting for a pending filter() (tests only): after an update whose launch folded the previous
@@ -427,10 +443,11 @@ mppi_status mppi_kernel_times(mppi_handle *h, float *ms5);
 /* As mppi_kernel_times without waiting for the side stream: [3] is the latest optimal rollout
  * already finished (possibly an earlier update's).  For timing loops that keep filter() overlapped. */
 mppi_status mppi_kernel_times_nowait(mppi_handle *h, float *ms5);
-/* The first n (<= 7) per-update times of mppi_kernel_times_nowait, where [5] is the rollout
+/* The first n (<= 8) per-update times of mppi_kernel_times_nowait, where [5] is the rollout
  * (dynamics) kernel alone: [1] spans it and the FrankaRidgeback cost kernel that sums the step
  * costs from its records; [6] (timing level 2) the weights + gradient launch alone, without the
- * finish kernel that [2] also spans. */
+ * finish kernel that [2] also spans (and, sharded over the engine's RCCL communicator, without the
+ * cost all-reduce ahead of it); [7] that cost all-reduce (0 otherwise). */
 mppi_status mppi_kernel_times_detail(mppi_handle *h, float *ms, int n);
 /* The rollout launch's HIP-event times (ms) of every update run at timing level 1 since the last
  * call, oldest first (at most the last 64): *count <- min(recorded, capacity), and the record is

@@ -58,7 +58,8 @@ def test_struct_layout_matches_header(tmp_path):
 
 def test_abi_version_and_defaults():
     L = _lib.load()
-    assert L.mppi_abi_version() == 4   # 2: mppi_cost_desc.track_point; 3: device forecast; 4: dynamics object, terms
+    assert L.mppi_abi_version() == 5   # 2: mppi_cost_desc.track_point; 3: device forecast; 4: dynamics object, terms;
+    # 5: mppi_device_costs_count, mppi_update_last, MPPI_INFO_GRAPH_* / UPDATE_COUNT
     m = am.FrankaRidgebackDynamics().model
     assert m.nbodies == 12
     assert [m.bodies[i].parent for i in range(12)] == [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 9]

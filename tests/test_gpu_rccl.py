@@ -91,3 +91,35 @@ def test_sharded_graph_equals_eager(rollouts, horison, window):
             continue
         for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
+
+
+@pytest.mark.parametrize("rollouts,horison", [(4096, 0.64)])
+def test_graph_capture_failure_runs_the_update_eagerly(rollouts, horison):
+    """a capture that fails after the update (its RCCL all-reduces included) was
+    recorded - here an injected instantiation failure (MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL) - must
+    still run that update, eagerly and with its two collectives, from the host state it started
+    from, so that peer ranks replaying the graph are not left blocked in an all-reduce; the handle
+    stays eager.  Bit-identical to a handle that never tried the graph."""
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8)
+    times = [0.0, 0.05, 0.07, 0.12, 0.17]
+    out = {}
+    for graph in (0, 1):
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), am.AssistedManipulation())
+        t.comm_init(1, 0, am.comm_unique_id())
+        t.set_graph(graph)
+        if graph:
+            t.debug_inject(abi.MPPI_DEBUG_GRAPH_INSTANTIATE_FAIL, 1)
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for tm in times:
+            t.update(x, tm)
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[graph] = (rec, t.update_info())
+    info = out[1][1]
+    assert info["graph_failures"] == 1 and info["graph_updates"] == 0, info
+    assert info["update_count"] == len(times) == out[0][1]["update_count"]
+    for j, (a, b) in enumerate(zip(out[0][0], out[1][0])):
+        for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+            np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))

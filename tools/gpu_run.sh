@@ -17,6 +17,8 @@
 #   pmcpm              the fetch / write / fp64 passes over the fused point-mass launch (configs[1])
 #   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
 #                      65536x128 SG)
+#   graphab[:ROUNDS]   configs[4]'s shapes as the hipGraph against eager launches, unsharded and through a
+#                      one-rank RCCL communicator (bench.py --graph / --comm1)
 #   ab:V1,V2,..:N      N interleaved rounds of bench over kernel variants (gpurun_variants/<V>/,
 #                      built by tools/ab_build.sh; "tree" = the in-tree library); BENCH_ARGS and
 #                      AB_ENV_<V> (extra env for variant V, e.g. AB_ENV_tree0="MPPI_HANDOVER=0") apply
@@ -140,6 +142,29 @@ step_sizes() {
     size s64k_h128_sg --steps 8 --warmup 2 --samples-per-gpu 65536 --horizon-steps 128 --smoothing 10
 }
 
+step_graphab() {   # [rounds]: configs[4]'s shapes, the hipGraph against eager launches, unsharded and through a
+                  # one-rank RCCL communicator (--comm1), interleaved on one box
+    local rounds=${1:-2} i
+    gsize() {   # name args...
+        local n=$1; shift
+        timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > $O/size_$n.json 2> $O/size_$n.err \
+            || { echo "size $n rc=$?"; tail -5 $O/size_$n.err; return 1; }
+        summary $O/size_$n.json $n
+        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); print('   graph_updates_timed', d['engine']['graph_updates_timed'], 'of', d['steps'])" $O/size_$n.json
+    }
+    for i in $(seq 1 $rounds); do
+        for c in 0 1; do
+            for g in 0 1; do
+                gsize s8k_sg_c${c}_g${g}_$i --steps 60 --warmup 5 --samples-per-gpu 8192 --horizon-steps 128 --smoothing 10 \
+                    --graph $g --comm1 $c || return 1
+            done
+        done
+    done
+    for g in 0 1; do
+        gsize s64k_sg_g${g} --steps 12 --warmup 3 --samples-per-gpu 65536 --horizon-steps 128 --smoothing 10 --graph $g || return 1
+    done
+}
+
 step_ab() {   # V1,V2,..  rounds
     local vs rounds=${2:-3}
     IFS=, read -ra vs <<< "$1"
@@ -187,6 +212,7 @@ for s in "$@"; do
         pmcpm) step_pmc pm ;;
         sizes) step_sizes ;;
         kpmc) step_kpmc "$arg" ;;
+        graphab) step_graphab "$arg" ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;
         pmstamps) step_pmstamps "$arg" ;;
