@@ -170,6 +170,7 @@ struct mppi_handle {
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [Rpad][H][FR_REC] and the filter() row's [H][FR_REC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
+    bool opt_rec_compact = false;   // d_rec_opt holds compact records (the standalone filter()), else 768-B ones (folded)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
     size_t inj_capacity = 0;   // doubles
@@ -1464,9 +1465,11 @@ static double *rollout_costs_out(const mppi_handle *h)
     return h->comm ? h->d_costs_local : h->d_costs;
 }
 
-static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a)
+// compact: the records are fr_coop_kernel's (FR_REC_C), not fr_coop_x_kernel's (FR_REC)
+static FrCostArgs cost_args(const mppi_handle *h, const FrRolloutArgs &a, bool compact)
 {
     FrCostArgs c{};
+    c.compact = compact ? 1 : 0;
     c.cost = a.cost;
     c.steps = a.steps;
     c.rec = a.rec;
@@ -1517,7 +1520,8 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         // the row's objective after its loop (fr_coop_kernel's one-wave path)
         a.costs_in_launch = fr_coop_costs_in_launch(h->env) ? 1 : 0;
         HIP_TRY(launch_fr_coop(a, h->stream_opt));
-        if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream_opt));
+        if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a, true), h->stream_opt));
+        h->opt_rec_compact = true;   // launch_fr_coop: fr_coop_kernel's compact records
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;
@@ -1688,7 +1692,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         h->gargs.nroll = ct.launches;
         if (h->timing >= 2) HIP_TRY(hipEventRecord(h->ev_dyn, h->stream));
         if (!folded) a.fcost = nullptr;
-        if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a), h->stream));
+        // fr_coop_x_kernel (the rows left over, the split) writes 768-B records, fr_coop_kernel compact ones
+        if (!costs_done && !h->graph_dry) HIP_TRY(launch_fr_step_cost(cost_args(h, a, !h->gargs.x_kernel), h->stream));
         h->tail_drawn = tail;
         h->info[MPPI_INFO_COOPERATIVE] = 1;
         h->info[MPPI_INFO_FOLDED_FILTER] = folded ? 1 : 0;
@@ -1702,6 +1707,7 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
             h->tail_xbase = ct.xbase;
             h->tail_nxb = ct.nxb;
         }
+        if (folded) h->opt_rec_compact = false;   // the folded row: fr_coop_x_kernel's 768-B records
         if (folded) {   // the optimal cost is ready with this update's rollouts; phase 3's host block
                         // carries it back (finish_kernel copies d_opt), on the same stream
             h->kernel_ms[3] = 0.0f;   // timed inside the rollout launch
@@ -2472,7 +2478,7 @@ mppi_status mppi_optimal_terms(mppi_handle *h, double *terms7)
     }
     mppi_status st = wait_optimal(h);   // the filter() row's records are then complete
     if (st != MPPI_OK) return st;
-    HIP_TRY(launch_fr_terms(h->d_cost, h->opt_steps, h->d_rec_opt, (int)h->H, h->d_terms, h->stream_opt));
+    HIP_TRY(launch_fr_terms(h->d_cost, h->opt_steps, h->d_rec_opt, (int)h->H, h->opt_rec_compact, h->d_terms, h->stream_opt));
     HIP_TRY(hipMemcpyAsync(h->h_opt + 1, h->d_terms, 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream_opt));
     HIP_TRY(hipStreamSynchronize(h->stream_opt));
     std::memcpy(terms7, h->h_opt + 1, 7 * sizeof(double));

@@ -72,6 +72,11 @@ constexpr int L_COL = 0;                    // no tank: the mass-matrix block (1
 constexpr int L_TP = L_COL + 16 * CSTR;     // no tank: the solved right-hand side (12)
 constexpr int L_S = 300;                    // 16-byte aligned; per slot S (6), qd, pad
 constexpr int S_STR = 10;
+// compact records without the tank (store_ks): per slot S linear x, y, z and qd, 48 B apart (the
+// sixteen lanes' 16-byte stores start at 12 j (mod 64) dwords: disjoint bank groups); past the
+// dummy lanes' 0 / 1 at L_TP + 12, 13 (with the tank store_ks reads coop_aba's L_S slots)
+constexpr int L_KS = 304;
+constexpr int KS_STR = 6;
 constexpr int LDS_KIN = 432;                // >= L_S + NSLOT * S_STR, = 16 (mod 32) doubles
 constexpr int L_F = 430;                    // energy tank: spatial force f of each body slot
 constexpr int LDS_KIN_EN = 528;             // >= L_F + NSLOT * 6, = 16 (mod 32) doubles
@@ -84,6 +89,7 @@ static_assert(L_I + NSLOT * 21 <= L_S && L_S + NSLOT * S_STR <= LDS_KIN && L_TAU
 // (L_TP + 12, 13: the dummy lanes' 0 / 1, over L_S, which only the tank's articulated-body pass uses)
 static_assert(L_TP + 14 <= LDS_KIN && L_TP % 2 == 0, "LDS row layout (mass-matrix block)");
 static_assert(L_S + NSLOT * S_STR <= L_F && L_F + NSLOT * 6 <= LDS_KIN_EN && L_F % 2 == 0, "LDS row layout (energy)");
+static_assert(L_TP + 14 <= L_KS && L_KS % 2 == 0 && L_KS + NSLOT * KS_STR <= LDS_KIN, "LDS row layout (kinematic sums)");
 static_assert(LDS_KIN % 32 == 16 && LDS_SCR % 32 == 16 && LDS_KIN_EN % 32 == 16, "row stride bank offset");
 
 // Per-block body table (doubles per body): scan placement R p (body 11: relative to body 10),
@@ -722,6 +728,8 @@ struct LaneConst {
     // lane coefficients (1.0 / 0.0, opaque): base_velocity's, and tau_u's (3 <= j < 10: the arm
     // joints it drives)
     double bA, bB, bnA, bC, bkeep, taud;
+    int ka, kb;     // store_ks (compact records): kinematic sum min(j, 8)'s x and y offsets in a body's LDS slot
+    int m_vsum;     // store_ks: the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     int fp_off;     // store_record: REC_EE / REC_AM on lanes FR_EE_PARENT / FR_AM_PARENT, else REC_FP_SINK
     double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
@@ -852,6 +860,33 @@ __device__ __forceinline__ void store_kin(double *rp, int j, const CoopBody &bd,
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
     *reinterpret_cast<double2 *>(rp + REC_S01 + 2 * j) = double2{bd.S[0], bd.S[1]};
     *reinterpret_cast<double2 *>(rp + REC_S2Q + 2 * j) = double2{bd.S[2], qd};
+}
+
+// The compact record's kinematics (fr_coop_kernel, FR_REC_C): the row forms the nine sums itself -
+// the EE frame velocity J v over bodies 0..9 and J_a J_a^T over the arm (3..9) - lane m = min(j, 8)
+// sum m from the S / qd slots the row writes to LDS, in the order and with the FMAs of the objective's
+// kin_sums (fr_cost_terms.hpp: i = 0..9, acc = fma(x_i, y_i, acc), y_i = 0 for the base's J_a J_a^T),
+// so the costs keep their bits.  About 40 instructions on the chain of every step (r04's form): where
+// a wave evaluates its own rows' objective after its loop there are no objective waves beside the
+// loops to absorb them, and the record, written and read back, is half the 768-B one's bytes.
+template <int CK, bool EN>
+__device__ __forceinline__ void store_ks(double *rp, int j, const LaneConst &L, const CoopBody &bd, double qd, double *Lk)
+{
+    if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
+    constexpr int B = EN ? L_S : L_KS, ST = EN ? S_STR : KS_STR;
+    if constexpr (!EN) {   // (with the tank coop_fk staged S and qd for coop_aba)
+        *reinterpret_cast<double2 *>(Lk + L_KS + L.slot * KS_STR) = double2{bd.S[0], bd.S[1]};
+        *reinterpret_cast<double2 *>(Lk + L_KS + L.slot * KS_STR + 2) = double2{bd.S[2], qd};
+    }
+    const double *xs = Lk + B + L.ka, *ys = Lk + B + L.kb;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i <= FR_EE_PARENT; i++) {
+        double y = ys[i * ST];
+        if (i < FR_ARM0) y = msel(L.m_vsum, 0.0, y);
+        acc = __builtin_fma(xs[i * ST], y, acc);
+    }
+    rp[REC_VL + (j < 9 ? j : 8)] = acc;   // lanes 9..15 repeat lane 8: same address, same value
 }
 
 // Articulated-body passes over the world inertias / S staged in LDS (energy-tank rollouts, whose
@@ -1289,7 +1324,10 @@ __device__ __forceinline__ void store_record(double *rp, int j, const LaneConst 
     *reinterpret_cast<double2 *>(rp + 2 * j) = double2{a0, a1};
 }
 // slots 88..90: S2Q's entries of the dummy lanes 12..15, written by store_kin and read by nobody
+// (the compact record's: REC_SINK_C)
 constexpr int REC_FP_SINK = REC_S2Q + 2 * 12;
+static_assert(REC_VL + 9 <= REC_SINK_C && REC_SINK_C + 3 <= FR_REC_C && FR_REC_C % 16 == 0 && FR_NREC <= FR_REC_C,
+              "compact record layout");
 static_assert(REC_EE == 24 && REC_AM == 27 && REC_E == 30 && REC_S01 == 32 && REC_S2Q == 64 && FR_REC == 96, "record layout");
 static_assert(REC_FP_SINK + 3 <= FR_REC, "frame-position sink");
 
@@ -1311,7 +1349,9 @@ static_assert(REC_FP_SINK + 3 <= FR_REC, "frame-position sink");
 // the horizon at priority 3 and hands the state to the next stage through LDS, so each of the four
 // main waves loses about a quarter of what wave 0 alone lost before.
 // PROG: the wave stores its step into *Lprog at the top of each step (the objective chunks, cost_work).
-template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false>
+// KC: compact records (FR_REC_C, store_ks: the kinematic sums on the row's chain), else the 768-B
+// ones (store_kin).
+template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false, bool KC = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, double *Lst = nullptr, int kb = 0,
                                          int ke = 0x7FFFFFFF, int *Lprog = nullptr)
@@ -1337,8 +1377,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     // shift reads U* itself (mppi.cpp:197-207); the state staged in LDS (stage_x0)
     const double *Up = FROW && frow ? a.fU : a.Ushift;
     const int ush = FROW && frow ? 0 : a.ush;
-    double *rp = FROW && frow ? a.frec : a.rec + lr * H * FR_REC;   // [rollout][step][FR_REC]
-    auto recp = [&](int k) -> double * { return rp + (int64_t)k * FR_REC; };
+    constexpr int RS = KC ? FR_REC_C : FR_REC;
+    double *rp = FROW && frow ? a.frec : a.rec + lr * H * RS;   // [rollout][step][RS]
+    auto recp = [&](int k) -> double * { return rp + (int64_t)k * RS; };
     const bool jl = j < FR_NB;   // lane owns a body / control component
     const int jb = jl ? j : 0;
     const double *M = Lmodel + (jl ? j : FR_NB) * MB;
@@ -1373,9 +1414,18 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         int ro = j < FR_NB ? 2 * j : REC_E;
         asm volatile("" : "+v"(ro));
         L.rec_off = ro;
-        int fo = j == FR_EE_PARENT ? REC_EE : (j == FR_AM_PARENT ? REC_AM : REC_FP_SINK);
+        int fo = j == FR_EE_PARENT ? REC_EE : (j == FR_AM_PARENT ? REC_AM : (KC ? REC_SINK_C : REC_FP_SINK));
         asm volatile("" : "+v"(fo));
         L.fp_off = fo;
+        if constexpr (KC) {   // store_ks: sum m's x and y in a body slot (S linear 0..2, qd at 3, or 6 with the tank)
+            const int m = j < 9 ? j : 8;
+            int ka = (int)((0x211000210ull >> (4 * m)) & 0xF);
+            int kb = (int)(((EN ? 0x221210666ull : 0x221210333ull) >> (4 * m)) & 0xF);
+            asm volatile("" : "+v"(ka), "+v"(kb));   // opaque: the LDS reads stay behind the row's stores
+            L.ka = ka;
+            L.kb = kb;
+            L.m_vsum = opaque_mask(m < 3);
+        }
 #pragma unroll
         for (int i = 0; i < 11; i++) {
             double d = ((anc >> i) & 1) ? 1.0 : 0.0;
@@ -1430,7 +1480,8 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     }
     if (kb == 0) {
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
-        store_kin<CK>(recp(0), j, bd, qd);
+        if constexpr (KC) store_ks<CK, false>(recp(0), j, L, bd, qd, Lk);
+        else store_kin<CK>(recp(0), j, bd, qd);
     }
 
     // eps and U*_shifted of step k: loaded at the top of the step
@@ -1464,7 +1515,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         if constexpr (EN)
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
         coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
-        store_kin<CK>(recp(k + 1), j, bd, qd);   // the next record's kinematics (the one-step lag)
+        // the next record's kinematics (the one-step lag)
+        if constexpr (KC) store_ks<CK, EN>(recp(k + 1), j, L, bd, qd, Lk);
+        else store_kin<CK>(recp(k + 1), j, bd, qd);
         double pe = 0.0;
         double qdd;
         if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe);
@@ -1507,9 +1560,10 @@ __device__ __forceinline__ void launch_row_cost(const FrRolloutArgs &a, int64_t 
     const bool frow = a.fcost != nullptr && lr == a.count;
     if (!(lr < a.count || frow)) return;
     if (frow && (a.status->all_nan || a.status->sg_error)) return;   // no filter() when the update threw
-    const double J = mppi_cost::rollout_cost<CK, EN, MB>(*a.cost, frow ? a.fsteps : a.steps,
-                                                          frow ? a.frec : a.rec + lr * a.H * FR_REC, a.H, lane,
-                                                          Lmodel + T_LO);
+    // (fr_coop_kernel's compact records)
+    const double J = mppi_cost::rollout_cost<CK, EN, MB, true>(*a.cost, frow ? a.fsteps : a.steps,
+                                                                frow ? a.frec : a.rec + lr * a.H * FR_REC_C, a.H, lane,
+                                                                Lmodel + T_LO);
     if (lane == 0) {
         if (frow) *a.fcost = J;
         else {
@@ -1900,8 +1954,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
             kept_rows_wave(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, rk);
         }
     }
-    coop_rows<CK, EN, FROW>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS, lds_scr + wrow * LDS_SCR,
-                            Lmodel, Lx0);
+    coop_rows<CK, EN, FROW, 0, false, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS,
+                                            lds_scr + wrow * LDS_SCR, Lmodel, Lx0);
     if constexpr (WPB == 4) {
         if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel);
     } else if constexpr (WPB == 1) {

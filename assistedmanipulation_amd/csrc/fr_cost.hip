@@ -35,7 +35,7 @@ using namespace mppi_cost;
 // lanes: every byte of the rollout's records is used once, through L2).  Staging through LDS took
 // 21.5 KB per wave and held a CU to seven waves, too few to hide the loads; without it the kernel
 // is bounded by registers (four waves per SIMD).
-template <int CK, bool EN>
+template <int CK, bool EN, bool KC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fr_step_cost_kernel(FrCostArgs a)
 {
     __shared__ double Lj[FR_NB * JT_STRIDE];
@@ -54,7 +54,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             Lj[i] = *src;
         }
     __syncthreads();
-    const double J = rollout_cost<CK, EN>(Cs, stp, frow ? a.frec : a.rec + row * H * FR_REC, H, lane, Lj);
+    const double J = rollout_cost<CK, EN, JT_STRIDE, KC>(Cs, stp, frow ? a.frec : a.rec + row * H * (KC ? FR_REC_C : FR_REC), H,
+                                                         lane, Lj);
     if (lane != 0) return;
     if (frow) *a.fcost = J;
     else if (a.optimal) *a.cost_out = J;
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 // mppi.cpp:450-479 with thread 0's cost, reset at its start): one wave over the filter() row's
 // records, lane = step, each term summed over the steps in step order (m_*_cost += per step).
 __global__ __launch_bounds__(64) void fr_terms_kernel(const DevCost *cost, const StepConst *steps, const double *rec, int H,
-                                                      double *out7)
+                                                      int compact, double *out7)
 {
     const int lane = threadIdx.x;
     double tot[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(64) void fr_terms_kernel(const DevCost *cost, const
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
         double t[7], r[FR_NREC];
-        derive_record(rec + (int64_t)k * FR_REC, r);
+        derive_record(rec + (int64_t)k * (compact ? FR_REC_C : FR_REC), r, compact != 0);
         assisted_manipulation_terms(*cost, steps[k], r, r[REC_QQD + 4], t);
 #pragma unroll
         for (int m = 0; m < 7; m++)
@@ -94,9 +95,10 @@ __global__ __launch_bounds__(64) void fr_terms_kernel(const DevCost *cost, const
 
 namespace mppi_eng {
 
-hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s)
+hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, bool compact, double *out7,
+                           hipStream_t s)
 {
-    hipLaunchKernelGGL(fr_terms_kernel, dim3(1), dim3(64), 0, s, cost, steps, rec, H, out7);
+    hipLaunchKernelGGL(fr_terms_kernel, dim3(1), dim3(64), 0, s, cost, steps, rec, H, compact ? 1 : 0, out7);
     return hipGetLastError();
 }
 
@@ -105,9 +107,16 @@ hipError_t launch_fr_step_cost(const FrCostArgs &a, hipStream_t s)
     const int64_t rows = a.count + (a.fcost ? 1 : 0);
     if (rows == 0) return hipSuccess;
     const dim3 grid((unsigned)rows), block(64);
-    if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_step_cost_kernel<CK_TRACK_POINT, false>), grid, block, 0, s, a);
-    else if (a.energy) hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, false>), grid, block, 0, s, a);
+    // the records' layout is the launch's that wrote them (FrCostArgs::compact)
+    if (a.compact) {
+        if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_step_cost_kernel<CK_TRACK_POINT, false, true>), grid, block, 0, s, a);
+        else if (a.energy) hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, true, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, false, true>), grid, block, 0, s, a);
+    } else {
+        if (a.cost_kind == CK_TRACK_POINT) hipLaunchKernelGGL((fr_step_cost_kernel<CK_TRACK_POINT, false, false>), grid, block, 0, s, a);
+        else if (a.energy) hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, true, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((fr_step_cost_kernel<CK_ASSISTED_MANIPULATION, false, false>), grid, block, 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -113,22 +113,23 @@ __device__ __forceinline__ void kin_sums(const double2 *rec2, double *vl, double
     }
 }
 
-// The derived record (FR_NREC) of a stored one (FR_REC)
-__device__ __forceinline__ void derive_record(const double *rk, double *r)
+// The derived record (FR_NREC) of a stored one (FR_REC; a compact FR_REC_C record is one already)
+__device__ __forceinline__ void derive_record(const double *rk, double *r, bool compact = false)
 {
     const double2 *src = reinterpret_cast<const double2 *>(rk);
-#pragma unroll
-    for (int i = 0; i < REC_VL / 2; i++) {
+    const int n = compact ? FR_NREC / 2 : REC_VL / 2;
+    for (int i = 0; i < n; i++) {
         const double2 v = src[i];
         r[2 * i] = v.x;
         r[2 * i + 1] = v.y;
     }
-    kin_sums(src, r + REC_VL, r + REC_JJ);
+    if (!compact) kin_sums(src, r + REC_VL, r + REC_JJ);
     r[FR_NREC - 1] = 0.0;
 }
 
-// AssistedManipulation::get_cost at the record's state with its kinematics
-template <bool EN, int JS>
+// AssistedManipulation::get_cost at the record's state with its kinematics (KC: a compact record,
+// J v and J_a J_a^T stored; else the 768-B record, whose motion subspaces they are formed from)
+template <bool EN, int JS, bool KC = false>
 __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
                                                              const double *Lj, const double2 *src)
 {
@@ -164,8 +165,22 @@ __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, 
         rest[2 * i] = v.x;
         rest[2 * i + 1] = v.y;
     }
-    double vl[3], jj[6];   // from the stored record's motion subspaces (kin_sums)
-    kin_sums(tp, vl, jj);
+    double vl[3], jj[6];
+    if constexpr (KC) {   // stored by the rows (REC_VL, REC_JJ)
+        double kv[10];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const double2 v = tp[REC_VL / 2 + i];
+            kv[2 * i] = v.x;
+            kv[2 * i + 1] = v.y;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) vl[i] = kv[i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) jj[i] = kv[3 + i];
+    } else {
+        kin_sums(tp, vl, jj);   // from the stored record's motion subspaces
+    }
     r = rest - REC_EE;   // r[REC_EE .. REC_VL) from here on
     double s, c;
     fsincos(yaw, &s, &c, sincos_constants());   // base yaw q_2
@@ -296,16 +311,17 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
 
 // gamma_k times the objective at step record r (AssistedManipulation: r holds the record's (q, qd)
 // pairs, the rest is read from the stored record src; TrackPoint: r holds the record up to REC_VL)
-template <int CK, bool EN, int JS = JT_STRIDE>
+template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false>
 __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
                                            const double2 *src)
 {
     if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r, r[REC_QQD + 4]);
-    else return sc.gamma_k * assisted_manipulation_cost<EN, JS>(Cs, sc, r, Lj, src);
+    else return sc.gamma_k * assisted_manipulation_cost<EN, JS, KC>(Cs, sc, r, Lj, src);
 }
 
-// gamma_k times the objective at the stored step record rk (FR_REC doubles, 16-byte aligned)
-template <int CK, bool EN, int JS = JT_STRIDE>
+// gamma_k times the objective at the stored step record rk (FR_REC doubles, or FR_REC_C with KC;
+// 16-byte aligned)
+template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false>
 __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const StepConst &sc, const double *rk, const double *Lj)
 {
     double r[FR_NREC];
@@ -317,22 +333,24 @@ __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const Step
         r[2 * i] = v.x;
         r[2 * i + 1] = v.y;
     }
-    return step_cost<CK, EN, JS>(Cs, sc, r, Lj, src);
+    return step_cost<CK, EN, JS, KC>(Cs, sc, r, Lj, src);
 }
 
-// J of one rollout from its H stored step records (rollout-major, FR_REC doubles each) by one wave:
+// J of one rollout from its H stored step records (rollout-major, FR_REC doubles each, FR_REC_C with
+// KC) by one wave:
 // lane k evaluates step k (64 steps a pass) and the wave sums the step costs in step order, as the
 // reference accumulates J += cost (mppi.cpp:322-337); a NaN step makes the sum NaN (the reference's
 // early stop), canonicalised to the quiet NaN it stores.  The same value on every lane.
-template <int CK, bool EN, int JS = JT_STRIDE>
+template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false>
 __device__ __forceinline__ double rollout_cost(const DevCost &Cs, const StepConst *stp, const double *rec, int H, int lane,
                                                const double *Lj)
 {
+    constexpr int RS = KC ? FR_REC_C : FR_REC;
     double J = 0.0;
     for (int base = 0; base < H; base += 64) {
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
-        const double c = record_step_cost<CK, EN, JS>(Cs, stp[k], rec + (int64_t)k * FR_REC, Lj);
+        const double c = record_step_cost<CK, EN, JS, KC>(Cs, stp[k], rec + (int64_t)k * RS, Lj);
         for (int i = 0; i < n; i++) J += readlane_f64(c, i);
     }
     return isnan(J) ? (double)NAN : J;

@@ -187,10 +187,19 @@ constexpr int REC_JJ = 35;    // J_a J_a^T (arm joints 3..9), packed 00 01 02 11
 constexpr int REC_S01 = 32;   // [32 + 2j], [33 + 2j]: S_j linear x, y (j < 10 read)
 constexpr int REC_S2Q = 64;   // [64 + 2j], [65 + 2j]: S_j linear z, the calculate()'s qd_j (j < 10 read)
 constexpr int FR_REC = 96;    // 768 B: sixteen records are 96 whole 128-byte lines
+// The compact stored record (fr_coop_kernel: the one-wave and four-wave launches whose waves evaluate
+// their own rows' objective after their loops, and the standalone filter()): the derived record
+// itself - the rows form J v and J_a J_a^T on their own chain (lane m < 9 writes sum m at REC_VL + m)
+// - plus a sink for the frame positions of the lanes that own neither the EE nor the arm mount.
+// 384 B: half the 768-B record's bytes, written and read back (sixteen records are 48 lines).
+// fr_coop_x_kernel keeps the 768-B record: its objective waves run the sums beside the loops.
+constexpr int REC_SINK_C = 42;   // slots 42..44: the other lanes' frame positions, read by nobody
+constexpr int FR_REC_C = 48;
 
 // The rollout costs from the records (fr_cost.hip): one wave per rollout, one lane per step, the
 // step costs summed in step order (the reference's J += cost, mppi.cpp:322-337).
 struct FrCostArgs {
+    int compact;              // the records are FR_REC_C compact ones (fr_coop_kernel), else FR_REC
     const DevCost *cost;
     const StepConst *steps;   // [H]
     const double *rec;        // [count][H][FR_REC]
@@ -433,7 +442,8 @@ struct PmFusedArgs {
 constexpr int PM_STAMPS = 12;
 hipError_t launch_pm_update(const PmFusedArgs &a, hipStream_t s);
 // AssistedManipulation's seven per-term totals of one rollout from its [H][FR_REC] records
-hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, double *out7, hipStream_t s);
+hipError_t launch_fr_terms(const DevCost *cost, const StepConst *steps, const double *rec, int H, bool compact, double *out7,
+                           hipStream_t s);
 
 
 }  // namespace mppi_eng

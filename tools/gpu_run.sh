@@ -17,6 +17,8 @@
 #   pmcpm              the fetch / write / fp64 passes over the fused point-mass launch (configs[1])
 #   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
 #                      65536x128 SG)
+#   absizes:V1,V2:N    N interleaved rounds of the 4096x64, 32768x64, 8192x128 SG and 65536x128 SG benches
+#                      over library variants (as ab)
 #   graphab[:ROUNDS]   configs[4]'s shapes as the hipGraph against eager launches, unsharded and through a
 #                      one-rank RCCL communicator (bench.py --graph / --comm1)
 #   ab:V1,V2,..:N      N interleaved rounds of bench over kernel variants (gpurun_variants/<V>/,
@@ -165,6 +167,26 @@ step_graphab() {   # [rounds]: configs[4]'s shapes, the hipGraph against eager l
     done
 }
 
+step_absizes() {   # V1,V2,..  rounds: interleaved A/B of the library variants over BASELINE's workloads
+    local vs rounds=${2:-2} i v w
+    IFS=, read -ra vs <<< "$1"
+    local shapes=("s4k:--steps 200 --warmup 10" "s32k:--steps 20 --warmup 3 --samples-per-gpu 32768"
+                  "s8k_sg:--steps 40 --warmup 3 --samples-per-gpu 8192 --horizon-steps 128 --smoothing 10"
+                  "s64k_sg:--steps 8 --warmup 2 --samples-per-gpu 65536 --horizon-steps 128 --smoothing 10")
+    for i in $(seq 1 $rounds); do
+        for w in "${shapes[@]}"; do
+            for v in "${vs[@]}"; do
+                local lib=$PWD/assistedmanipulation_amd/lib/libmppi_amd.so n=${w%%:*} f
+                case $v in tree*) ;; *) lib=$PWD/gpurun_variants/$v/libmppi_amd.so;; esac
+                f=$O/abs_${n}_${v}_$i.json
+                MPPI_AMD_LIB=$lib timeout -k 10 200 python -u bench.py --no-cpu-baseline ${w#*:} > $f 2> ${f%.json}.err \
+                    || { echo "absizes $n $v rc=$?"; tail -20 ${f%.json}.err; return 1; }
+                summary $f "$n/$v/$i"
+            done
+        done
+    done
+}
+
 step_ab() {   # V1,V2,..  rounds
     local vs rounds=${2:-3}
     IFS=, read -ra vs <<< "$1"
@@ -213,6 +235,7 @@ for s in "$@"; do
         sizes) step_sizes ;;
         kpmc) step_kpmc "$arg" ;;
         graphab) step_graphab "$arg" ;;
+        absizes) step_absizes "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         ab) step_ab "${arg%%:*}" "$( [ "${arg#*:}" != "$arg" ] && echo ${arg#*:} )" ;;
         wtrace) step_wtrace "$arg" ;;
         pmstamps) step_pmstamps "$arg" ;;
