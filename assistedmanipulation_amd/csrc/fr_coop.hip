@@ -869,14 +869,20 @@ __device__ __forceinline__ void store_kin(double *rp, int j, const CoopBody &bd,
 // so the costs keep their bits.  About 40 instructions on the chain of every step (r04's form): where
 // a wave evaluates its own rows' objective after its loop there are no objective waves beside the
 // loops to absorb them, and the record, written and read back, is half the 768-B one's bytes.
-template <int CK, bool EN>
+// EN: the tank kernel's layout (coop_aba's L_S slots, qd at 6); STAGED: coop_fk<CK, true> wrote them
+// (every step of the tank kernel but the set_state calculate() before its loop)
+template <int CK, bool EN, bool STAGED = EN>
 __device__ __forceinline__ void store_ks(double *rp, int j, const LaneConst &L, const CoopBody &bd, double qd, double *Lk)
 {
     if constexpr (CK == CK_TRACK_POINT) return;   // TrackPoint reads the EE / arm-mount positions only
     constexpr int B = EN ? L_S : L_KS, ST = EN ? S_STR : KS_STR;
-    if constexpr (!EN) {   // (with the tank coop_fk staged S and qd for coop_aba)
+    if constexpr (!EN) {
         *reinterpret_cast<double2 *>(Lk + L_KS + L.slot * KS_STR) = double2{bd.S[0], bd.S[1]};
         *reinterpret_cast<double2 *>(Lk + L_KS + L.slot * KS_STR + 2) = double2{bd.S[2], qd};
+    } else if constexpr (!STAGED) {
+        *reinterpret_cast<double2 *>(Lk + L_S + L.slot * S_STR) = double2{bd.S[0], bd.S[1]};
+        Lk[L_S + L.slot * S_STR + 2] = bd.S[2];
+        Lk[L_S + L.slot * S_STR + 6] = qd;
     }
     const double *xs = Lk + B + L.ka, *ys = Lk + B + L.kb;
     double acc = 0.0;
@@ -1480,7 +1486,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     }
     if (kb == 0) {
         coop_fk<CK, false>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);   // set_state -> calculate() at (q0, v0)
-        if constexpr (KC) store_ks<CK, false>(recp(0), j, L, bd, qd, Lk);
+        if constexpr (KC) store_ks<CK, EN, false>(recp(0), j, L, bd, qd, Lk);   // (coop_fk<CK, false> staged nothing)
         else store_kin<CK>(recp(0), j, bd, qd);
     }
 
