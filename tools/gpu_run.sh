@@ -15,6 +15,7 @@
 #   tracepm            trace of the point-mass workload (configs[1]), 200 updates
 #   pmc                rocprofv3 PMC passes (one counter set per run) -> pmc summaries + traffic JSON
 #   pmcpm              the fetch / write / fp64 passes over the fused point-mass launch (configs[1])
+#   pmcsize:NAME:KERN  the PMC passes over BENCH_ARGS's workload, kernel names containing KERN
 #   sizes              the other BASELINE workloads on one GPU (point mass, 32768x64, 8192x128 SG,
 #                      65536x128 SG)
 #   absizes:V1,V2:N    N interleaved rounds of the 4096x64, 32768x64, 8192x128 SG and 65536x128 SG benches
@@ -86,8 +87,11 @@ step_trace() {   # [name] [extra bench args...]
     return 0
 }
 
-step_pmc() {   # [pm]
+step_pmc() {   # [pm | NAME PREFIX]: NAME: a size's passes (BENCH_ARGS) into $O/pmc_NAME, the kernel matched by PREFIX
     local B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline $BENCH_ARGS" D=$O/pmc out=$O/pmc_rollout.json prefix=
+    if [ -n "$2" ]; then
+        D=$O/pmc_$1 out=$O/pmc_$1.json prefix=$2
+    fi
     if [ "$1" = pm ]; then
         B="python3 bench.py --workload point_mass --steps 50 --warmup 5 --no-cpu-baseline"
         D=$O/pmcpm out=$O/pmc_pm.json prefix=pm_update_kernel
@@ -231,6 +235,7 @@ for s in "$@"; do
         trace) step_trace "$arg" ;;
         tracepm) step_trace tracepm --workload point_mass --steps 200 ;;
         pmc) step_pmc ;;
+        pmcsize) step_pmc "${arg%%:*}" "${arg#*:}" ;;
         pmcpm) step_pmc pm ;;
         sizes) step_sizes ;;
         kpmc) step_kpmc "$arg" ;;
