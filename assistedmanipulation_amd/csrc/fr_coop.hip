@@ -49,6 +49,21 @@ using namespace mppi_eng;
 using mppi_dev::smax;
 using mppi_dev::smin;
 
+// PHASE_MARKS (analysis builds only, tools/phase_flops.py): a comment at each phase boundary of the
+// step, so that the executed instructions can be attributed to phases - 0 the control and the base
+// velocity, 1 FK (with the next step's sincos), 2 world inertias, 3 kinematics for the cost, 4 the
+// composite inertias, 5 the mass-matrix columns, 6 the Gauss-Jordan solve, 7 integration and the
+// record stores.  (A volatile asm ends the scheduler's region: the marked build is a little slower.)
+// PMARK_D ties the marker to a value the next phase's inline-asm blocks consume or the previous
+// one's produce: non-volatile asm statements are otherwise free to move across a plain marker.
+#ifdef PHASE_MARKS
+#define PMARK(n) asm volatile("; PHASE " #n)
+#define PMARK_D(n, x) asm volatile("; PHASE " #n : "+v"(x))
+#else
+#define PMARK(n)
+#define PMARK_D(n, x)
+#endif
+
 namespace {
 
 constexpr int ROW = 16;
@@ -256,8 +271,10 @@ __device__ __forceinline__ int opaque_mask(bool c)
 }
 
 // ---- BEGIN generated by tools/gen_gj.py: mass-matrix solve helpers ----
-// m[i] = S_i . F for i = 0..10, S_i broadcast from lane i: rows 0 and 1 are F[0] and F[1] (the
-// base's unit axes); rows 2..10 nine chains of six, round-robin
+// m[i] = S_i . F for i = 0..9, S_i broadcast from lane i: rows 0 and 1 are F[0] and F[1] (the
+// base's unit axes); rows 2..9 eight chains of six, round-robin, rows 3 and 7 on the lanes of
+// the banks that hold their descendants only (bank_mask: the others keep 0); m[10] = 0 (body 10
+// is nobody's ancestor)
 __device__ __forceinline__ void column_dots(const double *S, const double *F, double *m)
 {
     m[0] = F[0];
@@ -267,61 +284,55 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
     // no leading s_nop: S (the DPP sources) was formed long before (tools/dpp_hazard_check.py
     // checks every build's assembly)
     asm(""
+        "v_fmac_f64_dpp %0, %8, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %14 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
+        "v_fmac_f64_dpp %2, %8, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %8, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %8, %14 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
+        "v_fmac_f64_dpp %6, %8, %14 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %8, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, %9, %15 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %9, %15 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %9, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %9, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %9, %15 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %9, %15 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %9, %15 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
         "v_fmac_f64_dpp %6, %9, %15 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %9, %15 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %9, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, %10, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %10, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %10, %16 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %10, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %10, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %10, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %10, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %10, %16 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
         "v_fmac_f64_dpp %6, %10, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %10, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %10, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, %11, %17 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %11, %17 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %11, %17 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %11, %17 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %11, %17 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %11, %17 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %11, %17 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
         "v_fmac_f64_dpp %6, %11, %17 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %11, %17 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %11, %17 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, %12, %18 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %12, %18 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %12, %18 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %12, %18 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %12, %18 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %12, %18 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %12, %18 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
         "v_fmac_f64_dpp %6, %12, %18 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %12, %18 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %12, %18 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, %13, %19 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %13, %19 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %13, %19 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %13, %19 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %4, %13, %19 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %13, %19 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %13, %19 row_newbcast:7 row_mask:0xf bank_mask:0xc\n\t"
         "v_fmac_f64_dpp %6, %13, %19 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %7, %13, %19 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %13, %19 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %0, %14, %20 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %1, %14, %20 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %2, %14, %20 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %3, %14, %20 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %4, %14, %20 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %5, %14, %20 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %6, %14, %20 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %7, %14, %20 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f64_dpp %8, %14, %20 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
-        : "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9]), "+&v"(m[10])
+        : "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6]), "+&v"(m[7]), "+&v"(m[8]), "+&v"(m[9])
         : "v"(S[0]), "v"(S[1]), "v"(S[2]), "v"(S[3]), "v"(S[4]), "v"(S[5]), "v"(F[0]), "v"(F[1]), "v"(F[2]), "v"(F[3]), "v"(F[4]), "v"(F[5]));
 }
 // The twelve pivots of the Gauss-Jordan elimination, software-pipelined (pivot k's block
@@ -732,7 +743,7 @@ struct LaneConst {
     int m_vsum;     // store_ks: the sum is a J v row (bodies 0..9), else a J_a J_a^T entry (bodies 3..9)
     int rec_off;    // store_record: the lane's (q, qd) slot, 2 j, or REC_E for the dummy lanes
     int fp_off;     // store_record: REC_EE / REC_AM on lanes FR_EE_PARENT / FR_AM_PARENT, else REC_FP_SINK
-    double ancd[11];   // the same as 1.0 / 0.0: column_dots' entries are finite, so a product masks
+    double ancd[10];   // the same as 1.0 / 0.0 (rows 3 and 7 unused: bank masks): column_dots' entries are finite, so a product masks
     double cmask[9];   // composite_scan: 1.0 when body j is the parent of step s's child (edges 11-9, 10-9, 9-8, .., 3-2)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
@@ -743,6 +754,7 @@ template <int CK, bool EN>
 __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq, double cq, double qd, const double *M,
                                         double *Lk, CoopKin &kin, CoopBody &bd, const double *grav)
 {
+    PMARK(1);
     const double cz = __builtin_fma(L.rz, cq, L.nrz);   // cq on revolute lanes, 1 elsewhere
     const double sz = L.rz * sq;                         // sq on revolute lanes, 0 elsewhere
     const double qprev = shr<1>(q);
@@ -781,6 +793,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     S[1] = __builtin_fma(p[2], S[3], __builtin_fma(-p[0], S[5], w[1] * nrotf));
     S[2] = __builtin_fma(p[0], S[4], __builtin_fma(-p[1], S[3], w[2] * nrotf));
     double com[3], Iw[6], Ib[6];
+    PMARK(2);
     world_inertia<EN>(M, R, p, com, Iw, Ib);
     if constexpr (EN) inertia_to_lds(M[T_M], com, Ib, Lk + L_I + L.slot * 21);   // coop_aba's input
     {   // lanes 12..15: the table's dummy body has zero mass and inertia, so h = Ib = 0 there
@@ -843,6 +856,7 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     }
     // the frame at offset T_F of the lane's body: the EE on lane FR_EE_PARENT, the arm mount on lane
     // FR_AM_PARENT (zero offset elsewhere), for store_record
+    PMARK(3);
 #pragma unroll
     for (int r = 0; r < 3; r++)
         kin.fp[r] = __builtin_fma(R[3 * r + 2], M[T_F + 2], __builtin_fma(R[3 * r + 1], M[T_F + 1], __builtin_fma(R[3 * r], M[T_F], p[r])));
@@ -1131,7 +1145,11 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
 {
     // (h, Ib) summed over the subtree; the subtree's mass is a per-lane constant of the body table (T_MC)
     double v[9] = {bd.h[0], bd.h[1], bd.h[2], bd.Ib[0], bd.Ib[1], bd.Ib[2], bd.Ib[3], bd.Ib[4], bd.Ib[5]};
+#pragma unroll
+    for (int i = 0; i < 9; i++) PMARK_D(4, v[i]);
     composite_scan(v, L.cmask);
+#pragma unroll
+    for (int i = 0; i < 9; i++) PMARK_D(5, v[i]);
     // F = Ic S: [m v - h x w; h x v + Ib w], S = (v; w)
     const double *S = bd.S;
     const double m = L.mc, h0 = v[0], h1 = v[1], h2 = v[2];
@@ -1147,9 +1165,11 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     column_dots(S, F, Mc);
     const double diag = ((S[0] * F[0] + S[1] * F[1]) + (S[2] * F[2] + S[3] * F[3])) + (S[4] * F[4] + S[5] * F[5]);
     // strictly-upper part of column j: M_ij for the ancestors i of j (finger 11 hangs off body 9,
-    // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column
+    // not finger 10), zero elsewhere; lanes 12..15 have F = 0 and so a zero column.  Rows 3 and 7
+    // come masked by column_dots' bank masks and row 10 as zero (nobody's ancestor).
 #pragma unroll
-    for (int i = 0; i < 11; i++) Mc[i] *= L.ancd[i];
+    for (int i = 0; i < 10; i++)
+        if (i != 3 && i != 7) Mc[i] *= L.ancd[i];
     Mc[11] = 0.0;
     // row j of the block: that column, then tau_j and zeros in slots 12..15, then the diagonal over
     // slot j (LDS stores of a wave land in order).  Entry (i, j) of the block is then column i's
@@ -1163,6 +1183,8 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     Row[j] = diag;
 #pragma unroll
     for (int i = 0; i < 12; i++) Mc[i] += Lk[L_COL + i * CSTR + j];
+#pragma unroll
+    for (int i = 0; i < 12; i++) PMARK_D(6, Mc[i]);
     double nt = -Mc[0] * L.inv_m0;   // each pivot's block returns the next pivot's quotient
     gj_solve(Mc, nt, L.inv_m1);
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
@@ -1433,9 +1455,9 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             L.m_vsum = opaque_mask(m < 3);
         }
 #pragma unroll
-        for (int i = 0; i < 11; i++) {
+        for (int i = 0; i < 10; i++) {
             double d = ((anc >> i) & 1) ? 1.0 : 0.0;
-            asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
+            if (i != 3 && i != 7) asm volatile("" : "+v"(d));   // kept in registers across the loop, not rebuilt per step
             L.ancd[i] = d;
         }
         constexpr int parent[9] = {9, 9, 8, 7, 6, 5, 4, 3, 2};   // of composite_scan's children 11, 10, 9, .., 3
@@ -1508,6 +1530,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     // in flight on every step, the back edge's record stores included
     if constexpr (HO == 3) __builtin_amdgcn_s_waitcnt(0);
     for (int k = kb; k < kend; k++) {
+        PMARK(0);
         if constexpr (PROG) __hip_atomic_store(Lprog, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const double eps_l = eps_n, ub_l = ub_n;
         eps_n = np[(int64_t)(k + 1) * nstride];
@@ -1528,6 +1551,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         double qdd;
         if constexpr (EN) qdd = coop_aba<EN>(j, Lk, Lw, pe);
         else qdd = coop_solve(j, L, bd, u * L.taud, Lk);
+        PMARK_D(7, qdd);
         qd = qd + qdd * a.dt;
         q = q + qd * a.dt;
         if constexpr (EN) {   // power = (tau_u + NLE) . v_new; EnergyTank::step (energy.hpp:19-22)
@@ -1536,6 +1560,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             E = smax(0.0, E + power * a.dt);
         }
         store_record<EN>(recp(k + 1), j, L, q, qd, kin, E);
+        PMARK(1);
         fsincos(q, &sq, &cq, scK);
     }
     if (HO == 3 && kend < H - 1) {   // the next relay stage resumes at step kend

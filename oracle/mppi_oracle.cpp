@@ -39,6 +39,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../include/mppi_amd.h"
@@ -51,8 +52,21 @@ namespace orc {
 // ------------------------------------------------------------------------------------------
 struct FlopCount {
     static thread_local uint64_t flops;
+    // per-phase attribution for the executed-vs-algorithmic table (oracle_count_flops_phases):
+    // mark(p) charges the FLOPs since the last mark to phase `last` and makes p the current one
+    static thread_local uint64_t phase[8], at;
+    static thread_local int last;
+    static void mark(int p)
+    {
+        phase[last] += flops - at;
+        at = flops;
+        last = p;
+    }
 };
 thread_local uint64_t FlopCount::flops = 0;
+thread_local uint64_t FlopCount::phase[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+thread_local uint64_t FlopCount::at = 0;
+thread_local int FlopCount::last = 0;
 
 struct CF {
     double v;
@@ -568,9 +582,18 @@ template <class T> struct FrankaDynamics {
     // world coordinates (no parent/child inertia transforms), which equals the reference's
     // aba(q, v, tau_u + nle(q, v)) in exact arithmetic (pinocchio_dynamics.cpp:156-171).  The
     // world motion subspaces are the WORLD Jacobian columns; the frame velocity is J v.
+    // phases of the executed-vs-algorithmic table: 0 FK and motion subspaces, 1 world
+    // inertias, 2 the solve (articulated-body passes), 3 kinematics for the cost (EE / arm-mount
+    // positions, J v, J), 4 integration (base velocity, Euler, tank), 5 the objective (get_cost)
+    static void phase(int p)
+    {
+        if constexpr (std::is_same<T, CF>::value) FlopCount::mark(p);
+        (void)p;
+    }
     void calculate_reduced()
     {
         const int nb = M->nb;
+        phase(0);
         V3<T> Sv[MPPI_MAX_BODIES], Sw[MPPI_MAX_BODIES];
         for (int i = 0; i < nb; i++) {
             const int p = M->b[i].parent;
@@ -580,6 +603,7 @@ template <class T> struct FrankaDynamics {
             if (M->b[i].type == MPPI_JOINT_PRISMATIC) { Sv[i] = ax; Sw[i] = V3<T>(); }
             else { Sw[i] = ax; Sv[i] = cross(D.oMi[i].p, ax); }
         }
+        phase(1);
         // symmetric 6x6 articulated inertias, world frame, packed upper triangle (21)
         T Ia[MPPI_MAX_BODIES][21];
         T pA[MPPI_MAX_BODIES][6];
@@ -608,6 +632,7 @@ template <class T> struct FrankaDynamics {
                 for (int q2 = r; q2 < 6; q2++) P[k++] = full[r][q2];
             for (int j = 0; j < 6; j++) pA[i][j] = T(0);
         }
+        phase(2);
         auto idx = [](int r, int c) { if (r > c) { int t = r; r = c; c = t; } return r * 6 - r * (r - 1) / 2 + (c - r); };
         T U[MPPI_MAX_BODIES][6], Dinv[MPPI_MAX_BODIES], uu[MPPI_MAX_BODIES];
         for (int i = nb - 1; i >= 0; i--) {
@@ -645,6 +670,7 @@ template <class T> struct FrankaDynamics {
             T s6[6] = {Sv[i][0], Sv[i][1], Sv[i][2], Sw[i][0], Sw[i][1], Sw[i][2]};
             for (int r = 0; r < 6; r++) acc6[i][r] = a6[r] + s6[r] * qdd[i];
         }
+        phase(3);
         SE3<T> ee = compose(D.oMi[M->ee_parent], M->ee_place);
         SE3<T> am = compose(D.oMi[M->am_parent], M->am_place);
         ee_pos = ee.p;
@@ -666,10 +692,12 @@ template <class T> struct FrankaDynamics {
         J[2][0] = T(0); J[2][1] = T(0); J[2][2] = T(1);
         ee_lin_vel = vl;
         ee_ang_vel = vw;
+        phase(4);
     }
 
     const T *step(const T *u, T dt)
     {
+        phase(4);
         T yaw = q[2];
         T c = s_cos(yaw), s = s_sin(yaw);   // Eigen::Rotation2Dd(yaw) * base_velocity
         qd[0] = c * u[0] + (-s) * u[1];
@@ -1824,6 +1852,9 @@ double oracle_count_flops_split(const mppi_frankaridgeback_desc *desc, const mpp
     orc::CF state[MPPI_FR_STATE];
     for (int i = 0; i < MPPI_FR_STATE; i++) state[i] = orc::CF(x0[i]);
     orc::FlopCount::flops = 0;
+    for (auto &v : orc::FlopCount::phase) v = 0;   // (set_state's calculate() above is not counted)
+    orc::FlopCount::at = 0;
+    orc::FlopCount::last = 4;
     uint64_t in_cost = 0;
     for (int64_t k = 0; k < steps; k++) {
         orc::CF uu[12];
@@ -1836,6 +1867,23 @@ double oracle_count_flops_split(const mppi_frankaridgeback_desc *desc, const mpp
     }
     if (cost_part) *cost_part = (double)in_cost / (double)steps;
     return (double)orc::FlopCount::flops / (double)steps;
+}
+
+// The same count split by phase (FrankaDynamics::phase: FK, world inertias, solve, kinematics,
+// integration, objective), per rollout-step: out6[6].  Test / analysis infrastructure.
+double oracle_count_flops_phases(const mppi_frankaridgeback_desc *desc, const mppi_assisted_manipulation_desc *cost,
+                                 const double *x0, int64_t steps, double *out6)
+{
+    using orc::FlopCount;
+    double cost_part = 0.0;
+    // get_cost is phase 5: oracle_count_flops_split times it, the rest is marked inside the dynamics
+    const double tot = oracle_count_flops_split(desc, cost, x0, steps, &cost_part);
+    FlopCount::mark(4);
+    // every get_cost ran inside phase 4 (between step()'s marks): move its FLOPs to phase 5
+    FlopCount::phase[4] -= (uint64_t)(cost_part * (double)steps + 0.5);
+    FlopCount::phase[5] = (uint64_t)(cost_part * (double)steps + 0.5);
+    for (int p = 0; p < 6; p++) out6[p] = (double)FlopCount::phase[p] / (double)steps;
+    return tot;
 }
 
 double oracle_count_flops(const mppi_frankaridgeback_desc *desc, const mppi_assisted_manipulation_desc *cost,

@@ -70,6 +70,9 @@ def lib(path=None):
     L.oracle_count_flops_split.restype = C.c_double
     L.oracle_count_flops_split.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
                                            C.POINTER(abi.mppi_assisted_manipulation_desc), dp, C.c_int64, dp]
+    L.oracle_count_flops_phases.restype = C.c_double
+    L.oracle_count_flops_phases.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
+                                            C.POINTER(abi.mppi_assisted_manipulation_desc), dp, C.c_int64, dp]
     L.oracle_count_flops.restype = C.c_double
     L.oracle_count_flops.argtypes = [C.POINTER(abi.mppi_frankaridgeback_desc),
                                      C.POINTER(abi.mppi_assisted_manipulation_desc), dp, i64]
@@ -139,6 +142,17 @@ def count_flops_split(model, cost, x0, steps=64):
     part = C.c_double(0.0)
     tot = lib().oracle_count_flops_split(C.byref(model), C.byref(cost), _p(x0), steps, C.byref(part))
     return tot, part.value
+
+
+FLOP_PHASES = ("fk", "world_inertia", "solve", "kinematics", "integration", "objective")
+
+
+def count_flops_phases(model, cost, x0, steps=64):
+    """(total, {phase: FLOPs}) algorithmic FLOPs per rollout-step by phase (FLOP_PHASES)."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    out = np.zeros(6)
+    tot = lib().oracle_count_flops_phases(C.byref(model), C.byref(cost), _p(x0), steps, _p(out))
+    return tot, dict(zip(FLOP_PHASES, out.tolist()))
 
 
 def count_flops(model, cost, x0, steps=64):
