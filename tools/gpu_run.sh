@@ -220,7 +220,7 @@ step_wtrace() {   # variant
     local lib=$PWD/gpurun_variants/$1/libmppi_amd.so
     MPPI_WAVE_TRACE=$PWD/$O/wt.bin MPPI_AMD_LIB=$lib timeout -k 10 120 python bench.py --steps 40 --warmup 10 \
         --no-cpu-baseline $BENCH_ARGS > $O/wt.json 2> $O/wt.err || { echo "wtrace rc=$?"; tail $O/wt.err; return 1; }
-    python3 tools/wave_trace_r03.py $O/wt.bin 1064 relay
+    python3 tools/wave_trace_r06.py $O/wt.bin 1064 | tee $O/wave_trace.txt
 }
 
 for s in "$@"; do
