@@ -1745,8 +1745,23 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
         const int64_t r = lr0 + lane;
         if (row_live(a, r)) {
             const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
+            // J += c_q in step order, the loads sixteen at a time: one LDS round trip per sixteen
+            // adds, not per add (the one-by-one loop waited on every ds_read: ~3 us at the end of
+            // every workgroup's last chunk)
             double J = 0.0;
-            for (int q = 0; q < H; q++) J += cr[q];
+            int q = 0;
+            for (; q + 16 <= H; q += 16) {
+                double c[16];
+#pragma unroll
+                for (int u = 0; u < 16; u += 2) {
+                    const double2 v = *reinterpret_cast<const double2 *>(cr + q + u);
+                    c[u] = v.x;
+                    c[u + 1] = v.y;
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) J += c[u];
+            }
+            for (; q < H; q++) J += cr[q];
             J = isnan(J) ? (double)NAN : J;
             if (a.fcost != nullptr && r == a.count) {
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
@@ -2019,7 +2034,7 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __shared__ int Lflag[LF_N];      // records stored (main waves, relay), kept columns copied
     __shared__ int Lq[Q_N];          // the main waves' steps, chunk counters, the relay's stage
     __shared__ double Lst[64 * 3];   // the relay's (q, qd, E) per lane between stages
-    __shared__ double Lcs[5 * ROWS_PER_WAVE * HC_MAX];   // step costs of the groups' rows
+    __shared__ __attribute__((aligned(16))) double Lcs[5 * ROWS_PER_WAVE * HC_MAX];   // step costs of the groups' rows
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;

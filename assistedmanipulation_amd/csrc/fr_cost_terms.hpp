@@ -351,7 +351,16 @@ __device__ __forceinline__ double rollout_cost(const DevCost &Cs, const StepCons
         const int n = (H - base < 64) ? H - base : 64;
         const int k = base + (lane < n ? lane : 0);
         const double c = record_step_cost<CK, EN, JS, KC>(Cs, stp[k], rec + (int64_t)k * RS, Lj);
-        for (int i = 0; i < n; i++) J += readlane_f64(c, i);
+        // J += c_i in step order; the lane reads eight at a time, ahead of their adds
+        int i = 0;
+        for (; i + 8 <= n; i += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = readlane_f64(c, i + u);
+#pragma unroll
+            for (int u = 0; u < 8; u++) J += v[u];
+        }
+        for (; i < n; i++) J += readlane_f64(c, i);
     }
     return isnan(J) ? (double)NAN : J;
 }
