@@ -1520,8 +1520,9 @@ static mppi_status launch_filter_standalone(mppi_handle *h)
         // the row's objective after its loop (fr_coop_kernel's one-wave path)
         a.costs_in_launch = fr_coop_costs_in_launch(h->env) ? 1 : 0;
         HIP_TRY(launch_fr_coop(a, h->stream_opt));
-        if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a, true), h->stream_opt));
-        h->opt_rec_compact = true;   // launch_fr_coop: fr_coop_kernel's compact records
+        const bool compact = fr_coop_compact(a);   // (false: the standalone row keeps the 768-B record)
+        if (!a.costs_in_launch) HIP_TRY(launch_fr_step_cost(cost_args(h, a, compact), h->stream_opt));
+        h->opt_rec_compact = compact;
     } else {
         PmRolloutArgs a{};
         a.pm = h->d_pm;

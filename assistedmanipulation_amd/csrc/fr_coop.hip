@@ -1585,16 +1585,15 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
 // parameters are the body table's T_LO .. T_VW fields (stride MB).
 
 // J of local rollout lr (or the folded filter() row) from its records, written out
-template <int CK, bool EN>
+template <int CK, bool EN, bool KC>
 __device__ __forceinline__ void launch_row_cost(const FrRolloutArgs &a, int64_t lr, int lane, const double *Lmodel)
 {
     const bool frow = a.fcost != nullptr && lr == a.count;
     if (!(lr < a.count || frow)) return;
     if (frow && (a.status->all_nan || a.status->sg_error)) return;   // no filter() when the update threw
-    // (fr_coop_kernel's compact records)
-    const double J = mppi_cost::rollout_cost<CK, EN, MB, true>(*a.cost, frow ? a.fsteps : a.steps,
-                                                                frow ? a.frec : a.rec + lr * a.H * FR_REC_C, a.H, lane,
-                                                                Lmodel + T_LO);
+    const double J = mppi_cost::rollout_cost<CK, EN, MB, KC>(*a.cost, frow ? a.fsteps : a.steps,
+                                                              frow ? a.frec : a.rec + lr * a.H * (KC ? FR_REC_C : FR_REC), a.H,
+                                                              lane, Lmodel + T_LO);
     if (lane == 0) {
         if (frow) *a.fcost = J;
         else {
@@ -1830,14 +1829,14 @@ __device__ __forceinline__ void group_draws(const FrRolloutArgs &a, int g, int l
 
 // fr_coop_kernel's four-wave launch (no rows left over): each main wave evaluates its own rows'
 // objective after its loop (rollout_cost, a pass per row, lane = step) and makes their next draws
-template <int CK, bool EN>
+template <int CK, bool EN, bool KC>
 __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int lane, const double *Lmodel)
 {
     const int64_t w0 = (int64_t)blockIdx.x * 4;
     __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
-    for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
+    for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN, KC>(a, (w0 + wv) * ROWS_PER_WAVE + i, lane, Lmodel);
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
@@ -1975,7 +1974,9 @@ __device__ __forceinline__ void block0_sample_writes(const FrRolloutArgs &a, int
 // waves per CU but not per SIMD: the ~9 % of SIMDs it gave two waves ran 1.23x longer and set the
 // kernel's time, and a separate launch for the leftover rows was placed by XCD round-robin, not
 // on the free CU (per-block traces, tools/wave_trace.py).
-template <int CK, bool EN, int WPB, bool FROW>
+// KC: compact records with the kinematic sums on the rows' chains (the update's launches, throughput-
+// bound); the standalone filter() row (one latency-bound row) keeps the 768-B record and a shorter step.
+template <int CK, bool EN, int WPB, bool FROW, bool KC>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))) void fr_coop_kernel(FrRolloutArgs a)
 {
     constexpr int KS = EN ? LDS_KIN_EN : LDS_KIN;
@@ -2000,10 +2001,10 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
             kept_rows_wave(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, rk);
         }
     }
-    coop_rows<CK, EN, FROW, 0, false, true>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS,
-                                            lds_scr + wrow * LDS_SCR, Lmodel, Lx0);
+    coop_rows<CK, EN, FROW, 0, false, KC>(a, (int64_t)wblk * ROWS_PER_WAVE + rowi, lane, wblk, lds_kin + wrow * KS,
+                                          lds_scr + wrow * LDS_SCR, Lmodel, Lx0);
     if constexpr (WPB == 4) {
-        if (a.costs_in_launch) launch_costs<CK, EN>(a, wv, lane, Lmodel);
+        if (a.costs_in_launch) launch_costs<CK, EN, KC>(a, wv, lane, Lmodel);
     } else if constexpr (WPB == 1) {
         // past one round (two waves per SIMD, several rounds): the wave's own rows' objective after
         // its loop, while the launch's other waves still run, instead of fr_step_cost_kernel after it
@@ -2011,7 +2012,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(2, 2))
             __builtin_amdgcn_s_waitcnt(0);   // the wave's own record stores, read back by other lanes
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
-            for (int i = 0; i < ROWS_PER_WAVE; i++) launch_row_cost<CK, EN>(a, (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
+            for (int i = 0; i < ROWS_PER_WAVE; i++)
+                launch_row_cost<CK, EN, KC>(a, (int64_t)blockIdx.x * ROWS_PER_WAVE + i, lane, Lmodel);
         }
     }
 }
@@ -2105,11 +2107,11 @@ static unsigned one_per_cu_pad(K kernel, int wpb)
     return at.sharedSizeBytes >= want ? 0u : (unsigned)(want - at.sharedSizeBytes);
 }
 
-template <int CK, bool EN, int WPB, bool FROW>
+template <int CK, bool EN, int WPB, bool FROW, bool KC>
 static void launch_k(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
-    static const unsigned pad = one_per_cu_pad(fr_coop_kernel<CK, EN, WPB, FROW>, WPB);
-    hipLaunchKernelGGL((fr_coop_kernel<CK, EN, WPB, FROW>), dim3(nb), dim3(64 * WPB), pad, s, a);
+    static const unsigned pad = one_per_cu_pad(fr_coop_kernel<CK, EN, WPB, FROW, KC>, WPB);
+    hipLaunchKernelGGL((fr_coop_kernel<CK, EN, WPB, FROW, KC>), dim3(nb), dim3(64 * WPB), pad, s, a);
 }
 
 template <int CK, bool EN>
@@ -2119,19 +2121,22 @@ static void launch_x(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
     hipLaunchKernelGGL((fr_coop_x_kernel<CK, EN>), dim3(nb), dim3(64 * XW), pad, s, a);
 }
 
-template <int WPB, bool FROW>
+template <int WPB, bool FROW, bool KC>
 static void launch_one(const FrRolloutArgs &a, unsigned nb, hipStream_t s)
 {
-    if (a.cost_kind == CK_TRACK_POINT) launch_k<CK_TRACK_POINT, false, WPB, FROW>(a, nb, s);
-    else if (a.energy) launch_k<CK_ASSISTED_MANIPULATION, true, WPB, FROW>(a, nb, s);
-    else launch_k<CK_ASSISTED_MANIPULATION, false, WPB, FROW>(a, nb, s);
+    if (a.cost_kind == CK_TRACK_POINT) launch_k<CK_TRACK_POINT, false, WPB, FROW, KC>(a, nb, s);
+    else if (a.energy) launch_k<CK_ASSISTED_MANIPULATION, true, WPB, FROW, KC>(a, nb, s);
+    else launch_k<CK_ASSISTED_MANIPULATION, false, WPB, FROW, KC>(a, nb, s);
 }
+
+bool fr_coop_compact(const FrRolloutArgs &a) { return !a.optimal; }
 
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s)
 {
     const unsigned nb = (unsigned)((a.count + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
     if (nb == 0) return hipSuccess;
-    launch_one<1, false>(a, nb, s);
+    if (fr_coop_compact(a)) launch_one<1, false, true>(a, nb, s);
+    else launch_one<1, false, false>(a, nb, s);   // the standalone filter() row
     return hipGetLastError();
 }
 
@@ -2287,7 +2292,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
     if (tail) *tail = CoopTail{0, a.xbase, (int)((xrows + 3) / 4), 1};
     if (dry) return hipSuccess;
     if (e0) (void)hipEventRecord(e0, s);
-    if (xrows == 0) launch_one<4, false>(a, (unsigned)groups, s);
+    if (xrows == 0) launch_one<4, false, true>(a, (unsigned)groups, s);
     else launch_x_any(a, (unsigned)groups, s);
     if (e1) (void)hipEventRecord(e1, s);
     return hipGetLastError();

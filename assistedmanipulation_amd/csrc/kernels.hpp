@@ -311,6 +311,9 @@ static_assert(GRAD_SPLIT == sizeof(Status::tsplit) / sizeof(double), "normaliser
 // sum_splits (sharded): the GRAD_SPLIT partials are summed into gpart for the all-reduce
 hipError_t launch_weights_gradient(const WGradArgs &a, double *gpart, bool sum_splits, hipStream_t s);
 hipError_t launch_fr_coop(const FrRolloutArgs &a, hipStream_t s);
+// whether launch_fr_coop writes compact records (FR_REC_C): every launch but the standalone filter()
+// row's (a.optimal), which keeps the 768-B record and the shorter step of a latency-bound row
+bool fr_coop_compact(const FrRolloutArgs &a);
 // The update's rollouts (fr_coop_x_kernel): one workgroup per CU of four one-SIMD waves of rollouts
 // plus a fifth wave for the rows left over (and, when there are some, the previous update's
 // filter() as one more row: *folded).  Falls back to launch_fr_coop beyond one round of CUs.
