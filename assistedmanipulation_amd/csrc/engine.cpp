@@ -43,6 +43,8 @@ EnvSwitches env_switches_read()
     e.handover_off = is("MPPI_HANDOVER", '0');
     e.split_off = is("MPPI_SPLIT", '0');
     e.stream_prio_off = is("MPPI_STREAM_PRIO", '0');
+    const char *rk = std::getenv("MPPI_RELAY_K");
+    e.relay_k = (rk && rk[0] >= '1' && rk[0] <= '0' + RELAY_K_MAX) ? rk[0] - '0' : 0;
     return e;
 }
 }  // namespace mppi_eng
@@ -170,6 +172,8 @@ struct mppi_handle {
     double *d_wexp = nullptr, *d_wpart = nullptr;   // unnormalised weights e_r; large-R softmin partials
     // cooperative kernel's step records [Rpad][H][FR_REC] and the filter() row's [H][FR_REC]
     double *d_rec = nullptr, *d_rec_opt = nullptr;
+    RelayXfer *d_rx = nullptr;     // the relay's hand-offs between workgroups (fr_coop.hip relay_stage)
+    uint32_t relay_token = 0;      // one per rollout launch (nonzero)
     bool opt_rec_compact = false;   // d_rec_opt holds compact records (the standalone filter()), else 768-B ones (folded)
     uint32_t *d_trace = nullptr;   // MPPI_WAVE_TRACE=<file>: per-block timing of the rollout kernel (COOP_TRACE builds)
     std::string trace_path;
@@ -981,6 +985,10 @@ mppi_status mppi_create(const mppi_config *cfg, const mppi_dynamics_desc *dyn, c
     CREATE_TRY(dalloc(h, &h->d_T, (size_t)(Cd * Cd)));
     CREATE_TRY(dalloc(h, &h->d_opt, 1));
     CREATE_TRY(dalloc(h, &h->d_rec_opt, (size_t)(h->H * FR_REC)));
+    if (dyn->kind == MPPI_DYNAMICS_FRANKARIDGEBACK) {   // the relay's hand-off slots; tokens start at 0 (never a launch's)
+        CREATE_TRY(dalloc(h, &h->d_rx, (size_t)RELAY_GROUPS_MAX));
+        CREATE_TRY(hipMemset(h->d_rx, 0, sizeof(RelayXfer) * RELAY_GROUPS_MAX));
+    }
     CREATE_TRY(dalloc(h, &h->d_cmin, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_cmax, (size_t)Cd));
     CREATE_TRY(dalloc(h, &h->d_rank, (size_t)h->R));
@@ -1658,6 +1666,8 @@ mppi_status mppi_update_phase1(mppi_handle *h, const double *state, double time)
         a.energy = h->cost_kind == MPPI_COST_ASSISTED_MANIPULATION && h->am.enable_energy_limit;
         a.trace = h->d_trace;
         a.rec = h->d_rec;
+        a.rx = h->d_rx;
+        a.rtoken = ++h->relay_token ? h->relay_token : ++h->relay_token;   // (never 0)
         // sharded: this rank's wait timeouts into cost slot R, which the all-reduce carries to every rank
         a.wait_sum = h->comm ? h->d_costs_local + h->R : (sharded(h) ? h->d_costs + h->R : nullptr);
         if (h->debug_updates > 0) {   // mppi_debug_inject: this update's launch carries the fault

@@ -34,6 +34,7 @@
 // The rollout runs all H - 1 steps: a NaN step cost makes the rollout's sum NaN whatever follows.
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -1629,6 +1630,22 @@ __device__ __forceinline__ void wait_records(const FrRolloutArgs &a, int *flag)
     }
     if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
 }
+// The relay's wait across workgroups: until a token word holds this launch's token (a.rtoken).  The
+// producer stores its payload sc1 (agent-scope relaxed stores), waits for every one of them
+// (s_waitcnt 0), then one lane stores the token sc1; this wave polls with sc1 loads and loads the
+// payload with sc1 loads after the match (MI355X_MICROARCH.md, inter-workgroup visibility: one
+// storing wave, sc1 both sides, the polling wave loads).  Bounded; returns whether it arrived.
+__device__ __forceinline__ bool wait_token(const FrRolloutArgs &a, uint32_t *word)
+{
+    for (int i = 0; i < WAIT_SPINS; i++) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == a.rtoken)
+            return true;
+        __builtin_amdgcn_s_sleep(4);
+    }
+    if ((threadIdx.x & 63) == 0) note_wait_timeout(a);
+    return false;
+}
+
 // the same bounded wait, returning the value it saw (0 if it gave up)
 __device__ __forceinline__ int wait_nonzero(const FrRolloutArgs &a, int *word)
 {
@@ -1705,10 +1722,41 @@ __device__ __forceinline__ int lds_read(int *w)
 {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
+// The relay over a.relay_k workgroups: relay group q (rows [xbase + 4 q, xbase + 4 q + 4)) runs in
+// workgroups q + RELAY_STRIDE m, m < relay_k (one XCD under the dispatcher's round-robin placement:
+// speed only, nothing relies on it), member m over chunks [m nch / K, (m + 1) nch / K) of the horizon
+// - the records member m stores are the ones it evaluates.  -1: the workgroup holds no relay rows.
+__device__ __forceinline__ int relay_member(const FrRolloutArgs &a)
+{
+    const int nxb = (int)((a.xrows + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE);
+    const int q = (int)blockIdx.x % RELAY_STRIDE, m = (int)blockIdx.x / RELAY_STRIDE;
+    return (q < nxb && m < a.relay_k) ? m : -1;
+}
+// member m's first loop step: 0, else the step that stores the first record of its first chunk
+__device__ __forceinline__ int relay_member_step(const FrRolloutArgs &a, int m, int H)
+{
+    if (m <= 0) return 0;
+    if (m >= a.relay_k) return H - 1;
+    return (m * ((H + CH - 1) / CH) / a.relay_k) * CH - 1;
+}
 // first launch row of group g (main wave g of the workgroup, or the relay's rows for g = 4)
 __device__ __forceinline__ int64_t group_row0(const FrRolloutArgs &a, int g)
 {
-    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE;
+    return g < 4 ? ((int64_t)blockIdx.x * 4 + g) * ROWS_PER_WAVE
+                 : a.xbase + (int64_t)((int)blockIdx.x % RELAY_STRIDE) * ROWS_PER_WAVE;
+}
+// the chunks [c0, c1) of group g this workgroup evaluates: a main wave's every chunk; of the relay's
+// rows, its member's share
+__device__ __forceinline__ void group_chunks(const FrRolloutArgs &a, int g, int &c0, int &c1)
+{
+    const int nch = (a.H + CH - 1) / CH;
+    c0 = 0;
+    c1 = nch;
+    if (g == 4 && a.relay_k > 1) {
+        const int m = (int)blockIdx.x / RELAY_STRIDE;
+        c0 = m * nch / a.relay_k;
+        c1 = (m + 1) * nch / a.relay_k;
+    }
 }
 // whether chunk c of group g can be read: its records are complete
 __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
@@ -1725,7 +1773,8 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
                                           int *Lq)
 {
     const int H = a.H;
-    const int nch = (H + CH - 1) / CH;   // the group's chunks
+    int cb, ce;
+    group_chunks(a, g, cb, ce);   // the group's chunks in this workgroup
     const int i = lane >> 4, k = c * CH + (lane & 15);
     const int64_t lr0 = group_row0(a, g), lr = lr0 + i;
     const bool rl = row_live(a, lr), live = rl && k < H;
@@ -1739,17 +1788,29 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     // the stores before the count: the wave that completes the group reads every chunk's costs
     const int n = __builtin_amdgcn_readfirstlane(
         __hip_atomic_fetch_add(Lq + Q_DONE + g, lane == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (n + 1 != nch) return;
+    if (n + 1 != ce - cb) return;
+    // the relay's rows over several workgroups: the partial sums arrive from the previous member and
+    // go on to the next (the reference's J += cost in step order across the members)
+    const int m = (int)blockIdx.x / RELAY_STRIDE;
+    const bool from_prev = g == 4 && a.relay_k > 1 && m > 0;
+    const bool to_next = g == 4 && a.relay_k > 1 && m + 1 < a.relay_k;
+    RelayXfer *x = (from_prev || to_next) ? a.rx + ((int)blockIdx.x % RELAY_STRIDE) : nullptr;
+    double J0 = 0.0;
+    if (from_prev) {   // bounded; on a timeout the update fails (wait_timeouts)
+        const bool ok = wait_token(a, &x->sums_tok[m - 1][0]);
+        J0 = (ok && lane < ROWS_PER_WAVE) ? __hip_atomic_load(&x->sums[m - 1][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    }
     if (lane < ROWS_PER_WAVE) {
         const int64_t r = lr0 + lane;
-        if (row_live(a, r)) {
+        if (row_live(a, r) || to_next) {
             const double *cr = Lcs + (g * ROWS_PER_WAVE + lane) * HC_MAX;
             // J += c_q in step order, the loads sixteen at a time: one LDS round trip per sixteen
             // adds, not per add (the one-by-one loop waited on every ds_read: ~3 us at the end of
             // every workgroup's last chunk)
-            double J = 0.0;
-            int q = 0;
-            for (; q + 16 <= H; q += 16) {
+            double J = J0;
+            const int Hend = min(ce * CH, H);
+            int q = cb * CH;
+            for (; q + 16 <= Hend; q += 16) {
                 double c[16];
 #pragma unroll
                 for (int u = 0; u < 16; u += 2) {
@@ -1760,7 +1821,13 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
 #pragma unroll
                 for (int u = 0; u < 16; u++) J += c[u];
             }
-            for (; q < H; q++) J += cr[q];
+            for (; q < Hend; q++) J += cr[q];
+            if (to_next) {   // the next member continues from these (sc1, then the token)
+                __hip_atomic_store(&x->sums[m][lane], J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_waitcnt(0);
+                if (lane == 0) __hip_atomic_store(&x->sums_tok[m][0], a.rtoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
             J = isnan(J) ? (double)NAN : J;
             if (a.fcost != nullptr && r == a.count) {
                 if (!(a.status->all_nan || a.status->sg_error)) *a.fcost = J;   // no filter() when the update threw
@@ -1779,13 +1846,14 @@ template <int CK, bool EN>
 __device__ __forceinline__ void cost_work(const FrRolloutArgs &a, int first, int ng, int lane, const double *Lmodel,
                                          double *Lcs, int *Lflag, int *Lq)
 {
-    const int nch = (a.H + CH - 1) / CH;
 #pragma unroll 1
     for (int spin = 0; spin < WAIT_SPINS; spin++) {
         bool left = false, did = false;
 #pragma unroll 1
         for (int d = 0; d < ng && !did; d++) {
             const int g = first + d < ng ? first + d : first + d - ng;
+            int cb, nch;
+            group_chunks(a, g, cb, nch);   // (Lq[Q_NEXT + g] starts at cb)
             const int c0 = lds_read(Lq + Q_NEXT + g);
             if (c0 >= nch) continue;
             left = true;
@@ -1840,60 +1908,86 @@ __device__ __forceinline__ void launch_costs(const FrRolloutArgs &a, int wv, int
     if (a.ahead_noise) tail_draws(a, (w0 + wv) * ROWS_PER_WAVE, lane);
 }
 
-// Relay stage r's steps [relay_step(r), relay_step(r + 1)): quarters of the H - 1 loop steps
-__device__ __forceinline__ int relay_step(int r, int H) { return r >= 4 ? H - 1 : (r * (H - 1)) / 4; }
+// Relay stage r's steps [relay_step(r), relay_step(r + 1)): member m = r / 4 of the relay runs stages
+// 4 m .. 4 m + 3, quarters of its steps; one member: quarters of the H - 1 loop steps
+__device__ __forceinline__ int relay_step(const FrRolloutArgs &a, int r, int H)
+{
+    if (r >= 4 * a.relay_k) return H - 1;
+    const int m = r / 4, k0 = relay_member_step(a, m, H), k1 = relay_member_step(a, m + 1, H);
+    return k0 + ((r % 4) * (k1 - k0)) / 4;
+}
 
-// Relay stage r (wave 4 + r) of a workgroup with rows left over (a.handover): makes the next
-// update's draws for main wave r's rows (r > 0; wave 0's are left to rank_draw_kernel, as the
-// engine expects of the first wave of these workgroups), waits for stage r - 1 (Lq[Q_STAGE] == r),
-// runs its quarter of the horizon at priority 3 and passes the state on; the last stage raises the
-// relay's records flag.  Without a.handover wave 4 runs every step itself at the main waves'
-// priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the stage ran (false: the
-// previous stage never signalled, counted in Status::wait_timeouts).
+// Relay stage s (wave 4 + s) of member m of a relay group (a.handover): makes the next update's draws
+// for main wave s's rows (but main wave 0's of member 0, which rank_draw_kernel makes, as the engine
+// expects of the first wave of these workgroups), waits for stage s - 1 (Lq[Q_STAGE] == s) - or, as
+// a later member's first stage, for the previous member's state (rx, sc1, the launch's token) -
+// runs its part of the horizon at priority 3 and passes the state on; each member's last stage
+// raises its workgroup's relay records flag.  With relay_k members every SIMD that hosts a stage
+// carries 1 / (4 relay_k) of the extra wave instead of a quarter (the host main waves lost ~20 us
+// each to their stage with one member, r06 wave traces); the stages' loop is the same code, only the
+// hand-off crosses workgroups, once per member.  Without a.handover wave 4 runs every step itself
+// at the main waves' priority (the doubled SIMD of round 2, kept for A/B).  Returns whether the
+// stage ran (false: the previous stage never signalled, counted in Status::wait_timeouts).
 template <int CK, bool EN>
-__device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int r, int lane, double *Lk, double *Lw,
+__device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m, int lane, double *Lk, double *Lw,
                                             const double *Lmodel, const double *Lx0, int *Lflag, int *Lq, double *Lst)
 {
     const int H = a.H;
-    const int64_t xlr = a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + (lane >> 4);
-    const int wblk = gridDim.x * 4 + blockIdx.x;
+    const int q = (int)blockIdx.x % RELAY_STRIDE;
+    const int64_t xlr = a.xbase + (int64_t)q * ROWS_PER_WAVE + (lane >> 4);
+    const int wblk = gridDim.x * 4 + q;   // (the relay rows' trace slot)
+    const int r = 4 * m + s;
     int kb = 0, ke = 0x7FFFFFFF;   // without a.handover: every step on this wave (one stage)
     if (a.handover) {
-        // the next update's draws for main wave r's rows first (block 0's wave 0 rows are left to
-        // rank_draw_kernel)
-        if (r > 0 && a.ahead_noise) group_draws(a, r, lane, Lflag);
-        if (r > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
+        // the next update's draws for main wave s's rows first (member 0's wave 0 rows are left
+        // to rank_draw_kernel)
+        if ((s > 0 || m > 0) && a.ahead_noise) group_draws(a, s, lane, Lflag);
+        if (s > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
             int st = 0;
-            for (int i = 0; i < (1 << 22) && st < r; i++) {
+            for (int i = 0; i < (1 << 22) && st < s; i++) {
                 st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (st < r) __builtin_amdgcn_s_sleep(2);
+                if (st < s) __builtin_amdgcn_s_sleep(2);
             }
-            if (st < r) {
+            if (st < s) {
                 if (lane == 0) note_wait_timeout(a);
                 return false;
             }
+        } else if (m > 0) {   // the previous member's lanes' state (sc1 loads after the token), into Lst
+            RelayXfer *x = a.rx + q;
+            if (!wait_token(a, &x->state_tok[m - 1][0])) return false;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                Lst[3 * lane + c] = __hip_atomic_load(&x->state[m - 1][3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __builtin_amdgcn_s_setprio(3);   // above the main waves (1) and the objective's (0)
-        kb = relay_step(r, H);
-        ke = relay_step(r + 1, H);
+        kb = relay_step(a, r, H);
+        ke = relay_step(a, r + 1, H);
     }
     // one call site: one copy of the step loop for both shapes
     coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke);
     if (a.handover) {
         __builtin_amdgcn_s_setprio(0);
-#ifdef COOP_TRACE   // the stages' ends in the slot after the first relay's (block 0)
-        if (a.trace && blockIdx.x == 0 && lane == 0 && r < 4) a.trace[4 * (wblk + 1) + r] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#ifdef COOP_TRACE   // the stages' ends of relay group 0, member m in the slot 1 + m past the relay rows'
+        if (a.trace && q == 0 && lane == 0) a.trace[4 * (gridDim.x * 4 + 1 + m) + s] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (r < 3) {   // the state in Lst (and this stage's records) before the next stage starts
+        if (s < 3) {   // the state in Lst (and this stage's records) before the next stage starts
             __builtin_amdgcn_s_waitcnt(0);
             // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
             if (!((a.debug & 1) && r == 1))
-                __hip_atomic_store(Lq + Q_STAGE, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(Lq + Q_STAGE, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             return true;
         }
+        if (m + 1 < a.relay_k) {   // the last stage of a member: the state to the next member (sc1), then the token
+            RelayXfer *x = a.rx + q;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                __hip_atomic_store(&x->state[m][3 * lane + c], Lst[3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) __hip_atomic_store(&x->state_tok[m][0], a.rtoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(1, H) : -1;
-    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);
+    if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(a, 1, H) : -1;
+    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);   // this workgroup's relay records are stored
     return true;
 }
 
@@ -1918,7 +2012,9 @@ __device__ __forceinline__ int kept_rank(const FrRolloutArgs &a, int64_t lr)
     const int64_t g = a.samp.begin + lr;
     return (a.drawn_ahead && lr < a.count && g >= 2) ? a.samp.rank[g] : 0x7FFFFFFF;
 }
-__device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t lr, int lane, int rk)
+// [kmin, kmax): the steps whose columns this wave copies (a relay member: the steps it runs)
+__device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t lr, int lane, int rk, int kmin = 0,
+                                               int kmax = 0x7FFFFFFF)
 {
     const SampleArgs &sa = a.samp;
     const bool kept = rk < sa.sp.keep;
@@ -1926,25 +2022,26 @@ __device__ __forceinline__ void kept_rows_wave(const FrRolloutArgs &a, int64_t l
     const int j = lane & 15;
     if (kept && j < 12) {
         const int blk = j % 3, ph = j / 3;
-        const int kend = sa.sp.shift_by > 0 ? (int)sa.sp.shifted : sa.H;
+        const int kend = min(sa.sp.shift_by > 0 ? (int)sa.sp.shifted : sa.H, kmax);
+        const int kst = kmin <= ph ? ph : ph + ((kmin - ph + 3) / 4) * 4;   // the first step >= kmin of this phase
         const int64_t sh = sa.sp.shift_by > 0 ? sa.sp.shift_by : 0;
         constexpr int UN = 8;
         typedef double d2v __attribute__((ext_vector_type(2)));   // (HIP's double2 kept v on the stack)
-        for (int k0 = ph; k0 < kend; k0 += 4 * UN) {
+        for (int k0 = kst; k0 < kend; k0 += 4 * UN) {
             d2v v[UN][2];
 #pragma unroll
             for (int u = 0; u < UN; u++) {
-                const int k = k0 + 4 * u < kend ? k0 + 4 * u : ph;
+                const int k = k0 + 4 * u < kend ? k0 + 4 * u : kst;
                 const d2v *src = reinterpret_cast<const d2v *>(sa.prev + (((int64_t)k + sh) * sa.Rpad + lr) * FR_C + 4 * blk);
                 v[u][0] = src[0];
                 v[u][1] = src[1];
             }
-            // past kend the loads read step ph's source and the stores rewrite step ph with it (the
+            // past kend the loads read step kst's source and the stores rewrite step kst with it (the
             // value its first store wrote): no branch per store, so v stays in registers (a
             // conditional store sequence put it on the stack)
 #pragma unroll
             for (int u = 0; u < UN; u++) {
-                const int k = k0 + 4 * u < kend ? k0 + 4 * u : ph;
+                const int k = k0 + 4 * u < kend ? k0 + 4 * u : kst;
                 double *dst = sa.noise + ((int64_t)k * sa.Rpad + lr) * FR_C + 4 * blk;
                 reinterpret_cast<d2v *>(dst)[0] = v[u][0];
                 reinterpret_cast<d2v *>(dst)[1] = v[u][1];
@@ -2040,23 +2137,31 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int wv = (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int rowi = lane >> 4;
+    const int member = relay_member(a);   // of the relay rows this workgroup carries (-1: none)
+    const bool xr = member >= 0;
     const int64_t lr = wv < 4 ? (int64_t)(blockIdx.x * 4 + wv) * ROWS_PER_WAVE + rowi
-                              : a.xbase + (int64_t)blockIdx.x * ROWS_PER_WAVE + rowi;   // this lane's row (waves < 5)
-    const int rk = wv < 5 ? kept_rank(a, lr) : 0x7FFFFFFF;
+                              : a.xbase + (int64_t)((int)blockIdx.x % RELAY_STRIDE) * ROWS_PER_WAVE + rowi;   // (waves < 5)
+    const int rk = (wv < 4 || (wv == 4 && xr)) ? kept_rank(a, lr) : 0x7FFFFFFF;
     stage_body_table(a, Lmodel, 64 * XW);
     stage_x0(a, Lx0);
     if (threadIdx.x < LF_N) Lflag[threadIdx.x] = 0;
     if (threadIdx.x < Q_N) Lq[threadIdx.x] = threadIdx.x < Q_NEXT ? -1 : 0;
-    const bool xr = (int64_t)blockIdx.x * ROWS_PER_WAVE < a.xrows;   // the workgroup has relay rows
     const int ng = xr ? 5 : 4;   // row groups of the objective
-    if (!xr && threadIdx.x == Q_NEXT + 4) Lq[Q_NEXT + 4] = 0x7FFF;   // no relay group
+    if (threadIdx.x == Q_NEXT + 4) {   // the relay group's first chunk here (none: past every chunk)
+        int cb, ce;
+        group_chunks(a, 4, cb, ce);
+        Lq[Q_NEXT + 4] = xr ? cb : 0x7FFF;
+    }
     __syncthreads();
     // main wave w's rows use slots 4 w + i, the relay's rows (whichever wave runs them) 16 + i
     const int slot = wv < 4 ? wv * ROWS_PER_WAVE + rowi : 4 * ROWS_PER_WAVE + rowi;
     double *Lk = lds_kin + slot * KS, *Lw = lds_scr + slot * LDS_SCR;
     if (a.drawn_ahead) {
         if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the SIMD of the relay's first stage
-        if (wv < 4 || (wv == 4 && xr)) kept_rows_wave(a, lr, lane, rk);
+        if (wv < 4) kept_rows_wave(a, lr, lane, rk);
+        else if (wv == 4 && xr)   // the relay rows' columns of the steps this member runs
+            kept_rows_wave(a, lr, lane, rk, relay_member_step(a, member, a.H),
+                           member + 1 < a.relay_k ? relay_member_step(a, member + 1, a.H) : 0x7FFFFFFF);
     }
     const bool cil = a.costs_in_launch != 0;
     if (wv < 4) {
@@ -2079,11 +2184,11 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     } else {
         const int s = wv - 4;   // this wave's SIMD
         const bool relay = xr && (s == 0 || a.handover);
-        if (relay) relay_stage<CK, EN>(a, s, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
+        if (relay) relay_stage<CK, EN>(a, s, member, lane, Lk, Lw, Lmodel, Lx0, Lflag, Lq, Lst);
         if (!cil) return;
         // the draws for main wave s's rows (relay stages made theirs before their stage; wave 0's
         // rows of a workgroup with rows left over are left to rank_draw_kernel)
-        if (a.ahead_noise && !relay && !(xr && s == 0)) group_draws(a, s, lane, Lflag);
+        if (a.ahead_noise && !relay && !(member == 0 && s == 0)) group_draws(a, s, lane, Lflag);
         cost_work<CK, EN>(a, s, ng, lane, Lmodel, Lcs, Lflag, Lq);
     }
 }
@@ -2218,6 +2323,30 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
     return b;
 }
 
+// Relay members for a launch of `groups` workgroups with xrows rows left over (a.relay_k): the
+// engine's exchange buffer (a.rx), the hand-over, a member workgroup q + RELAY_STRIDE m in the grid for
+// every relay group q, at least one chunk and four steps per member; else one workgroup.
+constexpr int RELAY_K_DEFAULT = 4;
+static int relay_members(const FrRolloutArgs &a, int64_t groups, int64_t xrows, const EnvSwitches &env)
+{
+    if (!a.handover || a.rx == nullptr || xrows <= 0) return 1;
+    const int64_t nxb = (xrows + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
+    const int nch = (a.H + CH - 1) / CH;
+    int K = std::min(env.relay_k ? env.relay_k : RELAY_K_DEFAULT, RELAY_K_MAX);
+    K = std::min(K, nch);
+    if (nxb > RELAY_GROUPS_MAX) return 1;
+    for (; K > 1; K--) {
+        if (nxb + (int64_t)RELAY_STRIDE * (K - 1) > groups) continue;
+        bool ok = true;
+        for (int m = 0; m < K && ok; m++) {
+            const int k0 = m == 0 ? 0 : (m * nch / K) * CH - 1, k1 = m + 1 == K ? a.H - 1 : ((m + 1) * nch / K) * CH - 1;
+            ok = k1 - k0 >= 4;
+        }
+        if (ok) break;
+    }
+    return K;
+}
+
 // The update's rollouts.  e0 / e1 (may be null): timing events around the rollout launch.
 hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env, hipStream_t s, hipEvent_t e0, hipEvent_t e1, bool *folded,
                                  bool *costs_done, bool *tail_drawn, FrRolloutArgs *final, bool *x_kernel, bool dry,
@@ -2244,6 +2373,8 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
         if (!frow) B.fcost = nullptr;
         B.xbase = gb * WG_ROWS;
         B.xrows = xb + (frow ? 1 : 0);
+        A.relay_k = 1;
+        B.relay_k = relay_members(B, gb, B.xrows, env);
         *folded = frow;
         *costs_done = a.costs_in_launch != 0;
         *tail_drawn = a.ahead_noise != nullptr;
@@ -2268,6 +2399,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
         if (a.drawn_ahead) return hipErrorInvalidValue;   // the one-wave launch samples nothing
         a.fcost = nullptr;   // more than one round of workgroups: one-wave workgroups throughout
         a.ahead_noise = nullptr;
+        a.relay_k = 1;
         a.costs_in_launch = groups > 0 && !env.costs_in_launch_off ? 1 : 0;   // each wave its own rows'
         *costs_done = a.costs_in_launch != 0;
         if (final) *final = a;
@@ -2283,6 +2415,7 @@ hipError_t launch_fr_coop_update(const FrRolloutArgs &a0, const EnvSwitches &env
     *folded = frow;
     a.costs_in_launch = !env.costs_in_launch_off && a.H <= HC_MAX ? 1 : 0;   // Lcs holds HC_MAX steps
     a.handover = env.handover_off ? 0 : 1;
+    a.relay_k = relay_members(a, groups, xrows, env);
     *costs_done = a.costs_in_launch != 0;
     // tail draws ride in launch_costs of fr_coop_x_kernel only, and need the sampling arguments
     if (xrows == 0 || !a.costs_in_launch || !a.drawn_ahead) a.ahead_noise = nullptr;

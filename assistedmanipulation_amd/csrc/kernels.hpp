@@ -166,6 +166,22 @@ struct FrRolloutArgs {
     // MPPI_DEBUG_* fault injection (mppi_debug_inject; 0 in production): bit 0, relay stage 1 of
     // the workgroup with rows left over never signals stage 2 (tests the wait-timeout failure)
     int debug;
+    // The relay over relay_k workgroups (fr_coop.hip relay_stage): member m of relay group q is
+    // workgroup q + RELAY_STRIDE m and runs stages 4 m .. 4 m + 3 over its share of the horizon's
+    // chunks; the lanes' state and the rows' partial cost sums cross between members through rx,
+    // tagged with this launch's rtoken (nonzero, one per launch).  relay_k = 1: one workgroup.
+    struct RelayXfer *rx;
+    uint32_t rtoken;
+    int relay_k;
+};
+constexpr int RELAY_K_MAX = 4, RELAY_STRIDE = 8, RELAY_GROUPS_MAX = 4;
+// One relay group's hand-offs between consecutive members (m -> m + 1, m < RELAY_K_MAX - 1): the
+// 64 lanes' (q, qd, E) and the four rows' partial cost sums, each behind a token on a line of its own
+struct RelayXfer {
+    double state[RELAY_K_MAX - 1][64 * 3];
+    double sums[RELAY_K_MAX - 1][16];
+    uint32_t state_tok[RELAY_K_MAX - 1][32];
+    uint32_t sums_tok[RELAY_K_MAX - 1][32];
 };
 
 // What the objective reads at (step k, rollout): the state x_k the cost is evaluated at and the
@@ -343,6 +359,7 @@ bool fr_coop_costs_in_launch(const EnvSwitches &env);   // the objective runs in
 // the update path (~80 ns each)
 struct EnvSwitches {
     bool draw_ahead_off, tail_draws_off, pm_fused_off, costs_in_launch_off, handover_off, split_off, stream_prio_off;
+    int relay_k;   // MPPI_RELAY_K: workgroups the rows left over travel through (1..RELAY_K_MAX; 0: the default)
     // the handle's device: its CU count (the rollout launches' rounds of workgroups) and LDS per
     // block (the fused point mass's residency check), set at create for that device - per handle, so
     // that handles created on different devices from several threads never read each other's

@@ -426,6 +426,42 @@ def test_handover_equals_doubled_simd(rollouts, objective, monkeypatch):
             np.testing.assert_array_equal(u, v, err_msg="update %d %s" % (j, name))
 
 
+@pytest.mark.parametrize("rollouts,horison,objective,window", [(4096, 0.64, "am", 0), (4096, 0.64, "energy", 0),
+                                                               (4096, 0.64, "track_point", 0), (1000, 0.64, "am", 0),
+                                                               (4097, 0.64, "am", 0), (4096, 0.32, "am", 0),
+                                                               (8192, 1.28, "am", 10), (4096, 0.16, "am", 0)])
+def test_relay_members_equal_one_workgroup(rollouts, horison, objective, window, monkeypatch):
+    """The rows left over relayed through several workgroups (MPPI_RELAY_K, relay_stage: member m of
+    relay group q is workgroup q + 8 m, the lanes' state and the rows' partial cost sums handed on
+    through global memory under the launch's token) against the relay in one workgroup: every
+    output bit for bit, over updates with kept rollouts and shifts (the kept columns each member
+    copies for its own steps), three objectives, three relay groups (1000 rollouts), four rows left
+    over (4097), horizons of 32 and 16 steps (fewer members fit) and configs[4]'s per-GPU share
+    (8192 x 128 with the Savitzky-Golay filter: the relay rides in the split's second launch)."""
+    sg = am.Smoothing(window, 1) if window else None
+    conf = am.frankaridgeback_configuration(rollouts=rollouts, horison=horison, keep_best_rollouts=20, threads=8,
+                                            smoothing=sg)
+    times = [0.0, 0.05, 0.07, 0.12, 0.12, 0.17]
+    make_cost = {"am": am.AssistedManipulation, "energy": energy_only_cost, "track_point": _track_point_all_terms}[objective]
+    out = {}
+    for k in ("1", "2", "4"):
+        monkeypatch.setenv("MPPI_RELAY_K", k)
+        t = am.Trajectory.create(conf, am.FrankaRidgebackDynamics(), make_cost())
+        t.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+        t.set_forecast(am.constant_forecast(t.H))
+        x = am.huddled_state()
+        rec = []
+        for tm in times:
+            t.update(x, tm)
+            assert t.update_info()["wait_timeouts"] == 0
+            rec.append((t.noise().copy(), t.costs().copy(), t.get_optimal_rollout().copy(), t.get_weights().copy()))
+        out[k] = rec + [(np.float64(t.get_optimal_total_cost()),) * 4]   # the folded filter() rows
+    for k in ("2", "4"):
+        for j, (a, b) in enumerate(zip(out["1"], out[k])):
+            for name, u, v in zip(("noise", "costs", "optimal", "weights"), a, b):
+                np.testing.assert_array_equal(u, v, err_msg="K=%s update %d %s" % (k, j, name))
+
+
 def test_two_philox_shards_draw_ahead_equal_unsharded():
     """Device Philox across two shards on one GPU (phase-split ABI, host all-reduces): each shard
     holds 4098 rollouts, so its rollout launch runs one round of workgroups and its draws are made
