@@ -1383,7 +1383,7 @@ static_assert(REC_FP_SINK + 3 <= FR_REC, "frame-position sink");
 template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false, bool KC = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, double *Lst = nullptr, int kb = 0,
-                                         int ke = 0x7FFFFFFF, int *Lprog = nullptr)
+                                         int ke = 0x7FFFFFFF, int *Lprog = nullptr, int *Lgo = nullptr, int go_val = 0)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1473,9 +1473,40 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
     L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
 
-    double q, qd, E;
     if (HO != 3) kb = 0;
     const int kend = HO == 3 ? min(ke, H - 1) : H - 1;   // steps [kb, kend) in this call
+    // eps and U*_shifted of step k: loaded at the top of the step
+    const bool sampled = !opt_row && jl;
+    double sd = sampled ? 1.0 : 0.0, jd = jl ? 1.0 : 0.0;
+    asm volatile("" : "+v"(sd), "+v"(jd));   // opaque: kept as data, not folded into control flow
+    int64_t nstride = sampled ? a.Rpad * FR_C : 0;   // unsampled rows re-read their first element
+    asm volatile("" : "+v"(nstride));
+    const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
+    // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
+    // whose latency a single wave per SIMD cannot hide within one step
+    // (issued before the first record store: the loop header then waits for the loads alone,
+    // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
+    double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
+    // a relay stage past the first: its setup above and its first loads are in flight while it waits
+    // for the previous stage's state (Lgo: the stage counter it raises once Lst is written)
+    if constexpr (HO == 3) {
+        if (kb > 0 && Lgo != nullptr) {
+            int st = 0;
+            for (int i = 0; i < (1 << 22) && st < go_val; i++) {
+                st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lgo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (st < go_val) __builtin_amdgcn_s_sleep(1);
+            }
+            asm volatile("" ::: "memory");   // the reads of Lst below stay behind the poll (LDS is in order)
+            if (st < go_val) {
+                if (lane == 0) {
+                    if (a.status) atomicAdd(&const_cast<Status *>(a.status)->wait_timeouts, 1);
+                    if (a.wait_sum) atomicAdd(a.wait_sum, 1.0);
+                }
+                return -2;   // (the stage never ran)
+            }
+        }
+    }
+    double q, qd, E;
     if (kb > 0) {   // the state the previous relay stage left at the top of step kb
         q = Lst[3 * lane];
         qd = Lst[3 * lane + 1];
@@ -1513,18 +1544,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         else store_kin<CK>(recp(0), j, bd, qd);
     }
 
-    // eps and U*_shifted of step k: loaded at the top of the step
-    const bool sampled = !opt_row && jl;
-    double sd = sampled ? 1.0 : 0.0, jd = jl ? 1.0 : 0.0;
-    asm volatile("" : "+v"(sd), "+v"(jd));   // opaque: kept as data, not folded into control flow
-    int64_t nstride = sampled ? a.Rpad * FR_C : 0;   // unsampled rows re-read their first element
-    asm volatile("" : "+v"(nstride));
-    const double *np = sampled ? a.noise + lr * FR_C + jb : Up;   // any valid address when unused
-    // eps and U*_shifted one step ahead: the noise tensor streams from HBM / the Infinity Cache,
-    // whose latency a single wave per SIMD cannot hide within one step
-    // (issued before the first record store: the loop header then waits for the loads alone,
-    // vmcnt(2), on the entry edge as on the back edge, not for the stores behind them)
-    double eps_n = np[(int64_t)kb * nstride], ub_n = Up[min(kb + ush, H - 1) * FR_C + jb];
     if (kb == 0) store_record<EN>(recp(0), j, L, q, qd, kin, E);
     // a relay stage enters its loop with nothing in flight (its first step needs step kb's loads
     // anyway): where the entry edge held an unknown count, the loop header waited for every store
@@ -1609,6 +1628,12 @@ __device__ __forceinline__ void signal_records(int *flag)
 {
     __builtin_amdgcn_s_waitcnt(0);
     __hip_atomic_store(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the same, one count of several (the relay's stages: Lflag[LF_RELAY] counts those done)
+__device__ __forceinline__ void signal_records_add(int *flag)
+{
+    __builtin_amdgcn_s_waitcnt(0);
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // Bounded: a wave that never signals (a bug) costs about a second, not a hung GPU.  The timeout is
 // counted in Status::wait_timeouts (and, sharded over RCCL, in the rank's cost slot R that the
@@ -1761,7 +1786,7 @@ __device__ __forceinline__ void group_chunks(const FrRolloutArgs &a, int g, int 
 // whether chunk c of group g can be read: its records are complete
 __device__ __forceinline__ bool chunk_ready(const FrRolloutArgs &a, int g, int c, int *Lflag, int *Lq)
 {
-    if (g == 4) return lds_read(Lflag + LF_RELAY) != 0;
+    if (g == 4) return lds_read(Lflag + LF_RELAY) >= (a.handover ? 4 : 1);   // every stage here has stored its records
     const int last = min((c + 1) * CH, a.H) - 1;
     if (last < a.H - 1 && lds_read(Lq + Q_PROG + g) >= last + 3) return true;
     return lds_read(Lflag + g) != 0;
@@ -1942,17 +1967,7 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
         // the next update's draws for main wave s's rows first (member 0's wave 0 rows are left
         // to rank_draw_kernel)
         if ((s > 0 || m > 0) && a.ahead_noise) group_draws(a, s, lane, Lflag);
-        if (s > 0) {   // bounded: 2^22 short sleeps, about 0.2 s
-            int st = 0;
-            for (int i = 0; i < (1 << 22) && st < s; i++) {
-                st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lq + Q_STAGE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (st < s) __builtin_amdgcn_s_sleep(2);
-            }
-            if (st < s) {
-                if (lane == 0) note_wait_timeout(a);
-                return false;
-            }
-        } else if (m > 0) {   // the previous member's lanes' state (sc1 loads after the token), into Lst
+        if (s == 0 && m > 0) {   // the previous member's lanes' state (sc1 loads after the token), into Lst
             RelayXfer *x = a.rx + q;
             if (!wait_token(a, &x->state_tok[m - 1][0])) return false;
 #pragma unroll
@@ -1963,18 +1978,24 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
         kb = relay_step(a, r, H);
         ke = relay_step(a, r + 1, H);
     }
-    // one call site: one copy of the step loop for both shapes
-    coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke);
+    // one call site: one copy of the step loop for both shapes.  A stage past a member's first makes
+    // its setup and first loads, then waits inside for the previous stage's state (Lq[Q_STAGE] == s;
+    // bounded, about 0.2 s: -2 if it gave up)
+    if (coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke, nullptr,
+                                   (a.handover && s > 0) ? Lq + Q_STAGE : nullptr, s) == -2)
+        return false;
     if (a.handover) {
         __builtin_amdgcn_s_setprio(0);
 #ifdef COOP_TRACE   // the stages' ends of relay group 0, member m in the slot 1 + m past the relay rows'
         if (a.trace && q == 0 && lane == 0) a.trace[4 * (gridDim.x * 4 + 1 + m) + s] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (s < 3) {   // the state in Lst (and this stage's records) before the next stage starts
-            __builtin_amdgcn_s_waitcnt(0);
+        if (s < 3) {   // the state in Lst (LDS) is all the next stage waits for: signal it at once
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             // fault injection (tests only): stage 1 never signals, so stages 2 and 3 time out
             if (!((a.debug & 1) && r == 1))
-                __hip_atomic_store(Lq + Q_STAGE, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(Lq + Q_STAGE, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // then this stage's record stores, counted for the relay's cost chunks
+            if (a.costs_in_launch) signal_records_add(Lflag + LF_RELAY);
             return true;
         }
         if (m + 1 < a.relay_k) {   // the last stage of a member: the state to the next member (sc1), then the token
@@ -1987,7 +2008,7 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
         }
     }
     if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(a, 1, H) : -1;
-    if (a.costs_in_launch) signal_records(Lflag + LF_RELAY);   // this workgroup's relay records are stored
+    if (a.costs_in_launch) signal_records_add(Lflag + LF_RELAY);   // this workgroup's relay records are stored
     return true;
 }
 
