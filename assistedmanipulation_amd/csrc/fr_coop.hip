@@ -1378,12 +1378,16 @@ static_assert(REC_FP_SINK + 3 <= FR_REC, "frame-position sink");
 // the horizon at priority 3 and hands the state to the next stage through LDS, so each of the four
 // main waves loses about a quarter of what wave 0 alone lost before.
 // PROG: the wave stores its step into *Lprog at the top of each step (the objective chunks, cost_work).
+// bound of a relay stage's wait for its state (short sleeps: about 0.2 s)
+constexpr int WAIT_SPINS_ROWS = 1 << 22;
+
 // KC: compact records (FR_REC_C, store_ks: the kinematic sums on the row's chain), else the 768-B
 // ones (store_kin).
 template <int CK, bool EN, bool FROW, int HO = 0, bool PROG = false, bool KC = false>
 __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int lane, int wblk, double *Lk, double *Lw,
                                          const double *Lmodel, const double *Lx0, double *Lst = nullptr, int kb = 0,
-                                         int ke = 0x7FFFFFFF, int *Lprog = nullptr, int *Lgo = nullptr, int go_val = 0)
+                                         int ke = 0x7FFFFFFF, int *Lprog = nullptr, int *Lgo = nullptr, int go_val = 0,
+                                         RelayXfer *gx = nullptr, int gm = 0)
 {
     const int j = lane & (ROW - 1);
 #ifdef COOP_TRACE
@@ -1492,7 +1496,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     if constexpr (HO == 3) {
         if (kb > 0 && Lgo != nullptr) {
             int st = 0;
-            for (int i = 0; i < (1 << 22) && st < go_val; i++) {
+            for (int i = 0; i < WAIT_SPINS_ROWS && st < go_val; i++) {
                 st = __builtin_amdgcn_readfirstlane(__hip_atomic_load(Lgo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                 if (st < go_val) __builtin_amdgcn_s_sleep(1);
             }
@@ -1507,7 +1511,24 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         }
     }
     double q, qd, E;
-    if (kb > 0) {   // the state the previous relay stage left at the top of step kb
+    if (HO == 3 && gx != nullptr) {   // a later relay member's first stage: the previous member's state
+        bool ok = false;                // (the launch's token, then sc1 loads; bounded, -2 if it gave up)
+        for (int i = 0; i < WAIT_SPINS_ROWS && !ok; i++) {
+            ok = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&gx->state_tok[gm - 1][0], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)) == a.rtoken;
+            if (!ok) __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) {
+            if (lane == 0) {
+                if (a.status) atomicAdd(&const_cast<Status *>(a.status)->wait_timeouts, 1);
+                if (a.wait_sum) atomicAdd(a.wait_sum, 1.0);
+            }
+            return -2;
+        }
+        q = __hip_atomic_load(&gx->state[gm - 1][3 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qd = __hip_atomic_load(&gx->state[gm - 1][3 * lane + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        E = __hip_atomic_load(&gx->state[gm - 1][3 * lane + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (kb > 0) {   // the state the previous relay stage left at the top of step kb
         q = Lst[3 * lane];
         qd = Lst[3 * lane + 1];
         E = Lst[3 * lane + 2];
@@ -1964,16 +1985,11 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
     const int r = 4 * m + s;
     int kb = 0, ke = 0x7FFFFFFF;   // without a.handover: every step on this wave (one stage)
     if (a.handover) {
-        // the next update's draws for main wave s's rows first (member 0's wave 0 rows are left
-        // to rank_draw_kernel)
-        if ((s > 0 || m > 0) && a.ahead_noise) group_draws(a, s, lane, Lflag);
-        if (s == 0 && m > 0) {   // the previous member's lanes' state (sc1 loads after the token), into Lst
-            RelayXfer *x = a.rx + q;
-            if (!wait_token(a, &x->state_tok[m - 1][0])) return false;
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                Lst[3 * lane + c] = __hip_atomic_load(&x->state[m - 1][3 * lane + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        // the next update's draws for main wave s's rows (member 0's wave 0 rows are left to
+        // rank_draw_kernel): first where the stage waits long for its turn (later members), after
+        // the stage in member 0, whose stages follow each other within microseconds when the relay
+        // spans several workgroups
+        if (m > 0 && a.ahead_noise) group_draws(a, s, lane, Lflag);
         __builtin_amdgcn_s_setprio(3);   // above the main waves (1) and the objective's (0)
         kb = relay_step(a, r, H);
         ke = relay_step(a, r + 1, H);
@@ -1982,7 +1998,8 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
     // its setup and first loads, then waits inside for the previous stage's state (Lq[Q_STAGE] == s;
     // bounded, about 0.2 s: -2 if it gave up)
     if (coop_rows<CK, EN, true, 3>(a, xlr, lane, wblk, Lk, Lw, Lmodel, Lx0, Lst, kb, ke, nullptr,
-                                   (a.handover && s > 0) ? Lq + Q_STAGE : nullptr, s) == -2)
+                                   (a.handover && s > 0) ? Lq + Q_STAGE : nullptr, s,
+                                   (a.handover && s == 0 && m > 0) ? a.rx + q : nullptr, m) == -2)
         return false;
     if (a.handover) {
         __builtin_amdgcn_s_setprio(0);
@@ -1996,6 +2013,7 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
                 __hip_atomic_store(Lq + Q_STAGE, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             // then this stage's record stores, counted for the relay's cost chunks
             if (a.costs_in_launch) signal_records_add(Lflag + LF_RELAY);
+            if (m == 0 && s > 0 && a.ahead_noise) group_draws(a, s, lane, Lflag);   // (member 0: after the stage)
             return true;
         }
         if (m + 1 < a.relay_k) {   // the last stage of a member: the state to the next member (sc1), then the token
@@ -2009,6 +2027,7 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
     }
     if (blockIdx.x == 0 && lane == 0) const_cast<Status *>(a.status)->handover = a.handover ? relay_step(a, 1, H) : -1;
     if (a.costs_in_launch) signal_records_add(Lflag + LF_RELAY);   // this workgroup's relay records are stored
+    if (a.handover && m == 0 && s > 0 && a.ahead_noise) group_draws(a, s, lane, Lflag);   // (member 0: after the stage)
     return true;
 }
 

@@ -35,6 +35,9 @@ for u in (len(recs) // 2, len(recs) - 1):
     fx = rec[nmain]
     print("  relay rows: start %.1f end %.1f, stages end" % (us(fx[0]), us(fx[1])),
           ["%.1f" % us(x) for x in rec[nmain + 1]])
+    for m in range(1, 4):   # members 1..3 of a relay over several workgroups (MPPI_RELAY_K)
+        if rec[nmain + 1 + m].any():
+            print("  relay member %d stages end" % m, ["%.1f" % us(x) if x else "-" for x in rec[nmain + 1 + m]])
     for g in range(5):
         row = []
         for c in range(4):
