@@ -2365,8 +2365,11 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
 
 // Relay members for a launch of `groups` workgroups with xrows rows left over (a.relay_k): the
 // engine's exchange buffer (a.rx), the hand-over, a member workgroup q + RELAY_STRIDE m in the grid for
-// every relay group q, at least one chunk and four steps per member; else one workgroup.
-constexpr int RELAY_K_DEFAULT = 4;
+// every relay group q, at least one chunk and four steps per member; else one workgroup.  Two by
+// default: at 4096 x 64 (profiles/r06/relay_k) K = 2 ran 0.1838-0.1848 ms/update against 0.1881-0.1892
+// for K = 1, 0.1858-0.1880 for K = 3 and 0.1871-0.1879 for K = 4 (each member's first stage pays
+// ~10 us of hand-over and its own setup, so more members stop paying off past two).
+constexpr int RELAY_K_DEFAULT = 2;
 static int relay_members(const FrRolloutArgs &a, int64_t groups, int64_t xrows, const EnvSwitches &env)
 {
     if (!a.handover || a.rx == nullptr || xrows <= 0) return 1;
