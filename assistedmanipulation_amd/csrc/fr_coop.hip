@@ -540,6 +540,217 @@ __device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
         : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(qa), "=&v"(qb), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
         : "v"(nt), "v"(inv_next));
 }
+// Gauss-Jordan with one row per lane (tools/gen_gj.py solve_rows): Mc[0..11] row j of M, b
+// tau_j; returns with b the solution on lanes 2..11 (rows normalised), b * m on lanes 0 and 1
+// (scaled by 1 / m after).  f0 / f1: pivot 0 / 1's factors (-M_j0 / m0, -M_j1 / m1; 0 on lane
+// 0 / 1).  Exec is saved, narrowed for the factors of each pivot and restored inside.
+__device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double f1)
+{
+    double fa, fb, d, r0, e, q;
+    uint64_t sx, mk;
+    const uint64_t base = 0x0001000100010001ull;   // lane 0 of each 16-lane row
+    // s_nop 1: Mc / f0 / f1 (DPP operands) may be written right before the block
+    asm("s_nop 1\n\t"
+        "s_mov_b64 %19, exec\n\t"
+        /* pivot 0 */
+        "v_fmac_f64_dpp %2, %2, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 1 */
+        "v_fmac_f64_dpp %2, %2, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %3, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %5, %5, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %6, %6, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %7, %7, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %8, %8, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_lshl_b64 %20, %23, 2\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %13, -%2, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %13, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        "v_fmac_f64_dpp %11, %11, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 2 */
+        "v_fmac_f64_dpp %3, %3, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %4, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %3 row_newbcast:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_lshl_b64 %20, %23, 3\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %14, -%3, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %14, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 3 */
+        "v_fmac_f64_dpp %4, %4, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %5, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %4 row_newbcast:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %7, %7, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %8, %8, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %9, %9, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "v_fmac_f64_dpp %10, %10, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "s_lshl_b64 %20, %23, 4\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %13, -%4, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %13, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        "v_fmac_f64_dpp %11, %11, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 4 */
+        "v_fmac_f64_dpp %5, %5, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %6, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %5 row_newbcast:5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 5\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %14, -%5, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %14, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 5 */
+        "v_fmac_f64_dpp %6, %6, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %7, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %6 row_newbcast:6 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %9, %9, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %10, %10, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %11, %11, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 6\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %13, -%6, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %13, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        "v_fmac_f64_dpp %12, %12, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        /* pivot 6 */
+        "v_fmac_f64_dpp %7, %7, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %8, %8, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %7 row_newbcast:7 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fmac_f64_dpp %12, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 7\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %14, -%7, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %14, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        /* pivot 7 */
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %8, %8, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %9, %9, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %8 row_newbcast:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %11, %11, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fmac_f64_dpp %12, %12, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 8\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %13, -%8, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %13, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        /* pivot 8 */
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %9, %9, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %10, %10, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %12, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 9\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %14, -%9, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %14, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        /* pivot 9 */
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %10, %10, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %11, %11, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b64_dpp %15, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 10\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %13, -%10, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %13, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        /* pivot 10 */
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %11, %11, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %12, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_mov_b64_dpp %15, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_rcp_f64 %16, %15\n\t"
+        "v_fma_f64 %17, -%15, %16, 1.0\n\t"
+        "v_fma_f64 %18, %16, %17, %16\n\t"
+        "s_lshl_b64 %20, %23, 11\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t"
+        "v_mul_f64 %14, -%11, %18\n\t"
+        "s_and_b64 exec, %19, %20\n\t"
+        "v_add_f64 %14, %18, -1.0\n\t"
+        "s_mov_b64 exec, %19\n\t"
+        /* pivot 11 */
+        "s_nop 0\n\t"
+        "v_fmac_f64_dpp %12, %12, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
+        : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "+v"(b), "=&v"(fa), "=&v"(fb), "=&v"(d), "=&v"(r0), "=&v"(e), "=&v"(q), "=&s"(sx), "=&s"(mk)
+        : "v"(f0), "v"(f1), "s"(base)
+        : "scc");
+}
 // ---- END generated by tools/gen_gj.py ----
 
 // A rotation's third column from its first two, r2 = r0 x r1 (R row-major).
@@ -748,6 +959,8 @@ struct LaneConst {
     double cmask[9];   // composite_scan: 1.0 when body j is the parent of step s's child (edges 11-9, 10-9, 9-8, .., 3-2)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
+    double f0, f1;  // gj_rows: pivot 0 / 1's factor per unit of M_j0 / M_j1 (-1 / m; 0 on lane 0 / 1)
+    double qs;      // gj_rows: the solution's scale (1 / m on lanes 0 and 1, else 1)
 };
 
 // calculate(): FK by prefix scan, world inertias and S to LDS, the next cost's kinematic terms.
@@ -1180,12 +1393,21 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     double *Row = Lk + L_COL + j * CSTR;
 #pragma unroll
     for (int i = 0; i < 12; i += 2) *reinterpret_cast<double2 *>(Row + i) = double2{Mc[i], Mc[i + 1]};
+#ifdef GJ_COLS
     Row[12] = tau_l;   // (slots 13..15: zeros for good, coop_rows' entry)
+#endif
     Row[j] = diag;
 #pragma unroll
     for (int i = 0; i < 12; i++) Mc[i] += Lk[L_COL + i * CSTR + j];
 #pragma unroll
     for (int i = 0; i < 12; i++) PMARK_D(6, Mc[i]);
+#ifndef GJ_COLS
+    // one row per lane (M symmetric: the column is the row), tau_j the lane's own right-hand side;
+    // lanes 12..15 read zeros (slots 12..15 of every block row) and have tau 0, so their b stays 0
+    double b = tau_l;
+    gj_rows(Mc, b, Mc[0] * L.f0, Mc[1] * L.f1);
+    return b * L.qs;   // rows 2..11 normalised; rows 0 and 1 times 1 / m
+#else
     double nt = -Mc[0] * L.inv_m0;   // each pivot's block returns the next pivot's quotient
     gj_solve(Mc, nt, L.inv_m1);
     // The matrix is now diagonal (every row scaled alike): qdd_j = tau'_j / M'_jj.  Lane 12 leaves
@@ -1198,6 +1420,7 @@ __device__ __forceinline__ double coop_solve(int j, const LaneConst &L, const Co
     const double tp = Lk[j < FR_NB ? L_TP + j : L_TP + 12];
     const double dj = Lk[j < FR_NB ? L_COL + j * CSTR + j : L_TP + 13];
     return tp * frcp(dj);
+#endif
 }
 
 }  // namespace
@@ -1476,6 +1699,14 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     L.mc = M[T_MC];
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
     L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
+    {
+        double f0 = j == 0 ? 0.0 : -L.inv_m0, f1 = j == 1 ? 0.0 : -L.inv_m1;
+        double qs = j == 0 ? L.inv_m0 : (j == 1 ? L.inv_m1 : 1.0);
+        asm volatile("" : "+v"(f0), "+v"(f1), "+v"(qs));   // kept in registers across the loop
+        L.f0 = f0;
+        L.f1 = f1;
+        L.qs = qs;
+    }
 
     if (HO != 3) kb = 0;
     const int kend = HO == 3 ? min(ke, H - 1) : H - 1;   // steps [kb, kend) in this call
@@ -1555,7 +1786,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     CoopBody bd;
     // coop_solve's block rows: slots 13..15 hold zeros for good (slot 12 is tau, rewritten per step)
     if constexpr (!EN) {
-        Lk[L_COL + j * CSTR + 13] = 0.0;
+        *reinterpret_cast<double2 *>(Lk + L_COL + j * CSTR + 12) = double2{0.0, 0.0};   // (12: tau with GJ_COLS)
         *reinterpret_cast<double2 *>(Lk + L_COL + j * CSTR + 14) = double2{0.0, 0.0};
         *reinterpret_cast<double2 *>(Lk + L_TP + 12) = double2{0.0, 1.0};   // coop_solve's dummy-lane reads
     }
