@@ -540,6 +540,13 @@ __device__ __forceinline__ void gj_solve(double *Mc, double nt, double inv_next)
         : "+v"(Mc[0]), "+v"(Mc[1]), "+v"(Mc[2]), "+v"(Mc[3]), "+v"(Mc[4]), "+v"(Mc[5]), "+v"(Mc[6]), "+v"(Mc[7]), "+v"(Mc[8]), "+v"(Mc[9]), "+v"(Mc[10]), "+v"(Mc[11]), "=&v"(qa), "=&v"(qb), "=&v"(d), "=&v"(r), "=&v"(t), "=&v"(e)
         : "v"(nt), "v"(inv_next));
 }
+#ifdef GJ_EXEC_NOP   // (A/B: wait states after each exec write, -DGJ_EXEC_NOP=n: s_nop n)
+#define GJ_STR2(x) #x
+#define GJ_STR(x) GJ_STR2(x)
+#define GJ_EXEC_PAD "s_nop " GJ_STR(GJ_EXEC_NOP) "\n\t"
+#else
+#define GJ_EXEC_PAD ""
+#endif
 // Gauss-Jordan with one row per lane (tools/gen_gj.py solve_rows): Mc[0..11] row j of M, b
 // tau_j; returns with b the solution on lanes 2..11 (rows normalised), b * m on lanes 0 and 1
 // (scaled by 1 / m after).  f0 / f1: pivot 0 / 1's factors (-M_j0 / m0, -M_j1 / m1; 0 on lane
@@ -579,11 +586,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %9, %9, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "s_lshl_b64 %20, %23, 2\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%2, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         "v_fmac_f64_dpp %11, %11, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 2 */
@@ -600,11 +607,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %9, %9, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "s_lshl_b64 %20, %23, 3\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%3, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 3 */
@@ -620,11 +627,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "v_fmac_f64_dpp %10, %10, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "s_lshl_b64 %20, %23, 4\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%4, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         "v_fmac_f64_dpp %11, %11, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 4 */
@@ -639,11 +646,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %10, %10, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 5\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%5, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 5 */
@@ -658,11 +665,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %11, %11, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 6\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%6, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 6 */
         "v_fmac_f64_dpp %7, %7, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
@@ -676,11 +683,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 7\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%7, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         /* pivot 7 */
         "s_nop 0\n\t"
         "v_fmac_f64_dpp %8, %8, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
@@ -693,11 +700,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 8\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%8, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         /* pivot 8 */
         "s_nop 0\n\t"
         "v_fmac_f64_dpp %9, %9, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
@@ -706,14 +713,15 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_mov_b64_dpp %15, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_rcp_f64 %16, %15\n\t"
+        "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 9\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%9, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         /* pivot 9 */
         "s_nop 0\n\t"
         "v_fmac_f64_dpp %10, %10, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
@@ -721,14 +729,15 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_mov_b64_dpp %15, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
         "v_rcp_f64 %16, %15\n\t"
+        "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 10\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%10, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         /* pivot 10 */
         "s_nop 0\n\t"
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
@@ -736,14 +745,15 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "s_nop 0\n\t"
         "v_mov_b64_dpp %15, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
         "v_rcp_f64 %16, %15\n\t"
+        "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "s_lshl_b64 %20, %23, 11\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t"
+        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%11, %18\n\t"
-        "s_and_b64 exec, %19, %20\n\t"
+        "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
-        "s_mov_b64 exec, %19\n\t"
+        "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
         /* pivot 11 */
         "s_nop 0\n\t"
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"

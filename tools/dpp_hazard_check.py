@@ -22,13 +22,13 @@ def regs(tok):
 def check(path, prefix="", strict=True):
     bad = 0
     inside = False
-    recent = []   # (wait states since the write, registers)
+    recent, trans = [], []   # (wait states since the write, registers)
     for l in open(path):
         l = l.rstrip("\n")
         if not inside:
             m = re.match(r"^(_Z\w+):", l)
             if m and m.group(1).startswith(prefix or "_Z"):
-                inside, recent = True, []
+                inside, recent, trans = True, [], []
             continue
         if l.startswith(".Lfunc_end"):
             inside = False
@@ -36,7 +36,7 @@ def check(path, prefix="", strict=True):
         s = l.strip()
         if not s or s.startswith((".", ";")) or s.endswith(":"):
             if s.endswith(":"):
-                recent = []   # a branch target: the distance is only tracked in straight-line code
+                recent, trans = [], []   # a branch target: the distance is only tracked in straight-line code
             continue
         op = s.split()[0]
         ws = int(s.split()[1], 0) + 1 if op == "s_nop" else 1
@@ -53,11 +53,23 @@ def check(path, prefix="", strict=True):
                 elif dist < 2 and (w & srcs) and strict:
                     print("hazard on a non-DPP source (%d wait states): %s" % (dist, s))
                     bad += 1
+        # gfx940+ trans forwarding: a VALU reading a transcendental's result (v_rcp / v_rsq / v_sqrt /
+        # v_exp / v_log / v_sin / v_cos) in the very next instruction reads a stale value
+        if op.startswith("v_") and "_dpp" not in op:
+            srcs = set().union(*[regs(o.split()[0]) for o in s[len(op):].split(",")[1:] if o.strip()]) \
+                if "," in s else set()
+            for dist, w in trans:
+                if dist < 1 and (w & srcs):
+                    print("trans forwarding hazard: %s" % s)
+                    bad += 1
         recent = [(d + ws, w) for d, w in recent if d + ws < 2]
+        trans = [(d + ws, w) for d, w in trans if d + ws < 1]
         if op.startswith("v_") and op != "v_nop":
             dst = regs(s[len(op):].split(",")[0])
             if dst:
                 recent.append((0, dst))
+                if re.match(r"v_(rcp|rsq|sqrt|exp|log|sin|cos)_", op):
+                    trans.append((0, dst))
     return bad
 
 
