@@ -2003,7 +2003,7 @@ enum { Q_PROG = 0, Q_NEXT = 4, Q_DONE = 9, Q_STAGE = 14, Q_N = 16 };
 // LDS flags (Lflag): main wave g's records are stored (g), the relay's rows are done (LF_RELAY),
 // main wave g's kept columns are copied (LF_KEPT + g: its rows' previous eps is read, so their next
 // draws may overwrite it)
-constexpr int LF_RELAY = 4, LF_KEPT = 5, LF_N = 9;
+constexpr int LF_RELAY = 4, LF_KEPT = 5, LF_KEPT_X = 9, LF_N = 10;   // LF_KEPT_X: the relay rows' kept columns are copied
 
 __device__ __forceinline__ int lds_read(int *w)
 {
@@ -2235,6 +2235,9 @@ __device__ __forceinline__ bool relay_stage(const FrRolloutArgs &a, int s, int m
         kb = relay_step(a, r, H);
         ke = relay_step(a, r + 1, H);
     }
+    // a stage past the first issues its first eps loads before it waits for the previous stage: the
+    // relay rows' kept columns (wave 4's copy at entry, this member's steps) must have landed
+    if (s > 0 && a.drawn_ahead) wait_records(a, Lflag + LF_KEPT_X);
     // one call site: one copy of the step loop for both shapes.  A stage past a member's first makes
     // its setup and first loads, then waits inside for the previous stage's state (Lq[Q_STAGE] == s;
     // bounded, about 0.2 s: -2 if it gave up)
@@ -2440,9 +2443,11 @@ __global__ __launch_bounds__(64 * XW) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (a.drawn_ahead) {
         if (blockIdx.x == 0 && wv == 1) block0_sample_writes<64>(a, lane);   // off the SIMD of the relay's first stage
         if (wv < 4) kept_rows_wave(a, lr, lane, rk);
-        else if (wv == 4 && xr)   // the relay rows' columns of the steps this member runs
+        else if (wv == 4 && xr) {   // the relay rows' columns of the steps this member runs
             kept_rows_wave(a, lr, lane, rk, relay_member_step(a, member, a.H),
                            member + 1 < a.relay_k ? relay_member_step(a, member + 1, a.H) : 0x7FFFFFFF);
+            __hip_atomic_store(Lflag + LF_KEPT_X, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     const bool cil = a.costs_in_launch != 0;
     if (wv < 4) {

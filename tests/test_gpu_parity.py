@@ -462,6 +462,35 @@ def test_relay_members_equal_one_workgroup(rollouts, horison, objective, window,
                 np.testing.assert_array_equal(u, v, err_msg="K=%s update %d %s" % (k, j, name))
 
 
+@pytest.mark.parametrize("k", ["1", "2"])
+def test_relay_kept_rows_against_oracle(k, monkeypatch):
+    """The relay rows' kept columns (keep-best rollouts among the rows left over, shifted in by the
+    relay's wave 4 at entry) against the oracle with the device's draws replayed, over a state change
+    and shifts of 5, 2, 5, 0 and 5 steps, relay in one workgroup and over two.  A stage past the
+    first issues its first eps loads before it waits for the previous stage; before it also waited
+    for the kept copy (LF_KEPT_X), the one-workgroup relay read a kept rollout's unshifted eps at a
+    stage's first step (rollout 1000 at update 6: 7.2e-8 of Delta, r06)."""
+    monkeypatch.setenv("MPPI_RELAY_K", k)
+    conf = am.frankaridgeback_configuration(rollouts=1000, horison=0.64, keep_best_rollouts=20, threads=8)
+    dyn, cost = am.FrankaRidgebackDynamics(), am.AssistedManipulation()
+    dev = am.Trajectory.create(conf, dyn, cost)
+    dev.set_noise_source(abi.MPPI_NOISE_DEVICE_PHILOX, seed=0x5EED)
+    table = am.constant_forecast(dev.H)
+    dev.set_forecast(table)
+    cc, keep = conf.to_c()
+    orc = O.OracleTrajectory(cc, dyn.descriptor(), cost.descriptor(), scalar=0, mode=0)
+    orc.set_forecast(table)
+    x = am.huddled_state()
+    prev_costs, prev_noise = np.zeros(dev.R), np.zeros((dev.R, dev.H, dev.C))
+    for j, t in enumerate([0.0, 0.05, 0.07, 0.12, 0.12, 0.17, 0.22, 0.27]):
+        if j == 5:
+            x = x.copy()
+            x[12 + 4] = 0.3
+        prev_costs, prev_noise = replay_device_draws(dev, orc, x, t, prev_costs, prev_noise, 20)
+        assert dev.update_info()["wait_timeouts"] == 0
+        assert_update_parity(dev, orc, "relay K=%s upd %d" % (k, j))
+
+
 def test_two_philox_shards_draw_ahead_equal_unsharded():
     """Device Philox across two shards on one GPU (phase-split ABI, host all-reduces): each shard
     holds 4098 rollouts, so its rollout launch runs one round of workgroups and its draws are made
