@@ -559,6 +559,7 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
     // s_nop 1: Mc / f0 / f1 (DPP operands) may be written right before the block
     asm("s_nop 1\n\t"
         "s_mov_b64 %19, exec\n\t"
+        "s_lshl_b64 %20, %23, 2\n\t"
         /* pivot 0 */
         "v_fmac_f64_dpp %2, %2, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, %3, %21 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
@@ -585,12 +586,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %8, %8, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %9, %9, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_lshl_b64 %20, %23, 2\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%2, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 3\n\t"
         "v_fmac_f64_dpp %11, %11, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %22 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 2 */
@@ -606,12 +606,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "v_fmac_f64_dpp %9, %9, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-        "s_lshl_b64 %20, %23, 3\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%3, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 4\n\t"
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 3 */
@@ -626,12 +625,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %9, %9, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
         "v_fmac_f64_dpp %10, %10, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-        "s_lshl_b64 %20, %23, 4\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%4, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 5\n\t"
         "v_fmac_f64_dpp %11, %11, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 4 */
@@ -645,12 +643,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fmac_f64_dpp %10, %10, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 5\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%5, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 6\n\t"
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 5 */
@@ -664,12 +661,11 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fmac_f64_dpp %11, %11, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 6\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%6, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 7\n\t"
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
         /* pivot 6 */
         "v_fmac_f64_dpp %7, %7, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
@@ -682,14 +678,12 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 7\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%7, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 8\n\t"
         /* pivot 7 */
-        "s_nop 0\n\t"
         "v_fmac_f64_dpp %8, %8, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %9, %9, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
@@ -699,14 +693,12 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 8\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%8, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 9\n\t"
         /* pivot 8 */
-        "s_nop 0\n\t"
         "v_fmac_f64_dpp %9, %9, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %10, %10, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n\t"
@@ -716,14 +708,12 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 9\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%9, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 10\n\t"
         /* pivot 9 */
-        "s_nop 0\n\t"
         "v_fmac_f64_dpp %10, %10, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %11, %11, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n\t"
@@ -732,14 +722,12 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 10\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %13, -%10, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %13, %18, -1.0\n\t"
         "s_mov_b64 exec, %19\n\t" GJ_EXEC_PAD
+        "s_lshl_b64 %20, %23, 11\n\t"
         /* pivot 10 */
-        "s_nop 0\n\t"
         "v_fmac_f64_dpp %11, %11, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %12, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n\t"
         "s_nop 0\n\t"
@@ -748,8 +736,6 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
         "s_nop 0\n\t"
         "v_fma_f64 %17, -%15, %16, 1.0\n\t"
         "v_fma_f64 %18, %16, %17, %16\n\t"
-        "s_lshl_b64 %20, %23, 11\n\t"
-        "s_andn2_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_mul_f64 %14, -%11, %18\n\t"
         "s_and_b64 exec, %19, %20\n\t" GJ_EXEC_PAD
         "v_add_f64 %14, %18, -1.0\n\t"
