@@ -2600,7 +2600,8 @@ static FrRolloutArgs row_slice(const FrRolloutArgs &a, int64_t r0, int64_t n)
 // every relay group q, at least one chunk and four steps per member; else one workgroup.  Two by
 // default: at 4096 x 64 (profiles/r06/relay_k) K = 2 ran 0.1838-0.1848 ms/update against 0.1881-0.1892
 // for K = 1, 0.1858-0.1880 for K = 3 and 0.1871-0.1879 for K = 4 (each member's first stage pays
-// ~10 us of hand-over and its own setup, so more members stop paying off past two).
+// ~10 us of hand-over and its own setup, so more members stop paying off past two); with gj_rows
+// K = 2 0.1757-0.1772, K = 1 0.1789-0.1823, K = 3 0.1776-0.1791 (ab_gjrows.txt).
 constexpr int RELAY_K_DEFAULT = 2;
 static int relay_members(const FrRolloutArgs &a, int64_t groups, int64_t xrows, const EnvSwitches &env)
 {
