@@ -2056,7 +2056,12 @@ __device__ __forceinline__ void cost_chunk(const FrRolloutArgs &a, int g, int c,
     const double *rec = frow ? a.frec : a.rec + lrv * H * FR_REC;
     const StepConst *stp = frow ? a.fsteps : a.steps;
     const int kk = live ? k : 0;
-    const double cs = mppi_cost::record_step_cost<CK, EN, MB>(*a.cost, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO);
+    PMARK(8);
+#ifndef COST_JG
+#define COST_JG 2
+#endif
+    double cs = mppi_cost::record_step_cost<CK, EN, MB, false, COST_JG>(*a.cost, stp[kk], rec + (int64_t)kk * FR_REC, Lmodel + T_LO);
+    PMARK_D(9, cs);
     if (live) Lcs[(g * ROWS_PER_WAVE + i) * HC_MAX + k] = cs;
     // the stores before the count: the wave that completes the group reads every chunk's costs
     const int n = __builtin_amdgcn_readfirstlane(

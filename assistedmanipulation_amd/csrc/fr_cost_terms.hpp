@@ -104,11 +104,13 @@ __device__ __forceinline__ void kin_sums(const double2 *rec2, double *vl, double
         for (int i = 0; i < 10; i++) acc = __builtin_fma(S[m][i], qd[i], acc);
         vl[m] = acc;
     }
+    // (the base's three terms of J_a J_a^T are fma(x, 0, +0) = +0 on the rows' chains, store_ks: a
+    // chain that starts at body 3 from +0 has the same bits for finite S)
 #pragma unroll
     for (int p = 0; p < 6; p++) {
         double acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < 10; i++) acc = __builtin_fma(S[ja[p]][i], i < 3 ? 0.0 : S[jb[p]][i], acc);
+        for (int i = 3; i < 10; i++) acc = __builtin_fma(S[ja[p]][i], S[jb[p]][i], acc);
         jj[p] = acc;
     }
 }
@@ -129,24 +131,33 @@ __device__ __forceinline__ void derive_record(const double *rk, double *r, bool 
 
 // AssistedManipulation::get_cost at the record's state with its kinematics (KC: a compact record,
 // J v and J_a J_a^T stored; else the 768-B record, whose motion subspaces they are formed from)
-template <bool EN, int JS, bool KC = false>
+template <bool EN, int JS, bool KC = false, int JG = 1>
 __device__ __forceinline__ double assisted_manipulation_cost(const DevCost &Cs, const StepConst &sc, const double *r,
                                                              const double *Lj, const double2 *src)
 {
     double j0 = 0.0, j1 = 0.0, v0 = 0.0, v1 = 0.0;
     int off = 0;
+    // JG joints at a time: their parameters are read after the previous group's terms (left to
+    // itself the compiler hoisted all 84 LDS reads to the top: 168 registers live), and the group's
+    // barrier chains interleave (one joint at a time, each v_rcp_f64 waited a wait state for its
+    // reader: the trans forwarding hazard).  The sums add the joints in order either way.
 #pragma unroll
-    for (int j = 0; j < FR_NB; j++) {
-        // joint j's parameters are read after joint j - 1's terms: left to itself the compiler
-        // hoisted all 84 LDS reads to the top (168 registers live, two waves per SIMD)
+    for (int j = 0; j < FR_NB; j += JG) {
         asm volatile("" : "+v"(off) : "v"(j < 6 ? j0 : j1));
-        const double *P = Lj + off;
-        off += JS;
-        const double q = r[REC_QQD + 2 * j], vq = fabs(r[REC_QQD + 2 * j + 1]);
-        const double lj = left_barrier(P[0], P[1], P[2], q) + right_barrier(P[3], P[4], P[5], q);
-        const double lv = P[6] * (vq * vq);
-        if (j < 6) { j0 += lj; v0 += lv; }
-        else { j1 += lj; v1 += lv; }
+        double lj[JG], lv[JG];
+#pragma unroll
+        for (int u = 0; u < JG; u++) {
+            const double *P = Lj + off + u * JS;
+            const double q = r[REC_QQD + 2 * (j + u)], vq = fabs(r[REC_QQD + 2 * (j + u) + 1]);
+            lj[u] = left_barrier(P[0], P[1], P[2], q) + right_barrier(P[3], P[4], P[5], q);
+            lv[u] = P[6] * (vq * vq);
+        }
+        off += JG * JS;
+#pragma unroll
+        for (int u = 0; u < JG; u++) {
+            if (j + u < 6) { j0 += lj[u]; v0 += lv[u]; }
+            else { j1 += lj[u]; v1 += lv[u]; }
+        }
     }
     const double joint = j0 + j1, vel = v0 + v1;
     // the rest of the record (r holds the (q, qd) pairs only) is loaded through a pointer that
@@ -311,17 +322,17 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
 
 // gamma_k times the objective at step record r (AssistedManipulation: r holds the record's (q, qd)
 // pairs, the rest is read from the stored record src; TrackPoint: r holds the record up to REC_VL)
-template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false>
+template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false, int JG = 1>
 __device__ __forceinline__ double step_cost(const DevCost &Cs, const StepConst &sc, const double *r, const double *Lj,
                                            const double2 *src)
 {
     if constexpr (CK == CK_TRACK_POINT) return sc.gamma_k * track_point_cost(Cs, r, r[REC_QQD + 4]);
-    else return sc.gamma_k * assisted_manipulation_cost<EN, JS, KC>(Cs, sc, r, Lj, src);
+    else return sc.gamma_k * assisted_manipulation_cost<EN, JS, KC, JG>(Cs, sc, r, Lj, src);
 }
 
 // gamma_k times the objective at the stored step record rk (FR_REC doubles, or FR_REC_C with KC;
 // 16-byte aligned)
-template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false>
+template <int CK, bool EN, int JS = JT_STRIDE, bool KC = false, int JG = 1>
 __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const StepConst &sc, const double *rk, const double *Lj)
 {
     double r[FR_NREC];
@@ -333,7 +344,7 @@ __device__ __forceinline__ double record_step_cost(const DevCost &Cs, const Step
         r[2 * i] = v.x;
         r[2 * i + 1] = v.y;
     }
-    return step_cost<CK, EN, JS, KC>(Cs, sc, r, Lj, src);
+    return step_cost<CK, EN, JS, KC, JG>(Cs, sc, r, Lj, src);
 }
 
 // J of one rollout from its H stored step records (rollout-major, FR_REC doubles each, FR_REC_C with
