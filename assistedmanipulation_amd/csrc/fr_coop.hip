@@ -556,8 +556,9 @@ __device__ __forceinline__ void gj_rows(double *Mc, double &b, double f0, double
     double fa, fb, d, r0, e, q;
     uint64_t sx, mk;
     const uint64_t base = 0x0001000100010001ull;   // lane 0 of each 16-lane row
-    // s_nop 1: Mc / f0 / f1 (DPP operands) may be written right before the block
-    asm("s_nop 1\n\t"
+    // (no leading s_nop: tools/dpp_hazard_check.py checks every build that Mc / f0 / f1, DPP
+    // operands, were not written in the two instructions before the block)
+    asm(""
         "s_mov_b64 %19, exec\n\t"
         "s_lshl_b64 %20, %23, 2\n\t"
         /* pivot 0 */
@@ -1229,8 +1230,9 @@ __device__ __forceinline__ double coop_aba(int j, const double *Lk, double *Lw, 
 // FMAs plus nine zeroed accumulators; r05: 81 FMAs into the lanes' own values, nothing to zero.)
 __device__ __forceinline__ void composite_scan(double *v, const double *m)
 {
-    // s_nop 1: the lanes' own (h, Ib) may be written right before the block (DPP sources)
-    asm("s_nop 1\n\t"
+    // (no leading s_nop: tools/dpp_hazard_check.py checks every build that the lanes' own (h, Ib),
+    // the DPP sources, were not written in the two instructions before the block)
+    asm(""
         "v_fmac_f64_dpp %0, %0, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %1, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, %2, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n\t"

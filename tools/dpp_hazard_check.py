@@ -22,7 +22,8 @@ def regs(tok):
 def check(path, prefix="", strict=True):
     bad = 0
     inside = False
-    recent, trans = [], []   # (wait states since the write, registers)
+    recent, trans = [], []
+    in_asm, since_label = False, 2   # (wait states since the write, registers)
     for l in open(path):
         l = l.rstrip("\n")
         if not inside:
@@ -34,12 +35,23 @@ def check(path, prefix="", strict=True):
             inside = False
             continue
         s = l.strip()
+        if s == ";;#ASMSTART":
+            in_asm = True
+        elif s == ";;#ASMEND":
+            in_asm = False
         if not s or s.startswith((".", ";")) or s.endswith(":"):
             if s.endswith(":"):
                 recent, trans = [], []   # a branch target: the distance is only tracked in straight-line code
+                since_label = 0
             continue
         op = s.split()[0]
         ws = int(s.split()[1], 0) + 1 if op == "s_nop" else 1
+        # hand-written DPP within two wait states of a branch target: the writes before the label
+        # are not seen here (and LLVM cannot pad inside inline asm), so the distance is unverified
+        if in_asm and since_label < 2 and ("_dpp" in op or " row_" in s):
+            print("unverified (asm DPP at a block start): %s" % s)
+            bad += 1
+        since_label += ws
         if "_dpp" in op or " row_" in s or "quad_perm" in s:
             ops = s[len(op):].split(",")
             src0 = regs(ops[1]) if len(ops) > 1 else set()
