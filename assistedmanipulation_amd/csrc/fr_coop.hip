@@ -1777,6 +1777,30 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         E = EN ? (FROW && frow ? fE : lE) : 0.0;   // EnergyTank::set_energy(state.available_energy)
     }
     const double *grav = a.model->gravity;
+    // REGTAB: the body-table fields the step reads, held in registers across the loop instead of
+    // re-read from LDS every step (A/B: the loop's VGPR budget against sixteen ds_read2 per step)
+#ifdef REGTAB
+    double Mreg[T_IL + 1];
+    {
+        constexpr int idx[] = {REGTAB_IDX};
+#pragma unroll
+        for (int n = 0; n < (int)(sizeof(idx) / sizeof(idx[0])); n++) {
+            double v = M[idx[n]];
+            asm volatile("" : "+v"(v));
+            Mreg[idx[n]] = v;
+        }
+#pragma unroll
+        for (int n = 0; n <= T_IL; n++) {
+            bool in = false;
+#pragma unroll
+            for (int m = 0; m < (int)(sizeof(idx) / sizeof(idx[0])); m++) in = in || idx[m] == n;
+            if (!in) Mreg[n] = M[n];
+        }
+    }
+    const double *Mk = Mreg;
+#else
+    const double *Mk = M;
+#endif
     double sq, cq;
     const SinCosK scK = sincos_constants();
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
@@ -1813,7 +1837,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         qd = base_velocity(L, u, sq, cq, qd);
         if constexpr (EN)
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
-        coop_fk<CK, EN>(L, q, sq, cq, qd, M, Lk, kin, bd, grav);
+        coop_fk<CK, EN>(L, q, sq, cq, qd, Mk, Lk, kin, bd, grav);
         // the next record's kinematics (the one-step lag)
         if constexpr (KC) store_ks<CK, EN>(recp(k + 1), j, L, bd, qd, Lk);
         else store_kin<CK>(recp(k + 1), j, bd, qd);
