@@ -1327,7 +1327,11 @@ __device__ __forceinline__ void composite_scan(double *v, const double *m)
 __device__ __forceinline__ double base_velocity(const LaneConst &L, double u, double sq, double cq, double qd)
 {
     double P = 0.0, Q = 0.0, X, Y;
-    asm("v_fmac_f64_dpp %0, %5, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // P = c A
+    asm(
+#ifdef REGTAB
+        "s_nop 1\n\t"
+#endif
+        "v_fmac_f64_dpp %0, %5, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // P = c A
         "v_fmac_f64_dpp %1, %5, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"    // Q = c B
         "v_mul_f64 %2, %11, %6\n\t"                                                  // X = C u
         "v_mul_f64 %3, %12, %7\n\t"                                                  // Y = keep qd
