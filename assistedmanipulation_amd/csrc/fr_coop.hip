@@ -57,6 +57,9 @@ using mppi_dev::smin;
 // record stores.  (A volatile asm ends the scheduler's region: the marked build is a little slower.)
 // PMARK_D ties the marker to a value the next phase's inline-asm blocks consume or the previous
 // one's produce: non-volatile asm statements are otherwise free to move across a plain marker.
+#ifdef REGTAB
+#define COLUMN_DOTS_PAD "s_nop 1\n\t"
+#endif
 #ifdef PHASE_MARKS
 #define PMARK(n) asm volatile("; PHASE " #n)
 #define PMARK_D(n, x) asm volatile("; PHASE " #n : "+v"(x))
@@ -283,8 +286,11 @@ __device__ __forceinline__ void column_dots(const double *S, const double *F, do
 #pragma unroll
     for (int i = 2; i < 11; i++) m[i] = 0.0;
     // no leading s_nop: S (the DPP sources) was formed long before (tools/dpp_hazard_check.py
-    // checks every build's assembly)
-    asm(""
+    // checks every build's assembly; COLUMN_DOTS_PAD where a build puts an F write right before)
+#ifndef COLUMN_DOTS_PAD
+#define COLUMN_DOTS_PAD ""
+#endif
+    asm(COLUMN_DOTS_PAD
         "v_fmac_f64_dpp %0, %8, %14 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, %8, %14 row_newbcast:3 row_mask:0xf bank_mask:0xe\n\t"
         "v_fmac_f64_dpp %2, %8, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
