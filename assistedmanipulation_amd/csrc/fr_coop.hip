@@ -57,8 +57,12 @@ using mppi_dev::smin;
 // record stores.  (A volatile asm ends the scheduler's region: the marked build is a little slower.)
 // PMARK_D ties the marker to a value the next phase's inline-asm blocks consume or the previous
 // one's produce: non-volatile asm statements are otherwise free to move across a plain marker.
-#ifdef REGTAB
-#define COLUMN_DOTS_PAD "s_nop 1\n\t"
+// The body-table fields the step reads stay in registers across the horizon loop (REGTAB, round 6:
+// 789 -> 766 instructions per step, no LDS re-read of the table in every step); -DNO_REGTAB for A/B
+#ifndef NO_REGTAB
+#define REGTAB 1
+// (with it the compiler writes an F operand of column_dots right before the block: one wait state)
+#define COLUMN_DOTS_PAD "s_nop 0\n\t"
 #endif
 #ifdef PHASE_MARKS
 #define PMARK(n) asm volatile("; PHASE " #n)
@@ -1820,28 +1824,38 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
     const double *grav = a.model->gravity;
     // REGTAB: the body-table fields the step reads, held in registers across the loop instead of
     // re-read from LDS every step (A/B: the loop's VGPR budget against sixteen ds_read2 per step)
+    // the fields in REGTAB_MASK (bit n: field n) are loaded once, opaque, and stay in registers; the
+    // step's other fields are re-read from LDS in every step (tab_refresh).  Not in the energy-tank
+    // kernels, whose registers are spent already (their spills went 13 -> 33 with it).
 #ifdef REGTAB
+#ifndef REGTAB_MASK
+#define REGTAB_MASK 0xFFFFFFFFFFFFull
+#endif
+    constexpr bool RT = !EN;
+#else
+#define REGTAB_MASK 0ull
+    constexpr bool RT = false;
+#endif
+    constexpr uint64_t RT_USED = 0x1401FFFFFEDBull;   // fields the step reads (T_R cols 0, 1 .. T_NROT, T_FIX, T_IL)
     double Mreg[T_IL + 1];
-    {
-        constexpr int idx[] = {REGTAB_IDX};
-#pragma unroll
-        for (int n = 0; n < (int)(sizeof(idx) / sizeof(idx[0])); n++) {
-            double v = M[idx[n]];
-            asm volatile("" : "+v"(v));
-            Mreg[idx[n]] = v;
-        }
+    if constexpr (RT) {
 #pragma unroll
         for (int n = 0; n <= T_IL; n++) {
-            bool in = false;
-#pragma unroll
-            for (int m = 0; m < (int)(sizeof(idx) / sizeof(idx[0])); m++) in = in || idx[m] == n;
-            if (!in) Mreg[n] = M[n];
+            if ((RT_USED >> n) & (REGTAB_MASK >> n) & 1) {
+                double v = M[n];
+                asm volatile("" : "+v"(v));
+                Mreg[n] = v;
+            }
         }
     }
-    const double *Mk = Mreg;
-#else
-    const double *Mk = M;
-#endif
+    auto tab_refresh = [&]() {
+        if constexpr (RT) {
+#pragma unroll
+            for (int n = 0; n <= T_IL; n++)
+                if (((RT_USED >> n) & 1) && !((REGTAB_MASK >> n) & 1)) Mreg[n] = M[n];
+        }
+    };
+    const double *Mk = RT ? Mreg : M;
     double sq, cq;
     const SinCosK scK = sincos_constants();
     fsincos(q, &sq, &cq, scK);   // one sincos per lane and step: FK and base yaw
@@ -1878,6 +1892,7 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
         qd = base_velocity(L, u, sq, cq, qd);
         if constexpr (EN)
             Lw[L_TAU + j] = (j >= 3 && j < 10) ? u : 0.0;   // coop_aba's tau
+        tab_refresh();
         coop_fk<CK, EN>(L, q, sq, cq, qd, Mk, Lk, kin, bd, grav);
         // the next record's kinematics (the one-step lag)
         if constexpr (KC) store_ks<CK, EN>(recp(k + 1), j, L, bd, qd, Lk);
