@@ -966,9 +966,6 @@ struct LaneConst {
     double cmask[9];   // composite_scan: 1.0 when body j is the parent of step s's child (edges 11-9, 10-9, 9-8, .., 3-2)
     double mc;      // the mass of body j's subtree (composite inertia's mass, a constant)
     double inv_m0, inv_m1;   // 1 / composite mass of bodies 0 and 1: the base pivots (uniform)
-#ifdef FKREG
-    double fk[13];  // FKREG: coop_fk's body-table fields (T_R columns 0 and 1, T_P, T_MA, T_FIX) in registers
-#endif
     double f0, f1;  // gj_rows: pivot 0 / 1's factor per unit of M_j0 / M_j1 (-1 / m; 0 on lane 0 / 1)
     double qs;      // gj_rows: the solution's scale (1 / m on lanes 0 and 1, else 1)
 };
@@ -985,31 +982,15 @@ __device__ __forceinline__ void coop_fk(const LaneConst &L, double q, double sq,
     // delta form D = R - I (columns 0 and 1; the scan never reads the third): the diagonal's -1 is
     // the seed of its FMA chain
     double D[9], p[3];
-#ifdef FKREG
-    const double *fk = L.fk;
-#define FK_R(r, c) fk[2 * (r) + (c)]
-#define FK_P(r) fk[6 + (r)]
-#define FK_MA(r) fk[9 + (r)]
-#define FK_FIX fk[12]
-#else
-#define FK_R(r, c) M[T_R + 3 * (r) + (c)]
-#define FK_P(r) M[T_P + (r)]
-#define FK_MA(r) M[T_MA + (r)]
-#define FK_FIX M[T_FIX]
-#endif
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-        const double m0 = FK_R(r, 0), m1 = FK_R(r, 1);
+        const double m0 = M[T_R + 3 * r], m1 = M[T_R + 3 * r + 1];
         D[3 * r + 0] = r == 0 ? __builtin_fma(m0, cz, __builtin_fma(m1, sz, -1.0)) : m0 * cz + m1 * sz;
         D[3 * r + 1] = r == 1 ? __builtin_fma(m1, cz, __builtin_fma(-m0, sz, -1.0)) : m0 * (-sz) + m1 * cz;
         D[3 * r + 2] = 0.0;
-        p[r] = FK_P(r) + FK_MA(r) * q;
+        p[r] = M[T_P + r] + M[T_MA + r] * q;
     }
-    p[1] = p[1] + FK_FIX * qprev;
-#undef FK_R
-#undef FK_P
-#undef FK_MA
-#undef FK_FIX
+    p[1] = p[1] + M[T_FIX] * qprev;
     scan_level2<1>(D, p);
     scan_level2<2>(D, p);
     scan_level2<4>(D, p);
@@ -1727,18 +1708,6 @@ __device__ __forceinline__ int coop_rows(const FrRolloutArgs &a, int64_t lr, int
             L.cmask[e] = d;
         }
     }
-#ifdef FKREG
-    {
-        constexpr int idx[13] = {T_R + 0, T_R + 1, T_R + 3, T_R + 4, T_R + 6, T_R + 7, T_P, T_P + 1, T_P + 2,
-                                 T_MA, T_MA + 1, T_MA + 2, T_FIX};
-#pragma unroll
-        for (int n = 0; n < 13; n++) {
-            double v = M[idx[n]];
-            asm volatile("" : "+v"(v));   // kept in registers across the loop
-            L.fk[n] = v;
-        }
-    }
-#endif
     L.mc = M[T_MC];
     L.inv_m0 = 1.0 / Lmodel[0 * MB + T_MC];   // the base pivots' constant diagonals (gj_pivot_0 / 1)
     L.inv_m1 = 1.0 / Lmodel[1 * MB + T_MC];
