@@ -232,6 +232,16 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
     };
     // loaded here, stored to LDS after the eps batch: their loads travel with it
     const double us_t = t < HC ? us_at(t) : 0.0, gm_t = t < H ? a.steps[t].gamma_k : 0.0;
+    // the finisher's operands of its first output (U* as published, the bounds), loaded with the
+    // batch: behind the partial sums its publish then waits on no load (they were a memory trip of
+    // the finisher's "stored" phase)
+    const bool cb = t < HC && a.control_bound;
+    const double uo_t = t < HC ? a.U[t] : 0.0, hi_t = cb ? a.cmax[t % PC] : 0.0, lo_t = cb ? a.cmin[t % PC] : 0.0;
+    const double x0_t = t < a.X ? a.x0v[t] : 0.0;   // (its x0_opt copy)
+    // and its scalar arguments into the constant cache now: loaded first behind the sums, each missed
+    // it and their waits made a chain of scalar round trips there
+    asm volatile("" : : "s"(a.U), "s"(a.Us), "s"(a.gradient), "s"(a.out), "s"(a.x0_opt), "s"(a.seq), "s"(a.gradient_step),
+                 "s"(a.control_bound), "s"(a.status), "s"(a.stats));
     if (t == 0) s_last = 0;
     auto items = [&](int k0) {
         // both candidate sources of each item (the previous eps shifted, the draw made ahead or -U*)
@@ -438,22 +448,29 @@ __global__ __launch_bounds__(PT) void pm_update_kernel(PmFusedArgs a)
         // output's gradient sum: two independent chains, each in block order
         double total = 0.0, g0 = 0.0;
         if (upd) sum2_in_order(Lst + G, 1, Lst + min(t, HC - 1), HC, nb, total, g0);
-        for (int o = t; o < HC; o += PT) {   // finish (mppi.cpp:421-447) and publish (178-182)
-            const int c = o % PC;
+        // finish (mppi.cpp:421-447) and publish (178-182) of output o: gsum = sum_r e_r eps_r, uo = U*
+        // as published, [lo, hi] its bounds
+        auto finish = [&](int o, double gsum, double uo, double hi, double lo) {
             double u = Lus[o];
             if (upd) {
-                const double gs = (o == t ? g0 : sum_in_order(Lst + o, nb, HC)) / total;   // sum_r e_r eps_r / sum_r e_r
+                const double gs = gsum / total;   // sum_r e_r eps_r / sum_r e_r
                 a.gradient[o] = gs;
                 u += gs * a.gradient_step;
-                if (a.control_bound) u = smax(smin(u, a.cmax[c]), a.cmin[c]);
+                if (a.control_bound) u = smax(smin(u, hi), lo);
             }
             Lus[o] = u;
             if (upd || P.shift_by > 0) a.Us[o] = u;   // U*_shifted as sample() and the step leave it
-            const double v = ok ? u : a.U[o];
+            const double v = ok ? u : uo;
             if (ok) a.U[o] = v;
             pub(a.out + o, v);
+        };
+        if (t < HC) finish(t, g0, uo_t, hi_t, lo_t);
+        for (int o = t + PT; o < HC; o += PT) {   // H C > PT: the rest, loaded here
+            const int c = o % PC;
+            finish(o, upd ? sum_in_order(Lst + o, nb, HC) : 0.0, a.U[o], a.control_bound ? a.cmax[c] : 0.0,
+                   a.control_bound ? a.cmin[c] : 0.0);
         }
-        if (t < a.X) a.x0_opt[t] = a.x0v[t];
+        if (t < a.X) a.x0_opt[t] = x0_t;
         if (t == 0) {
             st->all_nan = all_nan;
             st->early = early;
