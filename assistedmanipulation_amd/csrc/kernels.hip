@@ -932,41 +932,37 @@ __global__ __launch_bounds__(256) void finish_kernel(FinishArgs a)
     publish_block(a);
 }
 
-// finish() without the Savitzky-Golay filter, one U* element per thread: every load is issued
-// before the first store, so the block makes one dependent memory trip where finish_block makes
-// five (gradient splits, U*_shifted, the bounds, U*, then the host block).
+// finish() without the Savitzky-Golay filter, one U* element per thread.  Every load of the block's
+// first (at H C <= 1024 its only) output is issued in one batch with the status words, the wait
+// count, the optimal cost and the state, before anything waits: the block makes one dependent
+// memory trip behind its arguments where finish_block makes five (gradient splits, U*_shifted, the
+// bounds, U*, then the host block).  (Round 6: the wait count's source and thread 0's optimal cost
+// behind branches, and the outputs' loads inside the loop behind the normaliser's sum, had made it
+// four scalar round trips before the partials were requested.)
 __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
 {
-    const int HC = a.H * a.C;
-    const Status stt = *a.status;   // the status words, the normaliser partials, min / max: one batch
-    const int wt = a.wait_all ? (int)*a.wait_all : stt.wait_timeouts;   // update_wait_timeouts
-    const bool upd = !stt.early && !wt, ok = !stt.all_nan && !wt;   // no filter: no SG error
-    const double oc = threadIdx.x == 0 ? *a.opt_cost : 0.0;
-    const double x0 = (int)threadIdx.x < a.X ? a.x0[threadIdx.x] : 0.0;
+    const int HC = a.H * a.C, t0 = threadIdx.x;
     const int nsp = a.ns > 0 ? a.ns : 1;
     const double *__restrict__ gs = a.ns > 0 ? a.gsplit : a.gpart;
     double *__restrict__ Us = a.Ushift;
     double *__restrict__ U = a.U;
+    const bool split8 = nsp == GRAD_SPLIT;   // the usual split: its partials loaded together, added in order
+    const int tf = t0 < HC ? t0 : 0;
+    const int cf = tf % a.C;
+    double pf[GRAD_SPLIT];
+#pragma unroll
+    for (int i = 0; i < GRAD_SPLIT; i++) pf[i] = gs[(int64_t)(split8 ? i : 0) * HC + tf];
+    const double uf = Us[tf], uof = U[tf], hif = a.cmax[cf], lof = a.cmin[cf];
+    const Status stt = *a.status;   // the status words, the normaliser partials, min / max
+    const double wa = *(a.wait_all ? a.wait_all : a.opt_cost);   // (a select of sources, not a branch)
+    const double oc = *a.opt_cost;
+    const double x0 = t0 < a.X ? a.x0[t0] : 0.0;
+    const int wt = a.wait_all ? (int)wa : stt.wait_timeouts;   // update_wait_timeouts
+    const bool upd = !stt.early && !wt, ok = !stt.all_nan && !wt;   // no filter: no SG error
     double total = stt.tsplit[0];   // softmin_total
 #pragma unroll
     for (int i = 1; i < GRAD_SPLIT; i++) total += stt.tsplit[i];
-    for (int t = threadIdx.x; t < HC; t += blockDim.x) {
-        const int c = t % a.C;
-        double u = Us[t];   // loaded first: with the partials in one trip
-        const double uo = U[t];
-        const double hi = a.control_bound ? a.cmax[c] : 0.0, lo = a.control_bound ? a.cmin[c] : 0.0;
-        double g;
-        if (nsp == GRAD_SPLIT) {   // the usual split: its partials loaded together, added in order
-            double p[GRAD_SPLIT];
-#pragma unroll
-            for (int i = 0; i < GRAD_SPLIT; i++) p[i] = gs[(int64_t)i * HC + t];
-            g = p[0];
-#pragma unroll
-            for (int i = 1; i < GRAD_SPLIT; i++) g += p[i];
-        } else {
-            g = gs[t];
-            for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
-        }
+    auto finish = [&](int t, double g, double u, double uo, double hi, double lo) {
         g /= total;   // sum_r e_r eps_r / sum_r e_r
         if (upd) {
             a.gradient[t] = g;
@@ -980,6 +976,26 @@ __global__ __launch_bounds__(1024) void finish_flat_kernel(FinishArgs a)
         const double v = ok ? u : uo;
         if (ok) U[t] = v;
         pub(a.out + t, v);
+    };
+    auto partials = [&](int t) {   // another split count, or outputs past the first: loaded here
+        double g = gs[t];
+        for (int i = 1; i < nsp; i++) g += gs[(int64_t)i * HC + t];
+        return g;
+    };
+    if (t0 < HC) {
+        double g;
+        if (split8) {
+            g = pf[0];
+#pragma unroll
+            for (int i = 1; i < GRAD_SPLIT; i++) g += pf[i];
+        } else {
+            g = partials(t0);
+        }
+        finish(t0, g, uf, uof, hif, lof);
+    }
+    for (int t = t0 + (int)blockDim.x; t < HC; t += blockDim.x) {
+        const int c = t % a.C;
+        finish(t, partials(t), Us[t], U[t], a.cmax[c], a.cmin[c]);
     }
     if ((int)threadIdx.x < a.X) a.x0_opt[threadIdx.x] = x0;
     for (int64_t i = threadIdx.x; i < a.rank_n; i += blockDim.x) a.rank_zero[i] = 0;   // for rank_tiled_kernel
