@@ -60,7 +60,7 @@ EV_EVERY = 8   # timed updates per rollout-kernel event sample
 EV_GRAPH = 16  # --graph 1: eager updates after the timed loop whose rollout launches are timed
 PMC_JSON = os.path.join(HERE, "profiles", "r06", "final", "pmc_rollout.json")
 PMC_WG_JSON = os.path.join(HERE, "profiles", "r06", "final", "pmc_weights.json")   # weights_gradient_kernel's traffic
-PMC_PM_JSON = os.path.join(HERE, "profiles", "r05", "final", "pmc_pm.json")      # pm_update_kernel's traffic
+PMC_PM_JSON = os.path.join(HERE, "profiles", "r06", "final", "pmc_pm.json")      # pm_update_kernel's traffic
 
 
 def recorded_label(path):
