@@ -121,7 +121,7 @@ def test_folded_filter_cost_against_oracle():
         x = x + 0.01
 
 
-@pytest.mark.parametrize("S,horison,fused", [(256, 3.0, 0), (1024, 1.28, 0), (2046, 0.64, 1)])
+@pytest.mark.parametrize("S,horison,fused", [(256, 3.0, 0), (1024, 1.28, 0), (2046, 0.64, 1), (256, 1.0, 1)])
 def test_fused_update_long_horizon_against_oracle(S, horison, fused):
     """The shared point-mass step (pm_model.hpp) associates differently from the oracle:
     the state cost as fma(q2, e2, fma(q1, e1, q0 e0)) and the control cost likewise against the
@@ -130,7 +130,8 @@ def test_fused_update_long_horizon_against_oracle(S, horison, fused):
     through the oracle still meet the parity bars of tests/helpers.py; the measured worst errors
     are printed.  At 300 and 128 steps the fused launch's LDS staging does not fit
     (pm_fused_rows), so those handles run the five launches - the same pm_model.hpp step, bit for
-    bit the fused costs (test_fused_update_equals_five_launches); 2046 x 64 runs the fused launch."""
+    bit the fused costs (test_fused_update_equals_five_launches); 2046 x 64 runs the fused launch, and
+    256 x 100 the fused launch with more outputs (H C = 300) than the finisher has threads."""
     conf, dev = _pm(S, horison)
     cc, keep = conf.to_c()
     orc = O.OracleTrajectory(cc, dev.dynamics.descriptor(), dev.cost.descriptor())
